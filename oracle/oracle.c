@@ -1,0 +1,413 @@
+/*
+ * oracle.c — CPU restatement of the reference hot path. TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Written for clarity, not speed: full 64-bit ntHash state (the product kernels use only the
+ * 33-bit lane), sorted pair arrays + binary search for the index, qsort-based counting.
+ * Every function cites the reference file:line it restates.
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- ntHash (third party, bcgsc ntHash >= 2.3) ----------------------------------------- */
+uint64_t orc_seed(unsigned char c) {
+    switch (c) {
+    case 'A': case 'a': return 0x3c8bfbb395c60474ULL;
+    case 'C': case 'c': return 0x3193c18562a02b4cULL;
+    case 'G': case 'g': return 0x20323ed082572324ULL;
+    case 'T': case 't': case 'U': case 'u': return 0x295549f54be24456ULL;
+    default: return 0; /* SEED_N: base is skipped */
+    }
+}
+
+uint64_t orc_srol(uint64_t x) {
+    uint64_t wrap = ((x & 0x8000000000000000ULL) >> 30) | ((x & 0x100000000ULL) >> 32);
+    return ((x << 1) & 0xFFFFFFFDFFFFFFFFULL) | wrap;
+}
+
+static uint64_t srol_n(uint64_t x, unsigned d) {
+    while (d--) x = orc_srol(x);
+    return x;
+}
+
+/* NtHash(seq, 1, k) then `while (roll()) get_forward_hash()` as called at src/sketch.cpp:31-33
+ * and src/kmer.cpp:26-30. init() skips past the last invalid base of the window; roll() with an
+ * invalid incoming base jumps pos += k and re-inits. */
+size_t orc_nthash_fwd(const char* seq, size_t len, unsigned k, uint64_t* out_hash, size_t* out_pos) {
+    if (k == 0 || len < k) return (size_t)-1;
+    size_t pos = 0, n = 0;
+    int initialized = 0;
+    uint64_t fwd = 0;
+    for (;;) {
+        int need_init = !initialized;
+        if (initialized) {
+            if (pos >= len - k) break;
+            if (orc_seed((unsigned char)seq[pos + k]) == 0) {
+                pos += k;
+                need_init = 1;
+            } else {
+                fwd = orc_srol(fwd) ^ orc_seed((unsigned char)seq[pos + k]) ^
+                      srol_n(orc_seed((unsigned char)seq[pos]), k);
+                ++pos;
+            }
+        }
+        if (need_init) {
+            for (;;) {
+                if (pos > len - k) break;
+                long bad = -1;
+                for (long i = (long)k - 1; i >= 0; --i)
+                    if (orc_seed((unsigned char)seq[pos + i]) == 0) { bad = i; break; }
+                if (bad < 0) break;
+                pos += (size_t)bad + 1;
+            }
+            if (pos > len - k) break;
+            fwd = 0;
+            for (unsigned i = 0; i < k; ++i) fwd = orc_srol(fwd) ^ orc_seed((unsigned char)seq[pos + i]);
+            initialized = 1;
+        }
+        if (out_hash) out_hash[n] = fwd;
+        if (out_pos) out_pos[n] = pos;
+        ++n;
+    }
+    return n;
+}
+
+/* src/sketch.cpp:25-26 — the caller passes (double)0.05f from src/main.cpp:43,110 */
+uint32_t orc_threshold(double fraction) {
+    const uint32_t H = 0xFFFFFFFFu;
+    return (uint32_t)(H * fraction);
+}
+
+/* src/data_io.cpp:17-34 */
+int orc_is_valid_sequence(const char* seq, size_t len) {
+    for (size_t i = 0; i < len; ++i) {
+        char c = seq[i];
+        if (c != 'A' && c != 'T' && c != 'C' && c != 'G') return 0;
+    }
+    return 1;
+}
+
+static int cmp_u32(const void* a, const void* b) {
+    uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+static size_t sort_unique_u32(uint32_t* v, size_t n) {
+    if (n == 0) return 0;
+    qsort(v, n, sizeof(uint32_t), cmp_u32);
+    size_t m = 1;
+    for (size_t i = 1; i < n; ++i)
+        if (v[i] != v[m - 1]) v[m++] = v[i];
+    return m;
+}
+
+static size_t hashes_filtered(const char* seq, size_t len, unsigned k, uint64_t thr, uint32_t* out) {
+    if (k == 0 || len < k) return (size_t)-1;
+    uint64_t* h = (uint64_t*)malloc(sizeof(uint64_t) * (len - k + 1));
+    size_t n = orc_nthash_fwd(seq, len, k, h, NULL), m = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t v = (uint32_t)h[i]; /* uint32_t hash_value = nth.get_forward_hash(); */
+        if ((uint64_t)v <= thr) out[m++] = v;
+    }
+    free(h);
+    return sort_unique_u32(out, m);
+}
+
+/* src/sketch.cpp:24-39 */
+size_t orc_sketch(const char* seq, size_t len, unsigned k, uint32_t threshold, uint32_t* out) {
+    return hashes_filtered(seq, len, k, threshold, out);
+}
+
+/* src/kmer.cpp:19-35 */
+size_t orc_all_hashes(const char* seq, size_t len, unsigned k, uint32_t* out) {
+    return hashes_filtered(seq, len, k, 0xFFFFFFFFull, out);
+}
+
+/* ---- inverted index (src/sketch.cpp:51-74) --------------------------------------------- */
+typedef struct { uint32_t hash, tid; } pair_t;
+
+struct orc_index {
+    unsigned nk;
+    unsigned ks[64];
+    uint32_t ntx;
+    uint64_t npairs[64];
+    pair_t* pairs[64]; /* sorted by (hash, tid), unique */
+    uint64_t nkeys[64];
+};
+
+static int cmp_pair(const void* a, const void* b) {
+    const pair_t* x = (const pair_t*)a;
+    const pair_t* y = (const pair_t*)b;
+    if (x->hash != y->hash) return x->hash < y->hash ? -1 : 1;
+    return x->tid < y->tid ? -1 : x->tid > y->tid;
+}
+
+static void finalize_k(orc_index* ix, unsigned i) {
+    pair_t* p = ix->pairs[i];
+    uint64_t n = ix->npairs[i];
+    if (n) qsort(p, n, sizeof(pair_t), cmp_pair);
+    uint64_t m = 0, keys = 0;
+    for (uint64_t j = 0; j < n; ++j) {
+        if (m && p[m - 1].hash == p[j].hash && p[m - 1].tid == p[j].tid) continue;
+        if (!m || p[m - 1].hash != p[j].hash) ++keys;
+        p[m++] = p[j];
+    }
+    ix->npairs[i] = m;
+    ix->nkeys[i] = keys;
+}
+
+orc_index* orc_index_build(unsigned nk, const unsigned* ks, uint32_t ntx, const char* seqs,
+                           const uint64_t* offs, uint32_t threshold) {
+    if (nk == 0 || nk > 64) return NULL;
+    orc_index* ix = (orc_index*)calloc(1, sizeof(orc_index));
+    ix->nk = nk;
+    ix->ntx = ntx;
+    memcpy(ix->ks, ks, nk * sizeof(unsigned));
+    uint64_t cap[64];
+    for (unsigned i = 0; i < nk; ++i) {
+        cap[i] = 1024;
+        ix->pairs[i] = (pair_t*)malloc(cap[i] * sizeof(pair_t));
+    }
+    uint64_t maxlen = 0;
+    for (uint32_t t = 0; t < ntx; ++t)
+        if (offs[t + 1] - offs[t] > maxlen) maxlen = offs[t + 1] - offs[t];
+    uint32_t* buf = (uint32_t*)malloc(sizeof(uint32_t) * (maxlen + 1));
+    for (uint32_t t = 0; t < ntx; ++t) {
+        const char* s = seqs + offs[t];
+        size_t len = offs[t + 1] - offs[t];
+        int ok = 1; /* src/main.cpp:66-75: skip if shorter than any k */
+        for (unsigned i = 0; i < nk; ++i)
+            if (len < ks[i]) ok = 0;
+        if (!ok) continue;
+        for (unsigned i = 0; i < nk; ++i) { /* src/main.cpp:78-80 */
+            size_t m = orc_sketch(s, len, ks[i], threshold, buf);
+            if (ix->npairs[i] + m > cap[i]) {
+                while (ix->npairs[i] + m > cap[i]) cap[i] *= 2;
+                ix->pairs[i] = (pair_t*)realloc(ix->pairs[i], cap[i] * sizeof(pair_t));
+            }
+            for (size_t j = 0; j < m; ++j) {
+                ix->pairs[i][ix->npairs[i]].hash = buf[j];
+                ix->pairs[i][ix->npairs[i]].tid = t;
+                ix->npairs[i]++;
+            }
+        }
+    }
+    free(buf);
+    for (unsigned i = 0; i < nk; ++i) finalize_k(ix, i);
+    return ix;
+}
+
+orc_index* orc_index_from_pairs(unsigned nk, const unsigned* ks, uint32_t ntx,
+                                const uint64_t* npairs, const uint32_t* const* hashes,
+                                const uint32_t* const* tids) {
+    if (nk == 0 || nk > 64) return NULL;
+    orc_index* ix = (orc_index*)calloc(1, sizeof(orc_index));
+    ix->nk = nk;
+    ix->ntx = ntx;
+    memcpy(ix->ks, ks, nk * sizeof(unsigned));
+    for (unsigned i = 0; i < nk; ++i) {
+        ix->npairs[i] = npairs[i];
+        ix->pairs[i] = (pair_t*)malloc((npairs[i] + 1) * sizeof(pair_t));
+        for (uint64_t j = 0; j < npairs[i]; ++j) {
+            ix->pairs[i][j].hash = hashes[i][j];
+            ix->pairs[i][j].tid = tids[i][j];
+        }
+        finalize_k(ix, i);
+    }
+    return ix;
+}
+
+void orc_index_free(orc_index* ix) {
+    if (!ix) return;
+    for (unsigned i = 0; i < ix->nk; ++i) free(ix->pairs[i]);
+    free(ix);
+}
+
+uint64_t orc_index_nkeys(const orc_index* ix, unsigned i) { return ix->nkeys[i]; }
+uint64_t orc_index_npost(const orc_index* ix, unsigned i) { return ix->npairs[i]; }
+
+void orc_index_export(const orc_index* ix, unsigned i, uint32_t* keys, uint64_t* offs, uint32_t* tids) {
+    uint64_t kk = 0;
+    const pair_t* p = ix->pairs[i];
+    for (uint64_t j = 0; j < ix->npairs[i]; ++j) {
+        if (j == 0 || p[j].hash != p[j - 1].hash) {
+            keys[kk] = p[j].hash;
+            offs[kk] = j;
+            ++kk;
+        }
+        tids[j] = p[j].tid;
+    }
+    offs[kk] = ix->npairs[i];
+}
+
+/* first pair with hash >= h */
+static uint64_t lower_bound(const pair_t* p, uint64_t n, uint32_t h) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) / 2;
+        if (p[mid].hash < h) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+/* ---- sparse_chain for one read (src/sparse_chaining.cpp:42-111) ------------------------ */
+typedef struct { uint32_t tid, ki; } hit_t;
+
+static int cmp_hit(const void* a, const void* b) {
+    const hit_t* x = (const hit_t*)a;
+    const hit_t* y = (const hit_t*)b;
+    if (x->tid != y->tid) return x->tid < y->tid ? -1 : 1;
+    return x->ki < y->ki ? -1 : x->ki > y->ki;
+}
+
+typedef struct { uint32_t tid, score; } cand_t;
+
+static int cmp_cand(const void* a, const void* b) {
+    const cand_t* x = (const cand_t*)a;
+    const cand_t* y = (const cand_t*)b;
+    if (x->score != y->score) return x->score > y->score ? -1 : 1; /* :108-109 score desc */
+    return x->tid < y->tid ? -1 : x->tid > y->tid;               /* normalised tie order */
+}
+
+/* `nq` k-lengths are the read's kmer_lengths list (in quant: the index's list, src/main.cpp:178),
+ * index slot qi corresponds to ix->ks[qi]. */
+static size_t chain_core(const orc_index* ix, const uint32_t* const* hashes, const uint32_t* nh,
+                         const int* present, double fraction, uint32_t* out_tid,
+                         uint32_t* out_score, size_t cap) {
+    const unsigned nq = ix->nk;
+    size_t nhits = 0;
+    for (unsigned i = 0; i < nq; ++i) {
+        if (!present[i]) continue;
+        for (uint32_t j = 0; j < nh[i]; ++j) {
+            const pair_t* p = ix->pairs[i];
+            uint64_t a = lower_bound(p, ix->npairs[i], hashes[i][j]);
+            while (a < ix->npairs[i] && p[a].hash == hashes[i][j]) { ++nhits; ++a; }
+        }
+    }
+    hit_t* hits = (hit_t*)malloc(sizeof(hit_t) * (nhits + 1));
+    size_t h = 0;
+    for (unsigned i = 0; i < nq; ++i) { /* :48-73 count matches per (transcript, k) */
+        if (!present[i]) continue;
+        for (uint32_t j = 0; j < nh[i]; ++j) {
+            const pair_t* p = ix->pairs[i];
+            uint64_t a = lower_bound(p, ix->npairs[i], hashes[i][j]);
+            for (; a < ix->npairs[i] && p[a].hash == hashes[i][j]; ++a) {
+                hits[h].tid = p[a].tid;
+                hits[h].ki = i;
+                ++h;
+            }
+        }
+    }
+    if (h) qsort(hits, h, sizeof(hit_t), cmp_hit);
+    /* distinct transcripts with their count vectors */
+    size_t ndist = 0;
+    for (size_t a = 0; a < h; ++a)
+        if (a == 0 || hits[a].tid != hits[a - 1].tid) ++ndist;
+    uint32_t* ctid = (uint32_t*)malloc(sizeof(uint32_t) * (ndist + 1));
+    int* cnt = (int*)calloc((ndist + 1) * nq, sizeof(int));
+    size_t d = 0;
+    for (size_t a = 0; a < h; ++a) {
+        if (a == 0 || hits[a].tid != hits[a - 1].tid) ctid[d++] = hits[a].tid;
+        cnt[(d - 1) * nq + hits[a].ki]++;
+    }
+    int maxc[64] = {0}; /* :76-82 */
+    for (size_t t = 0; t < ndist; ++t)
+        for (unsigned i = 0; i < nq; ++i)
+            if (cnt[t * nq + i] > maxc[i]) maxc[i] = cnt[t * nq + i];
+    double thr[64]; /* :84-87 */
+    for (unsigned i = 0; i < nq; ++i) thr[i] = fraction * maxc[i];
+    cand_t* cands = (cand_t*)malloc(sizeof(cand_t) * (ndist + 1));
+    size_t nc = 0;
+    for (size_t t = 0; t < ndist; ++t) { /* :89-105 */
+        int meets = 1, score = 0;
+        for (unsigned i = 0; i < nq; ++i) {
+            if (cnt[t * nq + i] < thr[i]) { meets = 0; break; }
+            score += cnt[t * nq + i];
+        }
+        if (meets) { cands[nc].tid = ctid[t]; cands[nc].score = (uint32_t)score; ++nc; }
+    }
+    if (nc) qsort(cands, nc, sizeof(cand_t), cmp_cand);
+    size_t ret = nc;
+    if (nc > cap) ret = (size_t)-1;
+    else
+        for (size_t c = 0; c < nc; ++c) { out_tid[c] = cands[c].tid; out_score[c] = cands[c].score; }
+    free(hits);
+    free(ctid);
+    free(cnt);
+    free(cands);
+    return ret;
+}
+
+size_t orc_chain_read(const orc_index* ix, const uint32_t* const* hashes, const uint32_t* nh,
+                      const int* present, double fraction, uint32_t* out_tid,
+                      uint32_t* out_score, size_t cap) {
+    return chain_core(ix, hashes, nh, present, fraction, out_tid, out_score, cap);
+}
+
+/* ---- batch: process_fastq_single_pass filters (src/main.cpp:132-144) + sparse_chain ----- */
+static int map_one(const orc_index* ix, const uint8_t* s, size_t len, uint32_t threshold,
+                   double fraction, uint8_t* status, uint32_t* hcnt, uint32_t* hout, uint32_t hcap,
+                   uint32_t* ccnt, uint32_t* ctid, uint32_t* cscore, uint32_t ccap, uint32_t* scratch) {
+    unsigned maxk = 0;
+    for (unsigned i = 0; i < ix->nk; ++i)
+        if (ix->ks[i] > maxk) maxk = ix->ks[i];
+    for (unsigned i = 0; i < ix->nk; ++i) hcnt[i] = 0;
+    *ccnt = 0;
+    if (!orc_is_valid_sequence((const char*)s, len)) { *status = ORC_INVALID; return 0; }
+    if (len < maxk) { *status = ORC_SHORT; return 0; }
+    *status = ORC_OK;
+    const uint32_t* hp[64];
+    int present[64];
+    for (unsigned i = 0; i < ix->nk; ++i) {
+        uint32_t* dst = scratch + (size_t)i * (len + 1);
+        size_t m = orc_sketch((const char*)s, len, ix->ks[i], threshold, dst);
+        if (hout && m > hcap) return -1;
+        hcnt[i] = (uint32_t)m;
+        if (hout) memcpy(hout + (size_t)i * hcap, dst, m * sizeof(uint32_t));
+        hp[i] = dst;
+        present[i] = 1;
+    }
+    size_t nc = chain_core(ix, hp, hcnt, present, fraction, ctid, cscore, ccap);
+    if (nc == (size_t)-1) return -1;
+    *ccnt = (uint32_t)nc;
+    return 0;
+}
+
+int orc_map_batch(const orc_index* ix, const uint8_t* reads, const uint64_t* offs, uint64_t n,
+                  uint32_t threshold, double fraction, uint8_t* status, uint32_t* hash_cnt,
+                  uint32_t* hashes, uint32_t hcap, uint32_t* cand_cnt, uint32_t* cand_tid,
+                  uint32_t* cand_score, uint32_t ccap) {
+    uint64_t maxlen = 0;
+    for (uint64_t r = 0; r < n; ++r)
+        if (offs[r + 1] - offs[r] > maxlen) maxlen = offs[r + 1] - offs[r];
+    uint32_t* scratch = (uint32_t*)malloc(sizeof(uint32_t) * (maxlen + 1) * ix->nk + 4);
+    int rc = 0;
+    for (uint64_t r = 0; r < n && rc == 0; ++r)
+        rc = map_one(ix, reads + offs[r], offs[r + 1] - offs[r], threshold, fraction, status + r,
+                     hash_cnt + r * ix->nk, hashes + r * ix->nk * hcap, hcap, cand_cnt + r,
+                     cand_tid + r * ccap, cand_score + r * ccap, ccap, scratch);
+    free(scratch);
+    return rc;
+}
+
+uint64_t orc_map_batch_count(const orc_index* ix, const uint8_t* reads, const uint64_t* offs,
+                             uint64_t n, uint32_t threshold, double fraction) {
+    uint64_t maxlen = 0, total = 0;
+    for (uint64_t r = 0; r < n; ++r)
+        if (offs[r + 1] - offs[r] > maxlen) maxlen = offs[r + 1] - offs[r];
+    uint32_t* scratch = (uint32_t*)malloc(sizeof(uint32_t) * (maxlen + 1) * ix->nk + 4);
+    uint32_t hcnt[64], ccnt;
+    uint32_t* ctid = (uint32_t*)malloc(sizeof(uint32_t) * (ix->ntx + 1));
+    uint32_t* csc = (uint32_t*)malloc(sizeof(uint32_t) * (ix->ntx + 1));
+    uint8_t st;
+    for (uint64_t r = 0; r < n; ++r) {
+        map_one(ix, reads + offs[r], offs[r + 1] - offs[r], threshold, fraction, &st, hcnt, NULL,
+                0, &ccnt, ctid, csc, ix->ntx + 1, scratch);
+        total += ccnt;
+    }
+    free(scratch);
+    free(ctid);
+    free(csc);
+    return total;
+}

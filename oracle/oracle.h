@@ -1,0 +1,100 @@
+/*
+ * oracle.h — CPU restatement of the reference hot path. TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ * and only as the checker / CPU baseline. The product (libskq.so, the skq CLI) never links it.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - the rolling hash is pinned by ntHash's own constant tables, read as data from the
+ *     reference's prebuilt binary (tests/golden/nthash_tables.json) and by the known-answer
+ *     vectors of SURVEY.md §8c;
+ *   - sketch/threshold/chain/record semantics are restated from the reference source text and
+ *     pinned end-to-end only by the edge-case fixture of SURVEY.md §8c (tests/golden/edge/).
+ *   The reference itself is unbuildable here (it needs the absent third-party ntHash library).
+ *
+ * Third-party algorithm restated: bcgsc ntHash >= 2.3 (not vendored in the reference, version
+ * not pinned by its build; identified from symbols in build/test):
+ *   fwd(s_0..s_{k-1}) = XOR_i srol^{k-1-i}(SEED[s_i]) on 64 bits, with the split rotate
+ *   srol(x) = ((x << 1) & ~(1<<33)) | (bit63 -> bit33) | (bit32 -> bit0); windows containing a
+ *   base whose seed is 0 (N and anything outside ACGTUacgtu) are skipped.
+ */
+#ifndef SKQ_ORACLE_H
+#define SKQ_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ntHash 64-bit seed of byte c (0 = invalid). */
+uint64_t orc_seed(unsigned char c);
+/* one split-rotate step of ntHash (srol). */
+uint64_t orc_srol(uint64_t x);
+
+/* ntHash NtHash(seq, 1, k) + roll()/get_forward_hash() loop: writes the 64-bit forward hash and
+ * the window start of every window free of invalid bases, in order. Returns the count, or
+ * (size_t)-1 for the argument errors ntHash rejects (k == 0 or len < k). */
+size_t orc_nthash_fwd(const char* seq, size_t len, unsigned k, uint64_t* out_hash, size_t* out_pos);
+
+/* (uint32_t)(UINT32_MAX * fraction) — src/sketch.cpp:25-26 */
+uint32_t orc_threshold(double fraction);
+
+/* is_valid_sequence — src/data_io.cpp:17-34: only uppercase A, C, G, T. Empty is valid. */
+int orc_is_valid_sequence(const char* seq, size_t len);
+
+/* createSketch_FracMinhash_direct — src/sketch.cpp:24-39. Writes the retained hash SET in
+ * ascending order (the reference's unordered_set has no order). out needs len-k+1 slots.
+ * Returns the count or (size_t)-1 on len < k. */
+size_t orc_sketch(const char* seq, size_t len, unsigned k, uint32_t threshold, uint32_t* out);
+
+/* extract_and_hash_kmers_nthash — src/kmer.cpp:19-35 (no threshold). Same output contract. */
+size_t orc_all_hashes(const char* seq, size_t len, unsigned k, uint32_t* out);
+
+/* ---- inverted index: build_kmer_to_transcript_map (src/sketch.cpp:51-74) ----------------- */
+typedef struct orc_index orc_index;
+
+/* Builds the oracle index from transcript sequences (concatenated bytes + offsets, tids are
+ * positions 0..ntx-1). Restates build_and_save_index (src/main.cpp:66-85): a transcript
+ * shorter than ANY k is skipped entirely; every other transcript is sketched at every k. */
+orc_index* orc_index_build(unsigned nk, const unsigned* ks, uint32_t ntx, const char* seqs,
+                           const uint64_t* offs, uint32_t threshold);
+/* Builds from explicit postings: per k, npairs (hash, tid) pairs (any order, duplicates of a
+ * (hash, tid) pair are removed since sketches are sets). */
+orc_index* orc_index_from_pairs(unsigned nk, const unsigned* ks, uint32_t ntx,
+                                const uint64_t* npairs, const uint32_t* const* hashes,
+                                const uint32_t* const* tids);
+void orc_index_free(orc_index*);
+/* number of distinct keys / postings at k index i */
+uint64_t orc_index_nkeys(const orc_index*, unsigned i);
+uint64_t orc_index_npost(const orc_index*, unsigned i);
+/* CSR export at k index i: keys ascending (nkeys), offs (nkeys+1), tids ascending per key. */
+void orc_index_export(const orc_index*, unsigned i, uint32_t* keys, uint64_t* offs, uint32_t* tids);
+
+/* ---- sparse_chain (src/sparse_chaining.cpp:29-115) for ONE read -------------------------- */
+/* hashes[i]/nh[i]: the read's sketch at k index i (a set; any order). present[i] = 0 means the
+ * read has no sketch for that k (skipped, :55-58). Output candidates sorted by score desc, then
+ * tid asc (the reference sort is unstable, :108-109: only this normalised order is comparable).
+ * Returns the number of candidates, or (size_t)-1 if cap is too small. */
+size_t orc_chain_read(const orc_index* idx, const uint32_t* const* hashes, const uint32_t* nh,
+                      const int* present, double fraction, uint32_t* out_tid,
+                      uint32_t* out_score, size_t cap);
+
+/* ---- whole hot path over a batch of read sequences -------------------------------------- */
+enum { ORC_OK = 0, ORC_INVALID = 1, ORC_SHORT = 2 };
+/* Per read r (bytes reads[offs[r] .. offs[r+1])): status (process_fastq_single_pass filters,
+ * src/main.cpp:132-138), per k sketch (hash_cnt[r*nk+i], hashes at (r*nk+i)*hcap), candidates
+ * (cand_cnt[r], tid/score at r*ccap). Returns 0, or -1 if a cap is exceeded. */
+int orc_map_batch(const orc_index* idx, const uint8_t* reads, const uint64_t* offs, uint64_t n,
+                  uint32_t threshold, double fraction, uint8_t* status, uint32_t* hash_cnt,
+                  uint32_t* hashes, uint32_t hcap, uint32_t* cand_cnt, uint32_t* cand_tid,
+                  uint32_t* cand_score, uint32_t ccap);
+
+/* The same without outputs (CPU-baseline timing): returns the total candidate count. */
+uint64_t orc_map_batch_count(const orc_index* idx, const uint8_t* reads, const uint64_t* offs,
+                             uint64_t n, uint32_t threshold, double fraction);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

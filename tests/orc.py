@@ -1,0 +1,153 @@
+"""ctypes wrapper over oracle/liboracle.so — TEST INFRASTRUCTURE (the checker, never the product).
+
+Builds the oracle with `make oracle` if the shared object is missing (gcc only, no GPU).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-C", ROOT, "oracle"], stdout=subprocess.DEVNULL)
+        L = C.CDLL(LIB)
+        L.orc_seed.restype = C.c_uint64
+        L.orc_seed.argtypes = [C.c_ubyte]
+        L.orc_srol.restype = C.c_uint64
+        L.orc_srol.argtypes = [C.c_uint64]
+        L.orc_nthash_fwd.restype = C.c_size_t
+        L.orc_nthash_fwd.argtypes = [C.c_char_p, C.c_size_t, C.c_uint, C.c_void_p, C.c_void_p]
+        L.orc_threshold.restype = C.c_uint32
+        L.orc_threshold.argtypes = [C.c_double]
+        L.orc_is_valid_sequence.restype = C.c_int
+        L.orc_is_valid_sequence.argtypes = [C.c_char_p, C.c_size_t]
+        for fn in (L.orc_sketch,):
+            fn.restype = C.c_size_t
+            fn.argtypes = [C.c_char_p, C.c_size_t, C.c_uint, C.c_uint32, C.c_void_p]
+        L.orc_all_hashes.restype = C.c_size_t
+        L.orc_all_hashes.argtypes = [C.c_char_p, C.c_size_t, C.c_uint, C.c_void_p]
+        L.orc_index_build.restype = C.c_void_p
+        L.orc_index_build.argtypes = [C.c_uint, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32]
+        L.orc_index_from_pairs.restype = C.c_void_p
+        L.orc_index_from_pairs.argtypes = [C.c_uint, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_index_free.argtypes = [C.c_void_p]
+        L.orc_index_nkeys.restype = C.c_uint64
+        L.orc_index_nkeys.argtypes = [C.c_void_p, C.c_uint]
+        L.orc_index_npost.restype = C.c_uint64
+        L.orc_index_npost.argtypes = [C.c_void_p, C.c_uint]
+        L.orc_index_export.argtypes = [C.c_void_p, C.c_uint, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_chain_read.restype = C.c_size_t
+        L.orc_chain_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+                                     C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orc_map_batch.restype = C.c_int
+        L.orc_map_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                    C.c_double] + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 3 + [C.c_uint32]
+        L.orc_map_batch_count.restype = C.c_uint64
+        L.orc_map_batch_count.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_double]
+        _lib = L
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+SKETCH_FRACTION = float(np.float32(0.05))  # src/main.cpp:43 `const float sketch_size = 0.05f`
+CHAIN_FRACTION = 0.9                        # src/main.cpp:185
+
+
+def threshold(fraction=SKETCH_FRACTION):
+    return lib().orc_threshold(fraction)
+
+
+def nthash_fwd(seq: bytes, k: int):
+    n = len(seq)
+    h = np.zeros(max(n, 1), np.uint64)
+    p = np.zeros(max(n, 1), np.uint64)
+    m = lib().orc_nthash_fwd(seq, n, k, ptr(h), ptr(p))
+    if m == C.c_size_t(-1).value:
+        raise ValueError("ntHash argument error")
+    return [int(x) for x in h[:m]], [int(x) for x in p[:m]]
+
+
+def sketch(seq: bytes, k: int, thr=None):
+    thr = threshold() if thr is None else thr
+    out = np.zeros(max(len(seq), 1), np.uint32)
+    m = lib().orc_sketch(seq, len(seq), k, thr, ptr(out))
+    if m == C.c_size_t(-1).value:
+        raise ValueError("len < k")
+    return [int(x) for x in out[:m]]
+
+
+class Index:
+    """Oracle inverted index (build_kmer_to_transcript_map restated)."""
+
+    def __init__(self, ks, seqs=None, thr=None, pairs=None, ntx=None):
+        self.ks = [int(k) for k in ks]
+        ka = np.array(self.ks, np.uint32)
+        if pairs is not None:
+            self.ntx = int(ntx)
+            npairs = np.array([len(h) for h, _ in pairs], np.uint64)
+            hs = [np.ascontiguousarray(h, np.uint32) for h, _ in pairs]
+            ts = [np.ascontiguousarray(t, np.uint32) for _, t in pairs]
+            hp = (C.c_void_p * len(hs))(*[x.ctypes.data for x in hs])
+            tp = (C.c_void_p * len(ts))(*[x.ctypes.data for x in ts])
+            self.h = lib().orc_index_from_pairs(len(self.ks), ptr(ka), self.ntx, ptr(npairs), hp, tp)
+        else:
+            thr = threshold() if thr is None else thr
+            self.ntx = len(seqs)
+            buf = b"".join(seqs)
+            offs = np.zeros(len(seqs) + 1, np.uint64)
+            offs[1:] = np.cumsum([len(s) for s in seqs])
+            bb = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
+            self.h = lib().orc_index_build(len(self.ks), ptr(ka), self.ntx, ptr(bb), ptr(offs), thr)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_index_free(self.h)
+            self.h = None
+
+    def csr(self, i):
+        nkeys = lib().orc_index_nkeys(self.h, i)
+        npost = lib().orc_index_npost(self.h, i)
+        keys = np.zeros(nkeys + 1, np.uint32)
+        offs = np.zeros(nkeys + 1, np.uint64)
+        tids = np.zeros(npost + 1, np.uint32)
+        lib().orc_index_export(self.h, i, ptr(keys), ptr(offs), ptr(tids))
+        return keys[:nkeys], offs, tids[:npost]
+
+    def map_batch(self, reads, offs=None, thr=None, fraction=CHAIN_FRACTION, hcap=None, ccap=None):
+        """reads: list of bytes (or a flat uint8 array + offs). Returns dict of numpy arrays."""
+        thr = threshold() if thr is None else thr
+        if offs is None:
+            buf = np.frombuffer(b"".join(reads) or b"\0", np.uint8)
+            offs = np.zeros(len(reads) + 1, np.uint64)
+            offs[1:] = np.cumsum([len(r) for r in reads])
+        else:
+            buf = reads
+        n = len(offs) - 1
+        nk = len(self.ks)
+        maxlen = int(np.max(np.diff(offs))) if n else 1
+        hcap = hcap or max(maxlen, 1)
+        ccap = ccap or max(self.ntx, 1)
+        st = np.zeros(max(n, 1), np.uint8)
+        hc = np.zeros(max(n * nk, 1), np.uint32)
+        hs = np.zeros(max(n * nk * hcap, 1), np.uint32)
+        cc = np.zeros(max(n, 1), np.uint32)
+        ct = np.zeros(max(n * ccap, 1), np.uint32)
+        cs = np.zeros(max(n * ccap, 1), np.uint32)
+        rc = lib().orc_map_batch(self.h, ptr(buf), ptr(offs), n, thr, fraction, ptr(st), ptr(hc),
+                                 ptr(hs), hcap, ptr(cc), ptr(ct), ptr(cs), ccap)
+        assert rc == 0
+        return dict(status=st[:n], hash_cnt=hc[:n * nk].reshape(n, nk),
+                    hashes=hs[:n * nk * hcap].reshape(n, nk, hcap), cand_cnt=cc[:n],
+                    cand_tid=ct[:n * ccap].reshape(n, ccap), cand_score=cs[:n * ccap].reshape(n, ccap))
