@@ -12,3 +12,22 @@ oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
 	gcc -O2 -Wall -Wextra -std=c11 -fPIC -shared $< -o $@
 
 .PHONY: oracle
+
+HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
+LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o
+HOST_CXX ?= g++
+HOSTFLAGS := $(CXXFLAGS_COMMON) -pthread
+
+lib: $(OUT)/libskq.so
+$(OUT)/obj/%.o: $(CSRC)/%.hip $(CSRC)/skq_internal.h include/skq.h include/skq_host.h
+	@mkdir -p $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(OUT)/obj/%.o: $(CSRC)/%.cpp $(CSRC)/skq_internal.h include/skq.h include/skq_host.h
+	@mkdir -p $(OUT)/obj
+	$(HOST_CXX) $(HOSTFLAGS) -c $< -o $@
+$(OUT)/libskq.so: $(LIB_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(LIB_OBJS)
+
+all: lib oracle
+.PHONY: lib all
+.DEFAULT_GOAL := all

@@ -1,0 +1,155 @@
+/*
+ * skq.h — C ABI of the MI355X-native FracMinHash sketch + sparse-chain hot path.
+ *
+ * Plain C: pointers, sizes, int status codes (0 = ok, < 0 = error, message via
+ * skq_last_error()); no exceptions and no C++/HIP/torch types cross this boundary. Streams are
+ * passed as `void*` (a hipStream_t, or NULL for the null stream).
+ *
+ * What each entry point replaces in the reference (Codfishz/Sketch-for-RNA-seq @ 2025-04-18):
+ *   skq_index_create        build_kmer_to_transcript_map's result, made device-resident
+ *                           (include/sketch.h:59, src/sketch.cpp:51-74; consumed at
+ *                           src/sparse_chaining.cpp:51-62)
+ *   skq_sketch              createSketch_FracMinhash_direct over a batch of reads, plus the
+ *                           read filters of process_fastq_single_pass
+ *                           (include/sketch.h:47, src/sketch.cpp:24-39; src/main.cpp:132-144)
+ *   skq_chain               sparse_chain (include/sparse_chaining.h:35-42,
+ *                           src/sparse_chaining.cpp:29-115)
+ *   skq_map                 skq_sketch + skq_chain (the quant hot path, src/main.cpp:181-185)
+ *   skq_chain_sketches      sparse_chain on caller-provided read sketches (drop-in wrapper path)
+ * The C++ drop-in signatures (kmer.h, sketch.h, sparse_chaining.h) are thin wrappers over these
+ * (sketch-for-rna-seq_amd/csrc/dropin.cpp); INTEGRATION.md shows the bindings.
+ *
+ * Threading: one skq_session per host thread / stream; an skq_index may be shared by sessions
+ * on its device. All device pointers must live on the index's device.
+ */
+#ifndef SKQ_H
+#define SKQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKQ_MAX_K 8 /* distinct k-mer lengths per index (the reference allows any list) */
+
+/* per-read status (low 2 bits; higher bits are internal flags) */
+#define SKQ_READ_OK 0      /* sketched and chained                                        */
+#define SKQ_READ_INVALID 1 /* a byte outside uppercase ACGT: dropped (src/main.cpp:132)  */
+#define SKQ_READ_SHORT 2   /* shorter than the largest k: dropped (src/main.cpp:136-138) */
+#define SKQ_STATUS_MASK 3
+
+typedef struct skq_index skq_index;
+typedef struct skq_session skq_session;
+
+const char* skq_last_error(void);
+int skq_version(void);
+int skq_device_count(void);
+
+/* One k: an inverted index in CSR form, host memory. keys ascending and unique; tids of key j
+ * are tids[offs[j] .. offs[j+1]), ascending and unique (a transcript appears at most once per
+ * (k, hash): sketches are sets). */
+typedef struct {
+    uint32_t k;
+    uint64_t nkeys;
+    const uint32_t* keys;
+    const uint64_t* offs; /* nkeys + 1 */
+    const uint32_t* tids;
+} skq_kmer_table;
+
+/* Upload an index to `device`. `ks[0..nk)` is the k list in CLI order (duplicates allowed, as in
+ * the reference); tables[] holds one entry per DISTINCT k (any order). */
+int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks,
+                     uint32_t ntables, const skq_kmer_table* tables, skq_index** out);
+int skq_index_free(skq_index* idx);
+/* device bytes held, total postings, longest postings list */
+int skq_index_stats(const skq_index* idx, uint64_t* device_bytes, uint64_t* npostings,
+                    uint32_t* max_list);
+
+/* A session owns the device workspace for batches of up to max_reads reads of at most
+ * max_len bases each (longer reads are still handled exactly, by the slow path). */
+int skq_session_create(skq_index* idx, uint64_t max_reads, uint32_t max_len, skq_session** out);
+int skq_session_free(skq_session* s);
+
+/* Reads: ASCII bytes on the device; read r is d_reads[d_offs[r] .. d_offs[r+1]). With
+ * d_offs == NULL every read is `fixed_len` bytes (read r at r * fixed_len). max_len bounds the
+ * read length of this batch (reads above it, or above 256, take the slow path).
+ * threshold = (uint32_t)(UINT32_MAX * fraction) — skq_threshold(). */
+int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+               uint64_t n_reads, uint32_t max_len, uint32_t threshold, void* stream);
+/* Chain the session's current sketches; `fraction` as sparse_chain's (0.9 in quant).
+ * accumulate != 0 adds each read's candidates into the per-transcript totals. */
+int skq_chain(skq_session* s, double fraction, int accumulate, void* stream);
+int skq_map(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+            uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction,
+            int accumulate, void* stream);
+
+/* Chain caller-provided sketches (device arrays): read r's sketch at k slot i is
+ * d_hashes[d_hash_offs[r*nk+i] .. +d_hash_cnt[r*nk+i]). present[r*nk+i] == 0 marks a k the
+ * read has no sketch for (skipped, src/sparse_chaining.cpp:55-58); NULL = all present. */
+int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashes,
+                       const uint64_t* d_hash_offs, const uint32_t* d_hash_cnt,
+                       const uint8_t* d_present, double fraction, int accumulate, void* stream);
+
+uint32_t skq_threshold(double fraction);
+
+/* Device-resident results of the last call (valid until the next call on the session).
+ * hashes: read r, k slot i: if hash_cnt[r*nk+i] <= hcap the sorted set is at
+ *   hashes[(r*nk+i)*hcap ...]; otherwise it is at hash_ext[hashes[(r*nk+i)*hcap] ...].
+ * candidates: sorted by score desc, tid asc; if cand_cnt[r] <= ccap at cand_tid/cand_score
+ *   [r*ccap ...]; otherwise at cand_ext[2*cand_tid[r*ccap] ...] as (tid, score) pairs. */
+typedef struct {
+    uint64_t n_reads;
+    uint32_t nk;
+    uint32_t hcap;
+    uint32_t ccap;
+    uint32_t ntx;
+    const uint8_t* status;
+    const uint32_t* hash_cnt;
+    const uint32_t* hashes;
+    const uint32_t* hash_ext;
+    const uint32_t* cand_cnt;
+    const uint32_t* cand_tid;
+    const uint32_t* cand_score;
+    const uint32_t* cand_ext;
+    const uint64_t* tx_reads; /* per transcript: reads listing it as a candidate (accumulated) */
+    const uint64_t* tx_score; /* per transcript: sum of those reads' scores (accumulated)      */
+} skq_results;
+int skq_session_results(skq_session* s, skq_results* out);
+
+/* Waits for the session's work on `stream` and reports device-side capacity errors
+ * (slow-path workspace exhausted). 0 = ok. */
+int skq_session_check(skq_session* s, void* stream);
+
+/* Zero the per-transcript totals. */
+int skq_session_reset_totals(skq_session* s, void* stream);
+
+/* Copy results to host memory in packed CSR form (reads in batch order):
+ * hash_offs[n*nk+1] / hashes[total]; cand_offs[n+1] / cand_tid / cand_score.
+ * Pass NULL arrays to query sizes first (*n_hashes, *n_cands are always written). */
+int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uint32_t* hashes,
+                       uint64_t* cand_offs, uint32_t* cand_tid, uint32_t* cand_score,
+                       uint64_t* n_hashes, uint64_t* n_cands);
+/* Copy the per-transcript totals (ntx each) to host or device memory. */
+int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, int to_device,
+                       void* stream);
+
+/* Device memory helpers (for hosts without their own allocator). */
+int skq_malloc(int device, size_t bytes, void** out);
+int skq_free(void* p);
+int skq_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int skq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int skq_stream_sync(void* stream);
+
+/* Kernel timing: with timing enabled, every skq_sketch / skq_chain call records HIP events on
+ * its stream around its fast kernel. skq_session_kernel_time waits for them and returns the
+ * summed milliseconds and launch count of one kind since the last query (then forgets them).
+ * kind: 0 = k_sketch, 1 = k_chain. Used by bench.py for the roofline figure. */
+int skq_session_enable_timing(skq_session* s, int enable);
+int skq_session_kernel_time(skq_session* s, int kind, double* total_ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,659 @@
+// skq_capi.hip — host side of the C ABI (include/skq.h): device index construction, session
+// workspaces, kernel launches, result export and kernel timing. HIP runtime calls only; the
+// kernels themselves are in skq_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "skq_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(-3, std::string(#expr ": ") + hipGetErrorString(e_));          \
+    } while (0)
+
+uint32_t ceil_log2(uint64_t v) {
+    uint32_t l = 0;
+    while ((1ull << l) < v) ++l;
+    return l;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+int skq::set_error(int code, const char* msg) { return fail(code, msg); }
+
+struct skq_index {
+    int device = 0;
+    uint32_t ntx = 0;
+    uint32_t nk = 0;
+    uint32_t ks[SKQ_MAX_K] = {};
+    uint32_t maxk = 0, mink = 0;
+    skq::DevTable tabs[SKQ_MAX_K] = {};
+    uint64_t* d_slots = nullptr;
+    uint32_t* d_post = nullptr;
+    uint64_t* d_rolltab = nullptr;
+    uint64_t nslots = 0, npost_words = 0, npostings = 0;
+    uint32_t max_list = 0;
+};
+
+struct TimedLaunch {
+    int kind;
+    hipEvent_t start, stop;
+};
+
+struct skq_session {
+    skq_index* idx = nullptr;
+    uint64_t max_reads = 0;
+    uint32_t max_len = 0;
+    uint32_t hcap = 0;         // stride of the current results
+    uint32_t hcap_alloc = 0;   // stride the hashes buffer was sized for
+    uint64_t n_reads = 0;      // reads in the current results
+    bool have_sketch = false;
+    uint8_t* status = nullptr;
+    uint32_t* hash_cnt = nullptr;
+    uint32_t* hashes = nullptr;
+    uint32_t* hash_ext = nullptr;
+    uint64_t hash_ext_cap = 0;
+    uint32_t* ovf1 = nullptr;
+    uint32_t* ovf2 = nullptr;
+    uint32_t ovf_cap = 0;
+    uint32_t* cand_cnt = nullptr;
+    uint32_t* cand_tid = nullptr;
+    uint32_t* cand_score = nullptr;
+    uint32_t* cand_ext = nullptr;
+    uint64_t cand_ext_cap = 0;
+    uint64_t* scratch = nullptr;
+    uint64_t scratch_cap = 0;
+    uint64_t* tx_reads = nullptr;
+    uint64_t* tx_score = nullptr;
+    uint32_t* ctrl = nullptr;
+    // explicit-sketch chaining (skq_chain_sketches) keeps its inputs' layout for export
+    const uint32_t* x_hashes = nullptr;
+    const uint64_t* x_offs = nullptr;
+    bool timing = false;
+    std::vector<TimedLaunch> timed;
+};
+
+namespace {
+
+template <typename T>
+int dev_alloc(T** p, uint64_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+    return 0;
+}
+
+template <typename T>
+void dev_free(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+// choose the raw-retained capacity per (read, k) for a batch: the smallest of 16/32/64 holding
+// the expected count plus 6 sigma (reads beyond it are still exact: slow path)
+uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold) {
+    const uint32_t L = std::min<uint32_t>(max_len, skq::LFAST);
+    const double w = L >= mink ? (double)(L - mink + 1) : 0.0;
+    const double f = ((double)threshold + 1.0) / 4294967296.0;
+    const double mu = w * f;
+    const double need = mu + 6.0 * std::sqrt(mu * (1.0 - f)) + 1.0;
+    if (need <= 16) return 16;
+    if (need <= 32) return 32;
+    return 64;
+}
+
+void record(skq_session* s, int kind, hipEvent_t* start, hipStream_t st) {
+    if (!s->timing) return;
+    (void)hipEventCreate(start);
+    (void)hipEventRecord(*start, st);
+}
+
+void record_stop(skq_session* s, int kind, hipEvent_t start, hipStream_t st) {
+    if (!s->timing) return;
+    hipEvent_t stop;
+    (void)hipEventCreate(&stop);
+    (void)hipEventRecord(stop, st);
+    s->timed.push_back({kind, start, stop});
+}
+
+int ensure_hashes(skq_session* s, uint32_t hcap) {
+    if (s->hcap_alloc >= hcap) return 0;
+    (void)hipDeviceSynchronize();
+    dev_free(s->hashes);
+    if (dev_alloc(&s->hashes, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
+    s->hcap_alloc = hcap;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* skq_last_error(void) { return g_err.c_str(); }
+int skq_version(void) { return 1; }
+
+int skq_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+uint32_t skq_threshold(double fraction) {
+    const uint32_t H = 0xFFFFFFFFu;  // std::numeric_limits<uint32_t>::max(), src/sketch.cpp:25
+    return static_cast<uint32_t>(H * fraction);
+}
+
+int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
+                     const skq_kmer_table* tables, skq_index** out) {
+    if (!out) return fail(-1, "out is null");
+    *out = nullptr;
+    if (nk == 0 || nk > SKQ_MAX_K) return fail(-1, "k list must hold 1..SKQ_MAX_K entries");
+    if (ntables > SKQ_MAX_K) return fail(-1, "too many tables");
+    for (uint32_t i = 0; i < nk; ++i)
+        if (ks[i] == 0) return fail(-1, "k must be greater than 0");
+    DeviceGuard g(device);
+    auto* ix = new skq_index();
+    ix->device = device;
+    ix->ntx = ntx;
+    ix->nk = nk;
+    ix->mink = ~0u;
+    for (uint32_t i = 0; i < nk; ++i) {
+        ix->ks[i] = ks[i];
+        ix->maxk = std::max(ix->maxk, ks[i]);
+        ix->mink = std::min(ix->mink, ks[i]);
+    }
+    // host images: one open-addressing table per distinct k (8-byte slots: key << 32 | postings
+    // offset, load <= 0.75) and one postings array of [count, tid...] runs, each 16-B aligned
+    std::vector<uint64_t> slots;
+    std::vector<uint32_t> post;
+    uint64_t tbase[SKQ_MAX_K] = {};
+    uint32_t tlog[SKQ_MAX_K] = {};
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const skq_kmer_table& T = tables[t];
+        for (uint32_t u = 0; u < t; ++u)
+            if (tables[u].k == T.k) { delete ix; return fail(-1, "duplicate table for one k"); }
+        const uint32_t log2cap = std::max<uint32_t>(6, ceil_log2(T.nkeys * 4 / 3 + 1));
+        const uint64_t cap = 1ull << log2cap;
+        tbase[t] = slots.size();
+        tlog[t] = log2cap;
+        slots.resize(slots.size() + cap, skq::EMPTY_SLOT);
+        uint64_t* S = slots.data() + tbase[t];
+        for (uint64_t j = 0; j < T.nkeys; ++j) {
+            if (j && T.keys[j] <= T.keys[j - 1]) { delete ix; return fail(-1, "keys must be ascending and unique"); }
+            const uint64_t a = T.offs[j], b = T.offs[j + 1];
+            if (b < a) { delete ix; return fail(-1, "offsets must be non-decreasing"); }
+            if (b == a) continue;  // a key with no postings behaves as a miss
+            for (uint64_t q = a; q < b; ++q) {
+                if (T.tids[q] >= ntx) { delete ix; return fail(-1, "transcript id out of range"); }
+                if (q > a && T.tids[q] <= T.tids[q - 1]) { delete ix; return fail(-1, "tids of a key must be ascending and unique"); }
+            }
+            const uint64_t off = (post.size() + 3) & ~3ull;
+            if (off + 1 + (b - a) >= 0xFFFFFFFFull) { delete ix; return fail(-1, "index too large"); }
+            post.resize(off + 1 + (b - a), 0);
+            post[off] = (uint32_t)(b - a);
+            std::copy(T.tids + a, T.tids + b, post.begin() + off + 1);
+            ix->npostings += b - a;
+            ix->max_list = std::max<uint32_t>(ix->max_list, (uint32_t)(b - a));
+            const uint32_t key = T.keys[j];
+            uint64_t s = (uint32_t)(key * skq::HASH_MUL) >> (32 - log2cap);
+            while (S[s] != skq::EMPTY_SLOT) s = (s + 1) & (cap - 1);
+            S[s] = ((uint64_t)key << 32) | (uint32_t)off;
+        }
+    }
+    post.resize(((post.size() + 3) & ~3ull) + 4, 0);  // a full uint4 is always readable
+    for (uint32_t i = 0; i < nk; ++i) {
+        ix->tabs[i].present = 0;
+        for (uint32_t t = 0; t < ntables; ++t)
+            if (tables[t].k == ks[i]) {
+                ix->tabs[i].slot_base = tbase[t];
+                ix->tabs[i].log2cap = tlog[t];
+                ix->tabs[i].present = 1;
+            }
+    }
+    std::vector<uint64_t> roll((size_t)nk * 32, 0);
+    for (uint32_t i = 0; i < nk; ++i)
+        for (uint32_t in = 0; in < 4; ++in)
+            for (uint32_t o = 0; o < 8; ++o)
+                roll[i * 32 + in * 8 + o] =
+                    skq::SEED33[in] ^ (o < 4 ? skq::rot33(skq::SEED33[o], ks[i]) : 0ull);
+    ix->nslots = slots.size();
+    ix->npost_words = post.size();
+    int rc = 0;
+    if ((rc = dev_alloc(&ix->d_slots, slots.size())) || (rc = dev_alloc(&ix->d_post, post.size())) ||
+        (rc = dev_alloc(&ix->d_rolltab, roll.size()))) {
+        skq_index_free(ix);
+        return rc;
+    }
+    if (hipMemcpy(ix->d_slots, slots.data(), slots.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ix->d_post, post.data(), post.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ix->d_rolltab, roll.data(), roll.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+        skq_index_free(ix);
+        return fail(-3, "index upload failed");
+    }
+    *out = ix;
+    return 0;
+}
+
+int skq_index_free(skq_index* ix) {
+    if (!ix) return 0;
+    DeviceGuard g(ix->device);
+    dev_free(ix->d_slots);
+    dev_free(ix->d_post);
+    dev_free(ix->d_rolltab);
+    delete ix;
+    return 0;
+}
+
+int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npostings, uint32_t* max_list) {
+    if (!ix) return fail(-1, "null index");
+    if (device_bytes) *device_bytes = ix->nslots * 8 + ix->npost_words * 4;
+    if (npostings) *npostings = ix->npostings;
+    if (max_list) *max_list = ix->max_list;
+    return 0;
+}
+
+int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
+    if (!ix || !out) return fail(-1, "null argument");
+    *out = nullptr;
+    if (max_reads == 0) max_reads = 1;
+    if (max_reads > 0xFFFFFFFFull) return fail(-1, "max_reads must fit 32 bits");
+    DeviceGuard g(ix->device);
+    auto* s = new skq_session();
+    s->idx = ix;
+    s->max_reads = max_reads;
+    s->max_len = std::max<uint32_t>(max_len, 1);
+    s->ovf_cap = (uint32_t)std::max<uint64_t>(65536, max_reads / 16);
+    const uint32_t Lc = std::min<uint32_t>(s->max_len, skq::LFAST);
+    s->hash_ext_cap = std::max<uint64_t>(1ull << 24, (uint64_t)s->ovf_cap * 4);
+    s->cand_ext_cap = 1ull << 22;
+    s->scratch_cap = 1ull << 24;
+    const uint32_t hcap0 = pick_hcap(Lc, ix->mink, skq_threshold((double)0.05f));
+    int rc = 0;
+    if ((rc = dev_alloc(&s->status, max_reads)) || (rc = dev_alloc(&s->hash_cnt, max_reads * ix->nk)) ||
+        (rc = dev_alloc(&s->hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&s->ovf1, s->ovf_cap)) ||
+        (rc = dev_alloc(&s->ovf2, s->ovf_cap)) || (rc = dev_alloc(&s->cand_cnt, max_reads)) ||
+        (rc = dev_alloc(&s->cand_tid, max_reads * skq::CCAP)) ||
+        (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
+        (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
+        (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
+        (rc = dev_alloc(&s->ctrl, skq::C_WORDS)) || (rc = ensure_hashes(s, hcap0))) {
+        skq_session_free(s);
+        return rc;
+    }
+    if (hipMemset(s->tx_reads, 0, ix->ntx * 8ull) != hipSuccess ||
+        hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess ||
+        hipMemset(s->ctrl, 0, skq::C_WORDS * 4) != hipSuccess) {
+        skq_session_free(s);
+        return fail(-3, "memset failed");
+    }
+    *out = s;
+    return 0;
+}
+
+int skq_session_free(skq_session* s) {
+    if (!s) return 0;
+    DeviceGuard g(s->idx->device);
+    for (auto& t : s->timed) {
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    dev_free(s->status);
+    dev_free(s->hash_cnt);
+    dev_free(s->hashes);
+    dev_free(s->hash_ext);
+    dev_free(s->ovf1);
+    dev_free(s->ovf2);
+    dev_free(s->cand_cnt);
+    dev_free(s->cand_tid);
+    dev_free(s->cand_score);
+    dev_free(s->cand_ext);
+    dev_free(s->scratch);
+    dev_free(s->tx_reads);
+    dev_free(s->tx_score);
+    dev_free(s->ctrl);
+    delete s;
+    return 0;
+}
+
+int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+               uint64_t n_reads, uint32_t max_len, uint32_t threshold, void* stream) {
+    if (!s) return fail(-1, "null session");
+    if (n_reads > s->max_reads) return fail(-1, "batch larger than the session's max_reads");
+    if (n_reads && !d_reads) return fail(-1, "null reads");
+    if (!d_offs) max_len = fixed_len;
+    DeviceGuard g(s->idx->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const skq_index* ix = s->idx;
+    const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
+    const uint32_t hcap = pick_hcap(Lc, ix->mink, threshold);
+    if (int rc = ensure_hashes(s, hcap)) return rc;
+    skq::SketchParams p{};
+    p.reads = d_reads;
+    p.offs = d_offs;
+    p.fixed_len = fixed_len;
+    p.n = n_reads;
+    p.nk = ix->nk;
+    p.maxk = ix->maxk;
+    for (uint32_t i = 0; i < ix->nk; ++i) p.ks[i] = ix->ks[i];
+    p.threshold = threshold;
+    p.tile_chunks = (skq::WG * Lc + 31) / 16 + 1;
+    p.hcap = hcap;
+    p.ovf_cap = s->ovf_cap;
+    p.rolltab = ix->d_rolltab;
+    p.status = s->status;
+    p.hash_cnt = s->hash_cnt;
+    p.hashes = s->hashes;
+    p.hash_ext = s->hash_ext;
+    p.hash_ext_cap = s->hash_ext_cap;
+    p.ctrl = s->ctrl;
+    p.ovf1 = s->ovf1;
+    HIP_TRY(hipMemsetAsync(s->ctrl, 0, 8 * 4, st));
+    hipEvent_t t0{};
+    record(s, 0, &t0, st);
+    if (skq::launch_sketch(p, stream)) return fail(-3, "sketch launch failed");
+    record_stop(s, 0, t0, st);
+    if (skq::launch_sketch_slow(p, stream)) return fail(-3, "sketch slow-path launch failed");
+    s->hcap = hcap;
+    s->n_reads = n_reads;
+    s->have_sketch = true;
+    s->x_hashes = nullptr;
+    s->x_offs = nullptr;
+    return 0;
+}
+
+static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const uint32_t* hash_cnt,
+                      const uint32_t* hashes, const uint64_t* hash_offs, const uint8_t* present,
+                      uint32_t hcap, double fraction, int accumulate, void* stream) {
+    DeviceGuard g(s->idx->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const skq_index* ix = s->idx;
+    skq::ChainParams p{};
+    p.n = n;
+    p.nk = ix->nk;
+    p.hcap = hcap;
+    p.fraction = fraction;
+    p.accumulate = accumulate;
+    p.ovf_cap = s->ovf_cap;
+    p.status = status;
+    p.hash_cnt = hash_cnt;
+    p.hashes = hashes;
+    p.hash_ext = s->hash_ext;
+    p.hash_offs = hash_offs;
+    p.present = present;
+    p.slots = ix->d_slots;
+    p.post = ix->d_post;
+    for (uint32_t i = 0; i < ix->nk; ++i) p.tabs[i] = ix->tabs[i];
+    p.cand_cnt = s->cand_cnt;
+    p.cand_tid = s->cand_tid;
+    p.cand_score = s->cand_score;
+    p.cand_ext = s->cand_ext;
+    p.cand_ext_cap = s->cand_ext_cap;
+    p.scratch = s->scratch;
+    p.scratch_cap = s->scratch_cap;
+    p.tx_reads = s->tx_reads;
+    p.tx_score = s->tx_score;
+    p.ctrl = s->ctrl;
+    p.ovf2 = s->ovf2;
+    HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
+    hipEvent_t t0{};
+    record(s, 1, &t0, st);
+    if (skq::launch_chain(p, stream)) return fail(-3, "chain launch failed");
+    record_stop(s, 1, t0, st);
+    if (skq::launch_chain_slow(p, stream)) return fail(-3, "chain slow-path launch failed");
+    return 0;
+}
+
+int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
+    if (!s) return fail(-1, "null session");
+    if (!s->have_sketch) return fail(-1, "no sketch to chain: call skq_sketch first");
+    return chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap,
+                      fraction, accumulate, stream);
+}
+
+int skq_map(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+            uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction, int accumulate,
+            void* stream) {
+    if (int rc = skq_sketch(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, stream)) return rc;
+    return skq_chain(s, fraction, accumulate, stream);
+}
+
+int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashes,
+                       const uint64_t* d_hash_offs, const uint32_t* d_hash_cnt, const uint8_t* d_present,
+                       double fraction, int accumulate, void* stream) {
+    if (!s) return fail(-1, "null session");
+    if (n_reads > s->max_reads) return fail(-1, "batch larger than the session's max_reads");
+    if (n_reads && (!d_hashes || !d_hash_offs || !d_hash_cnt)) return fail(-1, "null sketch arrays");
+    s->n_reads = n_reads;
+    s->have_sketch = false;
+    s->x_hashes = d_hashes;
+    s->x_offs = d_hash_offs;
+    // hash_cnt is read through p.hash_cnt; keep the session's status out of it (all sketched)
+    return chain_impl(s, n_reads, nullptr, d_hash_cnt, d_hashes, d_hash_offs, d_present, 0, fraction,
+                      accumulate, stream);
+}
+
+int skq_session_results(skq_session* s, skq_results* o) {
+    if (!s || !o) return fail(-1, "null argument");
+    o->n_reads = s->n_reads;
+    o->nk = s->idx->nk;
+    o->hcap = s->hcap;
+    o->ccap = skq::CCAP;
+    o->ntx = s->idx->ntx;
+    o->status = s->status;
+    o->hash_cnt = s->hash_cnt;
+    o->hashes = s->hashes;
+    o->hash_ext = s->hash_ext;
+    o->cand_cnt = s->cand_cnt;
+    o->cand_tid = s->cand_tid;
+    o->cand_score = s->cand_score;
+    o->cand_ext = s->cand_ext;
+    o->tx_reads = s->tx_reads;
+    o->tx_score = s->tx_score;
+    return 0;
+}
+
+int skq_session_check(skq_session* s, void* stream) {
+    if (!s) return fail(-1, "null session");
+    DeviceGuard g(s->idx->device);
+    uint32_t c[skq::C_WORDS];
+    HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    HIP_TRY(hipMemcpy(c, s->ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    const uint32_t err = c[skq::C_ERR1] | c[skq::C_ERR2];
+    if (err) {
+        char buf[160];
+        std::snprintf(buf, sizeof buf,
+                      "device workspace exhausted (error bits 0x%x: 1/2 overflow list, 4 hash_ext, 8 "
+                      "chain scratch, 16 cand_ext); split the batch",
+                      err);
+        return fail(-4, buf);
+    }
+    return 0;
+}
+
+int skq_session_reset_totals(skq_session* s, void* stream) {
+    if (!s) return fail(-1, "null session");
+    DeviceGuard g(s->idx->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemsetAsync(s->tx_reads, 0, s->idx->ntx * 8ull, st));
+    HIP_TRY(hipMemsetAsync(s->tx_score, 0, s->idx->ntx * 8ull, st));
+    return 0;
+}
+
+int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uint32_t* hashes,
+                       uint64_t* cand_offs, uint32_t* cand_tid, uint32_t* cand_score, uint64_t* n_hashes,
+                       uint64_t* n_cands) {
+    if (!s) return fail(-1, "null session");
+    if (int rc = skq_session_check(s, nullptr)) return rc;
+    DeviceGuard g(s->idx->device);
+    const uint64_t n = s->n_reads;
+    const uint32_t nk = s->idx->nk;
+    std::vector<uint32_t> hc(n * nk), cc(n);
+    std::vector<uint8_t> st(n);
+    if (n) {
+        HIP_TRY(hipMemcpy(hc.data(), s->hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(cc.data(), s->cand_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
+        if (s->have_sketch) HIP_TRY(hipMemcpy(st.data(), s->status, n, hipMemcpyDeviceToHost));
+    }
+    uint64_t th = 0, tc = 0;
+    if (s->have_sketch) for (uint64_t v : hc) th += v;
+    for (uint64_t v : cc) tc += v;
+    if (n_hashes) *n_hashes = th;
+    if (n_cands) *n_cands = tc;
+    if (status)
+        for (uint64_t r = 0; r < n; ++r) status[r] = s->have_sketch ? (st[r] & SKQ_STATUS_MASK) : 0;
+    if (hash_offs || hashes) {
+        if (s->have_sketch) {
+            const uint32_t hcap = s->hcap;
+            std::vector<uint32_t> pad(n * nk * hcap);
+            if (n) HIP_TRY(hipMemcpy(pad.data(), s->hashes, pad.size() * 4, hipMemcpyDeviceToHost));
+            uint64_t at = 0;
+            for (uint64_t e = 0; e < n * nk; ++e) {
+                if (hash_offs) hash_offs[e] = at;
+                if (hashes) {
+                    if (hc[e] <= hcap) {
+                        std::copy(pad.begin() + e * hcap, pad.begin() + e * hcap + hc[e], hashes + at);
+                    } else {
+                        HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + pad[e * hcap], hc[e] * 4ull,
+                                          hipMemcpyDeviceToHost));
+                    }
+                }
+                at += hc[e];
+            }
+            if (hash_offs) hash_offs[n * nk] = at;
+        } else if (hash_offs) {
+            for (uint64_t e = 0; e <= n * nk; ++e) hash_offs[e] = 0;
+        }
+    }
+    if (cand_offs || cand_tid || cand_score) {
+        std::vector<uint32_t> t(n * skq::CCAP), sc(n * skq::CCAP);
+        if (n) {
+            HIP_TRY(hipMemcpy(t.data(), s->cand_tid, t.size() * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(sc.data(), s->cand_score, sc.size() * 4, hipMemcpyDeviceToHost));
+        }
+        uint64_t at = 0;
+        std::vector<uint32_t> ext;
+        for (uint64_t r = 0; r < n; ++r) {
+            if (cand_offs) cand_offs[r] = at;
+            const uint32_t c = cc[r];
+            if (c <= (uint32_t)skq::CCAP) {
+                for (uint32_t j = 0; j < c; ++j) {
+                    if (cand_tid) cand_tid[at + j] = t[r * skq::CCAP + j];
+                    if (cand_score) cand_score[at + j] = sc[r * skq::CCAP + j];
+                }
+            } else {
+                ext.resize(2ull * c);
+                HIP_TRY(hipMemcpy(ext.data(), s->cand_ext + 2ull * t[r * skq::CCAP], ext.size() * 4,
+                                  hipMemcpyDeviceToHost));
+                for (uint32_t j = 0; j < c; ++j) {
+                    if (cand_tid) cand_tid[at + j] = ext[2 * j];
+                    if (cand_score) cand_score[at + j] = ext[2 * j + 1];
+                }
+            }
+            at += c;
+        }
+        if (cand_offs) cand_offs[n] = at;
+    }
+    return 0;
+}
+
+int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, int to_device, void* stream) {
+    if (!s) return fail(-1, "null session");
+    DeviceGuard g(s->idx->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t bytes = s->idx->ntx * 8ull;
+    const hipMemcpyKind kind = to_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (tx_reads) HIP_TRY(hipMemcpyAsync(tx_reads, s->tx_reads, bytes, kind, st));
+    if (tx_score) HIP_TRY(hipMemcpyAsync(tx_score, s->tx_score, bytes, kind, st));
+    if (!to_device) HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int skq_malloc(int device, size_t bytes, void** out) {
+    DeviceGuard g(device);
+    HIP_TRY(hipMalloc(out, bytes ? bytes : 1));
+    return 0;
+}
+
+int skq_free(void* p) {
+    if (p) HIP_TRY(hipFree(p));
+    return 0;
+}
+
+int skq_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, reinterpret_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int skq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int skq_stream_sync(void* stream) {
+    HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int skq_session_enable_timing(skq_session* s, int enable) {
+    if (!s) return fail(-1, "null session");
+    s->timing = enable != 0;
+    return 0;
+}
+
+int skq_session_kernel_time(skq_session* s, int kind, double* total_ms, uint64_t* launches) {
+    if (!s) return fail(-1, "null session");
+    DeviceGuard g(s->idx->device);
+    double tot = 0;
+    uint64_t cnt = 0;
+    std::vector<TimedLaunch> keep;
+    for (auto& t : s->timed) {
+        if (t.kind != kind) {
+            keep.push_back(t);
+            continue;
+        }
+        HIP_TRY(hipEventSynchronize(t.stop));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, t.start, t.stop));
+        tot += ms;
+        ++cnt;
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    s->timed.swap(keep);
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = cnt;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,304 @@
+"""Python binding (ctypes) over the C ABI in include/skq.h — for tests, bench.py and scripting.
+
+The hot path is the HIP code in libskq.so; this module only moves arrays across the boundary.
+Loading fails loudly when the shared library is missing: there is no CPU fallback.
+
+If PyTorch is used in the same process, import torch BEFORE this module so that torch's HIP
+runtime is the one libskq.so binds to (same SONAME, one runtime per process).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libskq.so")
+
+SKQ_MAX_K = 8
+READ_OK, READ_INVALID, READ_SHORT = 0, 1, 2
+
+_lib = None
+
+
+class SkqError(RuntimeError):
+    pass
+
+
+class _KmerTable(C.Structure):
+    _fields_ = [("k", C.c_uint32), ("nkeys", C.c_uint64), ("keys", C.c_void_p), ("offs", C.c_void_p),
+                ("tids", C.c_void_p)]
+
+
+class _Results(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("nk", C.c_uint32), ("hcap", C.c_uint32), ("ccap", C.c_uint32),
+                ("ntx", C.c_uint32)] + [(n, C.c_void_p) for n in (
+                    "status", "hash_cnt", "hashes", "hash_ext", "cand_cnt", "cand_tid", "cand_score",
+                    "cand_ext", "tx_reads", "tx_score")]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SkqError("libskq.so not built (%s): run `make` or __graft_entry__.build()" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        vp, u32, u64, i32, dbl = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_double
+        sig = {
+            "skq_last_error": (C.c_char_p, []),
+            "skq_version": (i32, []),
+            "skq_device_count": (i32, []),
+            "skq_threshold": (u32, [dbl]),
+            "skq_index_create": (i32, [i32, u32, u32, vp, u32, vp, C.POINTER(vp)]),
+            "skq_index_free": (i32, [vp]),
+            "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
+            "skq_session_create": (i32, [vp, u64, u32, C.POINTER(vp)]),
+            "skq_session_free": (i32, [vp]),
+            "skq_sketch": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
+            "skq_chain": (i32, [vp, dbl, i32, vp]),
+            "skq_map": (i32, [vp, vp, vp, u32, u64, u32, u32, dbl, i32, vp]),
+            "skq_chain_sketches": (i32, [vp, u64, vp, vp, vp, vp, dbl, i32, vp]),
+            "skq_session_results": (i32, [vp, C.POINTER(_Results)]),
+            "skq_session_check": (i32, [vp, vp]),
+            "skq_session_reset_totals": (i32, [vp, vp]),
+            "skq_session_export": (i32, [vp] + [vp] * 6 + [C.POINTER(u64), C.POINTER(u64)]),
+            "skq_session_totals": (i32, [vp, vp, vp, i32, vp]),
+            "skq_malloc": (i32, [i32, C.c_size_t, C.POINTER(vp)]),
+            "skq_free": (i32, [vp]),
+            "skq_memcpy_h2d": (i32, [vp, vp, C.c_size_t, vp]),
+            "skq_memcpy_d2h": (i32, [vp, vp, C.c_size_t, vp]),
+            "skq_stream_sync": (i32, [vp]),
+            "skq_session_enable_timing": (i32, [vp, i32]),
+            "skq_session_kernel_time": (i32, [vp, i32, C.POINTER(dbl), C.POINTER(u64)]),
+            "skq_tables_build": (i32, [u32, vp, vp, u32, vp, u32, i32, C.POINTER(vp)]),
+            "skq_tables_count": (u32, [vp]),
+            "skq_tables_get": (i32, [vp, u32, C.POINTER(_KmerTable)]),
+            "skq_tables_free": (i32, [vp]),
+            "skq_host_sketch": (C.c_int64, [vp, u64, u32, u32, vp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise SkqError("skq error %d: %s" % (rc, lib().skq_last_error().decode()))
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def threshold(fraction=float(np.float32(0.05))):
+    """(uint32_t)(UINT32_MAX * fraction); quant passes (double)0.05f (src/main.cpp:43)."""
+    return lib().skq_threshold(fraction)
+
+
+class DeviceBuffer:
+    """Raw device allocation through the C ABI (no torch needed)."""
+
+    def __init__(self, nbytes, device=0):
+        self.nbytes = int(nbytes)
+        self.ptr = C.c_void_p()
+        _check(lib().skq_malloc(device, max(self.nbytes, 1), C.byref(self.ptr)))
+
+    @classmethod
+    def from_numpy(cls, a, device=0):
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes, device)
+        if a.nbytes:
+            _check(lib().skq_memcpy_h2d(b.ptr, _p(a), a.nbytes, None))
+            _check(lib().skq_stream_sync(None))
+        return b
+
+    def to_numpy(self, dtype, count):
+        out = np.empty(count, dtype)
+        if out.nbytes:
+            _check(lib().skq_memcpy_d2h(_p(out), self.ptr, out.nbytes, None))
+        return out
+
+    @property
+    def value(self):
+        return self.ptr.value
+
+    def free(self):
+        if self.ptr:
+            lib().skq_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Index:
+    """Device-resident inverted index. tables: {k: (keys u32 asc, offs u64 [nkeys+1], tids u32)}."""
+
+    def __init__(self, ks, ntx, tables, device=0):
+        self.ks = [int(k) for k in ks]
+        self.ntx = int(ntx)
+        self.device = device
+        self._keep = []
+        arr = (_KmerTable * len(tables))()
+        for j, (k, (keys, offs, tids)) in enumerate(tables.items()):
+            keys = np.ascontiguousarray(keys, np.uint32)
+            offs = np.ascontiguousarray(offs, np.uint64)
+            tids = np.ascontiguousarray(tids, np.uint32)
+            self._keep += [keys, offs, tids]
+            arr[j] = _KmerTable(int(k), len(keys), _p(keys), _p(offs), _p(tids))
+        ka = np.array(self.ks, np.uint32)
+        self.h = C.c_void_p()
+        _check(lib().skq_index_create(device, self.ntx, len(self.ks), _p(ka), len(tables),
+                                      C.cast(arr, C.c_void_p), C.byref(self.h)))
+        self._keep = None
+
+    def stats(self):
+        b, n, m = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        _check(lib().skq_index_stats(self.h, C.byref(b), C.byref(n), C.byref(m)))
+        return dict(device_bytes=b.value, postings=n.value, max_list=m.value)
+
+    def free(self):
+        if self.h:
+            lib().skq_index_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Session:
+    def __init__(self, index, max_reads, max_len):
+        self.index = index
+        self.h = C.c_void_p()
+        _check(lib().skq_session_create(index.h, int(max_reads), int(max_len), C.byref(self.h)))
+
+    def sketch(self, d_reads, d_offs, n_reads, max_len, fixed_len=0, thr=None, stream=None):
+        thr = threshold() if thr is None else thr
+        _check(lib().skq_sketch(self.h, d_reads, d_offs, fixed_len, n_reads, max_len, thr, stream))
+
+    def chain(self, fraction=0.9, accumulate=True, stream=None):
+        _check(lib().skq_chain(self.h, fraction, int(accumulate), stream))
+
+    def map(self, d_reads, d_offs, n_reads, max_len, fixed_len=0, thr=None, fraction=0.9,
+            accumulate=True, stream=None):
+        thr = threshold() if thr is None else thr
+        _check(lib().skq_map(self.h, d_reads, d_offs, fixed_len, n_reads, max_len, thr, fraction,
+                             int(accumulate), stream))
+
+    def chain_sketches(self, n_reads, d_hashes, d_offs, d_cnt, d_present=None, fraction=0.9,
+                       accumulate=True, stream=None):
+        _check(lib().skq_chain_sketches(self.h, n_reads, d_hashes, d_offs, d_cnt, d_present, fraction,
+                                        int(accumulate), stream))
+
+    def check(self, stream=None):
+        _check(lib().skq_session_check(self.h, stream))
+
+    def results(self):
+        r = _Results()
+        _check(lib().skq_session_results(self.h, C.byref(r)))
+        return r
+
+    def export(self):
+        nh, nc = C.c_uint64(), C.c_uint64()
+        _check(lib().skq_session_export(self.h, None, None, None, None, None, None, C.byref(nh), C.byref(nc)))
+        r = self.results()
+        n, nk = r.n_reads, r.nk
+        st = np.zeros(max(n, 1), np.uint8)
+        ho = np.zeros(n * nk + 1, np.uint64)
+        hs = np.zeros(max(nh.value, 1), np.uint32)
+        co = np.zeros(n + 1, np.uint64)
+        ct = np.zeros(max(nc.value, 1), np.uint32)
+        cs = np.zeros(max(nc.value, 1), np.uint32)
+        _check(lib().skq_session_export(self.h, _p(st), _p(ho), _p(hs), _p(co), _p(ct), _p(cs),
+                                        C.byref(nh), C.byref(nc)))
+        return dict(status=st[:n], hash_offs=ho, hashes=hs[:nh.value], cand_offs=co,
+                    cand_tid=ct[:nc.value], cand_score=cs[:nc.value], nk=nk)
+
+    def totals(self):
+        ntx = self.index.ntx
+        a = np.zeros(max(ntx, 1), np.uint64)
+        b = np.zeros(max(ntx, 1), np.uint64)
+        _check(lib().skq_session_totals(self.h, _p(a), _p(b), 0, None))
+        return a[:ntx], b[:ntx]
+
+    def totals_to_device(self, d_reads_ptr, d_score_ptr, stream=None):
+        _check(lib().skq_session_totals(self.h, d_reads_ptr, d_score_ptr, 1, stream))
+
+    def reset_totals(self, stream=None):
+        _check(lib().skq_session_reset_totals(self.h, stream))
+
+    def enable_timing(self, on=True):
+        _check(lib().skq_session_enable_timing(self.h, int(on)))
+
+    def kernel_time(self, kind):
+        ms, n = C.c_double(), C.c_uint64()
+        _check(lib().skq_session_kernel_time(self.h, kind, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def free(self):
+        if self.h:
+            lib().skq_session_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def build_tables(seqs, offs, ks, thr=None, nthreads=0):
+    """Host index builder (product C++): sketch transcripts seqs[offs[t]:offs[t+1]] at every
+    k and invert. Returns {k: (keys, offs, tids)} as numpy arrays."""
+    thr = threshold() if thr is None else thr
+    seqs = np.ascontiguousarray(seqs, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    ka = np.array(ks, np.uint32)
+    h = C.c_void_p()
+    _check(lib().skq_tables_build(len(offs) - 1, _p(seqs), _p(offs), len(ka), _p(ka), thr, nthreads,
+                                  C.byref(h)))
+    out = {}
+    try:
+        for i in range(lib().skq_tables_count(h)):
+            t = _KmerTable()
+            _check(lib().skq_tables_get(h, i, C.byref(t)))
+            n = t.nkeys
+
+            def arr(ptr, ctype, count, dtype):
+                if count == 0:
+                    return np.zeros(0, dtype)
+                return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), (count,)).astype(dtype, copy=True)
+
+            offs_a = arr(t.offs, C.c_uint64, n + 1, np.uint64)
+            out[int(t.k)] = (arr(t.keys, C.c_uint32, n, np.uint32), offs_a,
+                             arr(t.tids, C.c_uint32, int(offs_a[-1]), np.uint32))
+    finally:
+        lib().skq_tables_free(h)
+    return out
+
+
+def host_sketch(seq: bytes, k: int, thr=None):
+    thr = threshold() if thr is None else thr
+    a = np.frombuffer(seq, np.uint8) if seq else np.zeros(1, np.uint8)
+    out = np.zeros(max(len(seq), 1), np.uint32)
+    m = lib().skq_host_sketch(_p(a), len(seq), k, thr, _p(out))
+    if m < 0:
+        raise SkqError("len < k or k == 0")
+    return [int(x) for x in out[:m]]
+
+
+def pack_reads(reads):
+    """list of bytes -> (uint8 buffer, uint64 offsets)"""
+    buf = np.frombuffer(b"".join(reads) or b"\0", np.uint8).copy()
+    offs = np.zeros(len(reads) + 1, np.uint64)
+    if reads:
+        offs[1:] = np.cumsum([len(r) for r in reads])
+    return buf, offs

@@ -1,0 +1,280 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit-exact.
+
+Every comparison is exact: retained-hash sets per (read, k), per-read status, and candidate
+lists (tid, score) in the normalised order (score desc, tid asc).
+"""
+import random
+
+import numpy as np
+import pytest
+
+import orc
+import skq
+from skq import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def build(ks, seqs=None, tx=None, pairs=None, ntx=None):
+    """(product device index, oracle index) over the same transcripts / postings."""
+    if pairs is not None:
+        tables = {}
+        for k, (h, t) in zip(ks, pairs):
+            order = np.lexsort((t, h))
+            h, t = np.asarray(h, np.uint32)[order], np.asarray(t, np.uint32)[order]
+            keep = np.ones(len(h), bool)
+            keep[1:] = (h[1:] != h[:-1]) | (t[1:] != t[:-1])
+            h, t = h[keep], t[keep]
+            keys, first = np.unique(h, return_index=True)
+            offs = np.append(first, len(h)).astype(np.uint64)
+            tables[k] = (keys, offs, t)
+        return skq.Index(ks, ntx, tables), orc.Index(ks, pairs=pairs, ntx=ntx)
+    if tx is not None:
+        seqs = [tx.seq(t) for t in range(tx.ntx)]
+    buf, offs = skq.pack_reads(seqs)
+    tables = skq.build_tables(buf, offs, ks)
+    return skq.Index(ks, len(seqs), tables), orc.Index(ks, seqs=seqs)
+
+
+def run_gpu(index, reads, fixed_len=0, fraction=0.9, thr=None, max_len=None):
+    buf, offs = skq.pack_reads(reads)
+    n = len(reads)
+    max_len = max_len if max_len is not None else max([len(r) for r in reads] + [1])
+    s = skq.Session(index, max(n, 1), max_len)
+    d_buf = skq.DeviceBuffer.from_numpy(buf)
+    d_offs = None if fixed_len else skq.DeviceBuffer.from_numpy(offs)
+    s.map(d_buf.ptr, d_offs.ptr if d_offs else None, n, max_len, fixed_len=fixed_len, thr=thr,
+          fraction=fraction)
+    s.check()
+    out = s.export()
+    out["totals"] = s.totals()
+    return out
+
+
+def compare(out, ref, n, nk, check_hashes=True):
+    np.testing.assert_array_equal(out["status"], ref["status"][:n])
+    ho = out["hash_offs"]
+    co = out["cand_offs"]
+    for r in range(n):
+        if check_hashes:
+            for i in range(nk):
+                e = r * nk + i
+                got = out["hashes"][ho[e]:ho[e + 1]]
+                exp = ref["hashes"][r, i, :ref["hash_cnt"][r, i]]
+                assert list(got) == list(exp), (r, i)
+        gt = out["cand_tid"][co[r]:co[r + 1]]
+        gs = out["cand_score"][co[r]:co[r + 1]]
+        c = ref["cand_cnt"][r]
+        assert list(gt) == list(ref["cand_tid"][r, :c]), r
+        assert list(gs) == list(ref["cand_score"][r, :c]), r
+
+
+def totals_from(ref, n, ntx):
+    tr = np.zeros(ntx, np.uint64)
+    ts = np.zeros(ntx, np.uint64)
+    for r in range(n):
+        c = ref["cand_cnt"][r]
+        for j in range(c):
+            tr[ref["cand_tid"][r, j]] += 1
+            ts[ref["cand_tid"][r, j]] += ref["cand_score"][r, j]
+    return tr, ts
+
+
+@pytest.fixture(scope="module")
+def tx300():
+    return synth.transcriptome(300, seed=21)
+
+
+@pytest.mark.parametrize("ks", [[31], [21, 25, 31], [31, 31], [19]])
+@pytest.mark.parametrize("read_len", [100, 150])
+def test_random_reads_match_oracle(tx300, ks, read_len):
+    gi, oi = build(ks, tx=tx300)
+    bases, _, _ = synth.reads(tx300, 3000, read_len, seed=read_len + len(ks), err=0.002)
+    reads = [bases[i * read_len:(i + 1) * read_len].tobytes() for i in range(3000)]
+    out = run_gpu(gi, reads)
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), len(ks))
+    tr, ts = totals_from(ref, len(reads), tx300.ntx)
+    np.testing.assert_array_equal(out["totals"][0], tr)
+    np.testing.assert_array_equal(out["totals"][1], ts)
+    assert (ref["cand_cnt"] > 0).mean() > 0.9
+
+
+def test_fixed_length_mode_equals_offsets_mode(tx300):
+    gi, oi = build([31], tx=tx300)
+    bases, _, _ = synth.reads(tx300, 2049, 150, seed=5)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(2049)]
+    a = run_gpu(gi, reads, fixed_len=150)
+    ref = oi.map_batch(reads)
+    compare(a, ref, len(reads), 1)
+
+
+def test_edge_reads(tx300):
+    gi, oi = build([31], tx=tx300)
+    base = tx300.seq(3)
+    rng = random.Random(1)
+    reads = [
+        b"",                                   # empty: valid but short
+        base[:30],                             # short
+        base[:31],                             # exactly k
+        base[:150].lower(),                    # lowercase: invalid
+        base[:70] + b"N" + base[71:150],       # N: invalid
+        base[:149] + b"\r",                    # trailing CR: invalid
+        base[:150] + b" ",                     # trailing space: invalid
+        base[:300],                            # > 256: slow path
+        base[:257],
+        base[:256],
+        b"A" * 150,                            # low complexity
+        (b"ACGT" * 70)[:280],
+        bytes(rng.choice(b"ACGT") for _ in range(150)),
+        base[10:160],
+    ]
+    reads += [base[j:j + 40] for j in range(0, 200, 7)]
+    out = run_gpu(gi, reads)
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), 1)
+
+
+def test_variable_lengths_and_unaligned(tx300):
+    gi, oi = build([21, 31], tx=tx300)
+    rng = random.Random(7)
+    reads = []
+    for _ in range(1500):
+        t = rng.randrange(tx300.ntx)
+        s = tx300.seq(t)
+        L = rng.randint(0, min(len(s), 400))
+        p = rng.randint(0, len(s) - L)
+        reads.append(s[p:p + L])
+    out = run_gpu(gi, reads)
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), 2)
+
+
+def test_many_retained_hashes_take_slow_path():
+    # a high sketch fraction forces more than HCAP retained hashes per read
+    tx = synth.transcriptome(80, seed=3)
+    thr = orc.threshold(0.5)
+    seqs = [tx.seq(t) for t in range(tx.ntx)]
+    buf, offs = skq.pack_reads(seqs)
+    gi = skq.Index([31], len(seqs), skq.build_tables(buf, offs, [31], thr=thr))
+    oi = orc.Index([31], seqs=seqs, thr=thr)
+    bases, _, _ = synth.reads(tx, 500, 150, seed=4)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(500)]
+    out = run_gpu(gi, reads, thr=thr)
+    ref = oi.map_batch(reads, thr=thr)
+    compare(out, ref, len(reads), 1)
+
+
+@pytest.mark.parametrize("fraction", [0.0, 0.5, 0.9, 1.0, 1.5, -1.0])
+def test_chain_fractions(tx300, fraction):
+    gi, oi = build([21, 31], tx=tx300)
+    bases, _, _ = synth.reads(tx300, 800, 150, seed=17, err=0.01)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(800)]
+    out = run_gpu(gi, reads, fraction=fraction)
+    ref = oi.map_batch(reads, fraction=fraction)
+    compare(out, ref, len(reads), 2)
+
+
+def test_wide_postings_take_slow_chain_path():
+    # hand-built index: some hashes map to 40 transcripts (> DCAP distinct per read) and the
+    # candidate list exceeds the 16 fixed slots
+    rng = np.random.default_rng(0)
+    ntx = 200
+    reads_tx = synth.transcriptome(20, seed=8)
+    seqs = [reads_tx.seq(t) for t in range(reads_tx.ntx)]
+    h, t = [], []
+    for tid, s in enumerate(seqs):
+        for x in orc.sketch(s, 31):
+            h.append(x)
+            t.append(tid)
+            if rng.random() < 0.3:
+                for extra in rng.choice(np.arange(20, ntx), 40, replace=False):
+                    h.append(x)
+                    t.append(int(extra))
+    pairs = [(np.array(h, np.uint32), np.array(t, np.uint32))]
+    gi, oi = build([31], pairs=pairs, ntx=ntx)
+    bases, _, _ = synth.reads(reads_tx, 400, 150, seed=9)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(400)]
+    for fraction in (0.9, 0.0):
+        out = run_gpu(gi, reads, fraction=fraction)
+        ref = oi.map_batch(reads, fraction=fraction)
+        compare(out, ref, len(reads), 1)
+        assert ref["cand_cnt"].max() > 16 or fraction != 0.0
+
+
+def test_index_without_some_k():
+    # k list [21, 31] but the index only holds k=31: k=21 is skipped (src/sparse_chaining.cpp:51-53)
+    tx = synth.transcriptome(100, seed=12)
+    seqs = [tx.seq(t) for t in range(tx.ntx)]
+    buf, offs = skq.pack_reads(seqs)
+    tabs = skq.build_tables(buf, offs, [31])
+    gi = skq.Index([21, 31], len(seqs), tabs)
+    keys, o, tids = tabs[31]
+    cnt = np.diff(o.astype(np.int64))
+    oi = orc.Index([21, 31], pairs=[(np.zeros(0, np.uint32), np.zeros(0, np.uint32)),
+                                    (np.repeat(keys, cnt), tids)], ntx=len(seqs))
+    bases, _, _ = synth.reads(tx, 300, 150, seed=2)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(300)]
+    out = run_gpu(gi, reads)
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), 2)
+
+
+def test_chain_sketches_entry_point(tx300):
+    gi, oi = build([21, 31], tx=tx300)
+    bases, _, _ = synth.reads(tx300, 500, 150, seed=30)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(500)]
+    ref = oi.map_batch(reads)
+    n, nk = len(reads), 2
+    flat, offs, cnt = [], [], []
+    present = np.ones(n * nk, np.uint8)
+    rng = np.random.default_rng(1)
+    for r in range(n):
+        for i in range(nk):
+            offs.append(len(flat))
+            hs = list(ref["hashes"][r, i, :ref["hash_cnt"][r, i]])
+            if rng.random() < 0.1:
+                present[r * nk + i] = 0
+            cnt.append(len(hs))
+            flat += hs
+    flat = np.array(flat + [0], np.uint32)
+    d_h = skq.DeviceBuffer.from_numpy(flat)
+    d_o = skq.DeviceBuffer.from_numpy(np.array(offs, np.uint64))
+    d_c = skq.DeviceBuffer.from_numpy(np.array(cnt, np.uint32))
+    d_p = skq.DeviceBuffer.from_numpy(present)
+    s = skq.Session(gi, n, 150)
+    s.chain_sketches(n, d_h.ptr, d_o.ptr, d_c.ptr, d_p.ptr, fraction=0.9)
+    s.check()
+    out = s.export()
+    import ctypes as C
+    co = out["cand_offs"]
+    for r in range(n):
+        hp = [np.ascontiguousarray(ref["hashes"][r, i, :ref["hash_cnt"][r, i]], np.uint32) for i in range(nk)]
+        arr = (C.c_void_p * nk)(*[x.ctypes.data for x in hp])
+        nh = np.array([ref["hash_cnt"][r, i] for i in range(nk)], np.uint32)
+        pres = np.array([present[r * nk + i] for i in range(nk)], np.int32)
+        t = np.zeros(tx300.ntx, np.uint32)
+        sc = np.zeros(tx300.ntx, np.uint32)
+        c = orc.lib().orc_chain_read(oi.h, arr, orc.ptr(nh), orc.ptr(pres), 0.9, orc.ptr(t), orc.ptr(sc), tx300.ntx)
+        assert list(out["cand_tid"][co[r]:co[r + 1]]) == list(t[:c])
+        assert list(out["cand_score"][co[r]:co[r + 1]]) == list(sc[:c])
+
+
+def test_repeated_batches_accumulate_totals(tx300):
+    gi, oi = build([31], tx=tx300)
+    bases, _, _ = synth.reads(tx300, 1000, 150, seed=44)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(1000)]
+    buf, offs = skq.pack_reads(reads)
+    s = skq.Session(gi, 1000, 150)
+    d_buf = skq.DeviceBuffer.from_numpy(buf)
+    for _ in range(3):
+        s.map(d_buf.ptr, None, 1000, 150, fixed_len=150)
+    s.check()
+    ref = oi.map_batch(reads)
+    tr, ts = totals_from(ref, 1000, tx300.ntx)
+    a, b = s.totals()
+    np.testing.assert_array_equal(a, 3 * tr)
+    np.testing.assert_array_equal(b, 3 * ts)
+    s.reset_totals()
+    a, _ = s.totals()
+    assert a.sum() == 0
