@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""bench.py — reads/s of the quant hot path (FracMinHash sketch + sparse chain) on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): synthetic 150 bp forward-strand reads
+against a ~200k-transcript GENCODE-scale synthetic index, k = 31, sketch fraction (double)0.05f,
+chain fraction 0.9. One step = one pass of the hot path (k_sketch + k_chain, slow paths included)
+over one batch of `--reads` reads already resident in HBM, plus — when N > 1 — the one RCCL
+all-reduce of the per-transcript totals (reads, score) over xGMI.
+
+One process per GPU (torch.distributed.run); reads are sharded (each rank its own seeded batch,
+weak scaling), the index is replicated. rank 0 prints one JSON line.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # first: libskq.so then binds to torch's HIP runtime (one runtime per process)
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sketch-for-rna-seq_amd"))
+import skq  # noqa: E402
+from skq import synth  # noqa: E402
+
+METRIC = "reads/sec (quant, 150 bp, k=31) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "cfg2": dict(ntx=10_000, reads=1_000_000, read_len=100, ks=[31],
+                 desc="synthetic 1M x 100 bp reads vs 10k-transcript index, k=31"),
+    "cfg3": dict(ntx=200_000, reads=10_000_000, read_len=150, ks=[31],
+                 desc="synthetic 10M x 150 bp reads/GPU vs ~200k-transcript index, k=31"),
+    "cfg5": dict(ntx=200_000, reads=10_000_000, read_len=150, ks=[21, 25, 31],
+                 desc="synthetic 10M x 150 bp reads/GPU vs ~200k-transcript index, k={21,25,31}"),
+}
+
+
+def log(*a):
+    print("[bench r%s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
+
+
+def per_read_stats(sess, tables, ks, n):
+    """h (retained hashes, summed over k), P (postings touched), C (candidates) per read, from
+    an export of the current results (deterministic given the inputs)."""
+    out = sess.export()
+    nk = len(ks)
+    ho = out["hash_offs"].astype(np.int64)
+    hs = out["hashes"]
+    P = 0
+    for i, k in enumerate(ks):
+        keys, offs, _ = tables[k]
+        # gather the k-slot-i hashes of every read
+        starts = ho[i:-1:nk]
+        ends = ho[i + 1::nk]
+        lens = ends - starts
+        idx = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+        x = hs[idx]
+        pos = np.searchsorted(keys, x)
+        pos = np.minimum(pos, len(keys) - 1)
+        hit = keys[pos] == x
+        P += int((offs[pos + 1].astype(np.int64) - offs[pos].astype(np.int64))[hit].sum())
+    h = len(hs) / n
+    return dict(h=h, P=P / n, C=len(out["cand_tid"]) / n,
+                ok=float((out["status"] == 0).mean()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
+    ap.add_argument("--cpu-reads", type=int, default=1_000_000, help="CPU-baseline sample size")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.reads:
+        cfg["reads"] = args.reads
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    L, ks, n = cfg["read_len"], cfg["ks"], cfg["reads"]
+    t0 = time.time()
+    tx = synth.transcriptome(cfg["ntx"], seed=1)  # identical on every rank: replicated index
+    tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
+    index = skq.Index(ks, tx.ntx, tables, device=local)
+    bases, _, _ = synth.reads(tx, n, L, seed=1000 + rank, err=0.001)  # rank's shard
+    d_reads = torch.from_numpy(bases).to(dev)
+    sess = skq.Session(index, n, L)
+    stream = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+    totals = torch.zeros(2, tx.ntx, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    log("setup %.1fs: %d transcripts, %d reads x %d bp, index %s" % (
+        time.time() - t0, tx.ntx, n, L, index.stats()))
+
+    def step():
+        sess.map(d_reads.data_ptr(), None, n, L, fixed_len=L, stream=sp)
+        if world > 1:
+            sess.totals_to_device(totals[0].data_ptr(), totals[1].data_ptr(), stream=sp)
+            dist.all_reduce(totals)
+
+    for _ in range(args.warmup):
+        step()
+    sess.check(sp)
+    sess.kernel_time(0), sess.kernel_time(1)
+    sess.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - ts
+    sess.enable_timing(False)
+    sess.check(sp)
+    k1_ms, k1_n = sess.kernel_time(0)
+    k2_ms, k2_n = sess.kernel_time(1)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-read workload figures on a 1M-read slice of this rank's batch
+    ns = min(n, 1_000_000)
+    sess.map(d_reads.data_ptr(), None, ns, L, fixed_len=L, stream=sp, accumulate=False)
+    st = per_read_stats(sess, tables, ks, ns)
+    h, P, Cn = st["h"], st["P"], st["C"]
+    nk = len(ks)
+    # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"):
+    b_sketch = L + 4 * h + 4 * nk + 1                  # read bases in; retained hashes, counts, status out
+    b_chain = 1 + 4 * nk + 4 * h + 8 * h + 4 * P + 8 * Cn + 4 + 16 * Cn
+    b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
+    k1_avg = k1_ms / max(k1_n, 1)
+    k2_avg = k2_ms / max(k2_n, 1)
+    kern = ("k_chain", k2_avg, b_chain) if k2_avg >= k1_avg else ("k_sketch", k1_avg, b_sketch)
+    achieved = n * kern[2] / (kern[1] * 1e-3) / 1e9
+    total_reads = n * world * args.steps
+    value = total_reads / elapsed
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import orc  # the CPU oracle: baseline only, never the measured path
+        keys, offs, tids = tables[ks[0]]
+        pairs = []
+        for k in ks:
+            keys, offs, tids = tables[k]
+            pairs.append((np.repeat(keys, np.diff(offs.astype(np.int64))), tids))
+        oi = orc.Index(ks, pairs=pairs, ntx=tx.ntx)
+        m = min(args.cpu_reads, n)
+        ro = np.arange(0, (m + 1) * L, L, dtype=np.uint64)
+        tc = time.perf_counter()
+        orc.lib().orc_map_batch_count(oi.h, orc.ptr(bases), orc.ptr(ro), m, orc.threshold(), 0.9)
+        dt = time.perf_counter() - tc
+        cpu = {"value": m / dt, "unit": "reads/s", "cores": 1, "kind": "port",
+               "sample": "first %d reads of the same batch (in RAM), same index, oracle/oracle.c "
+                         "single-threaded, %.1fs" % (m, dt)}
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": args.config + ": " + cfg["desc"], "reads_per_gpu": n, "read_len": L,
+                       "transcripts": tx.ntx, "ks": ks, "sketch_fraction": "(double)0.05f",
+                       "chain_fraction": 0.9, "parallelism": "read-sharded x%d, index replicated" % world
+                       + (", 1 all-reduce of per-transcript totals per step" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "kernel": kern[0], "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_read": kern[2], "avg_launch_ms": kern[1]},
+            "path": {"bytes_per_read": b_path, "achieved_GBps": value / world * b_path / 1e9,
+                     "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
+                     "k_sketch_ms": k1_avg, "k_chain_ms": k2_avg, "h": h, "P": P, "C": Cn},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -70,6 +70,7 @@ int skq_index_stats(const skq_index* idx, uint64_t* device_bytes, uint64_t* npos
 /* A session owns the device workspace for batches of up to max_reads reads of at most
  * max_len bases each (longer reads are still handled exactly, by the slow path). */
 int skq_session_create(skq_index* idx, uint64_t max_reads, uint32_t max_len, skq_session** out);
+/* (max_reads < 2^24: per-batch transcript totals are packed into 24-bit read counts) */
 int skq_session_free(skq_session* s);
 
 /* Reads: ASCII bytes on the device; read r is d_reads[d_offs[r] .. d_offs[r+1]). With
@@ -94,11 +95,14 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
 
 uint32_t skq_threshold(double fraction);
 
-/* Device-resident results of the last call (valid until the next call on the session).
- * hashes: read r, k slot i: if hash_cnt[r*nk+i] <= hcap the sorted set is at
- *   hashes[(r*nk+i)*hcap ...]; otherwise it is at hash_ext[hashes[(r*nk+i)*hcap] ...].
- * candidates: sorted by score desc, tid asc; if cand_cnt[r] <= ccap at cand_tid/cand_score
- *   [r*ccap ...]; otherwise at cand_ext[2*cand_tid[r*ccap] ...] as (tid, score) pairs. */
+/* Device-resident results of the last call (valid until the next call on the session), in
+ * structure-of-arrays layout (n = n_reads of the call, so a wave's accesses are contiguous):
+ * hashes: read r, k slot i: c = hash_cnt[i*n + r]; if c <= hcap the sorted set is
+ *   hashes[(i*hcap + j)*n + r] for j < c; otherwise it is hash_ext[hashes[i*hcap*n + r] + j].
+ * candidates (sorted by score desc, tid asc): c = cand_cnt[r]; if c <= ccap candidate j is
+ *   (cand_tid[j*n + r], cand_score[j*n + r]); otherwise the (tid, score) pairs are at
+ *   cand_ext[2*(cand_tid[r] + j)], cand_ext[2*(cand_tid[r] + j) + 1].
+ * After skq_chain_sketches, hash_cnt/hashes are not the session's (the caller's inputs). */
 typedef struct {
     uint64_t n_reads;
     uint32_t nk;
@@ -147,6 +151,8 @@ int skq_stream_sync(void* stream);
  * summed milliseconds and launch count of one kind since the last query (then forgets them).
  * kind: 0 = k_sketch, 1 = k_chain. Used by bench.py for the roofline figure. */
 int skq_session_enable_timing(skq_session* s, int enable);
+/* Development A/B switch for the chain kernel (0 = default). Not needed by users. */
+int skq_session_set_variant(skq_session* s, int variant);
 int skq_session_kernel_time(skq_session* s, int kind, double* total_ms, uint64_t* launches);
 
 #ifdef __cplusplus

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "skq_internal.h"
@@ -27,12 +28,6 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                          \
             return fail(-3, std::string(#expr ": ") + hipGetErrorString(e_));          \
     } while (0)
-
-uint32_t ceil_log2(uint64_t v) {
-    uint32_t l = 0;
-    while ((1ull << l) < v) ++l;
-    return l;
-}
 
 struct DeviceGuard {
     int prev = -1;
@@ -58,10 +53,10 @@ struct skq_index {
     uint32_t ks[SKQ_MAX_K] = {};
     uint32_t maxk = 0, mink = 0;
     skq::DevTable tabs[SKQ_MAX_K] = {};
-    uint64_t* d_slots = nullptr;
-    uint32_t* d_post = nullptr;
+    uint32_t* d_buckets = nullptr;
+    uint32_t* d_lists = nullptr;
     uint64_t* d_rolltab = nullptr;
-    uint64_t nslots = 0, npost_words = 0, npostings = 0;
+    uint64_t nbucket_words = 0, nlist_words = 0, npostings = 0;
     uint32_t max_list = 0;
 };
 
@@ -93,6 +88,7 @@ struct skq_session {
     uint64_t cand_ext_cap = 0;
     uint64_t* scratch = nullptr;
     uint64_t scratch_cap = 0;
+    uint64_t* tx_acc = nullptr;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     uint32_t* ctrl = nullptr;
@@ -101,6 +97,7 @@ struct skq_session {
     const uint64_t* x_offs = nullptr;
     bool timing = false;
     std::vector<TimedLaunch> timed;
+    int variant = 0;
 };
 
 namespace {
@@ -120,13 +117,14 @@ void dev_free(T*& p) {
 }
 
 // choose the raw-retained capacity per (read, k) for a batch: the smallest of 16/32/64 holding
-// the expected count plus 6 sigma (reads beyond it are still exact: slow path)
+// the expected count plus 4 sigma (reads beyond it are still exact, through the slow path;
+// at 150 bp, k = 31, 5 % that is ~4e-5 of reads)
 uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold) {
     const uint32_t L = std::min<uint32_t>(max_len, skq::LFAST);
     const double w = L >= mink ? (double)(L - mink + 1) : 0.0;
     const double f = ((double)threshold + 1.0) / 4294967296.0;
     const double mu = w * f;
-    const double need = mu + 6.0 * std::sqrt(mu * (1.0 - f)) + 1.0;
+    const double need = mu + 4.0 * std::sqrt(mu * (1.0 - f));
     if (need <= 16) return 16;
     if (need <= 32) return 32;
     return 64;
@@ -192,70 +190,105 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
         ix->maxk = std::max(ix->maxk, ks[i]);
         ix->mink = std::min(ix->mink, ks[i]);
     }
-    // host images: one open-addressing table per distinct k (8-byte slots: key << 32 | postings
-    // offset, load <= 0.75) and one postings array of [count, tid...] runs, each 16-B aligned
-    std::vector<uint64_t> slots;
-    std::vector<uint32_t> post;
+    // host image (skq_internal.h): distinct postings lists stored once ([n, tid...], 16-B
+    // aligned) and, per distinct k, a table of 64-B buckets mapping keys to list offsets
+    std::vector<uint32_t> buckets;
+    std::vector<uint32_t> lists;
+    std::unordered_map<uint64_t, std::vector<uint32_t>> seen;  // list hash -> offsets
+    auto list_offset = [&](const uint32_t* a, uint64_t n) -> uint64_t {
+        uint64_t h = 1469598103934665603ull ^ n;
+        for (uint64_t q = 0; q < n; ++q) h = (h ^ a[q]) * 1099511628211ull;
+        auto& cand = seen[h];
+        for (uint32_t off : cand)
+            if (lists[off] == n && std::equal(a, a + n, lists.begin() + off + 1)) return off;
+        const uint64_t off = lists.size();
+        lists.push_back((uint32_t)n);
+        lists.insert(lists.end(), a, a + n);
+        lists.resize((lists.size() + 3) & ~3ull, 0);
+        cand.push_back((uint32_t)off);
+        return off;
+    };
     uint64_t tbase[SKQ_MAX_K] = {};
-    uint32_t tlog[SKQ_MAX_K] = {};
+    uint32_t tnb[SKQ_MAX_K] = {}, tprobe[SKQ_MAX_K] = {};
     for (uint32_t t = 0; t < ntables; ++t) {
         const skq_kmer_table& T = tables[t];
         for (uint32_t u = 0; u < t; ++u)
             if (tables[u].k == T.k) { delete ix; return fail(-1, "duplicate table for one k"); }
-        const uint32_t log2cap = std::max<uint32_t>(6, ceil_log2(T.nkeys * 4 / 3 + 1));
-        const uint64_t cap = 1ull << log2cap;
-        tbase[t] = slots.size();
-        tlog[t] = log2cap;
-        slots.resize(slots.size() + cap, skq::EMPTY_SLOT);
-        uint64_t* S = slots.data() + tbase[t];
+        std::vector<std::pair<uint32_t, uint32_t>> recs;  // (key, list offset)
+        recs.reserve(T.nkeys);
         for (uint64_t j = 0; j < T.nkeys; ++j) {
             if (j && T.keys[j] <= T.keys[j - 1]) { delete ix; return fail(-1, "keys must be ascending and unique"); }
             const uint64_t a = T.offs[j], b = T.offs[j + 1];
             if (b < a) { delete ix; return fail(-1, "offsets must be non-decreasing"); }
-            if (b == a) continue;  // a key with no postings behaves as a miss
             for (uint64_t q = a; q < b; ++q) {
                 if (T.tids[q] >= ntx) { delete ix; return fail(-1, "transcript id out of range"); }
                 if (q > a && T.tids[q] <= T.tids[q - 1]) { delete ix; return fail(-1, "tids of a key must be ascending and unique"); }
             }
-            const uint64_t off = (post.size() + 3) & ~3ull;
-            if (off + 1 + (b - a) >= 0xFFFFFFFFull) { delete ix; return fail(-1, "index too large"); }
-            post.resize(off + 1 + (b - a), 0);
-            post[off] = (uint32_t)(b - a);
-            std::copy(T.tids + a, T.tids + b, post.begin() + off + 1);
+            if (b == a) continue;  // a key with no postings behaves as a miss
+            const uint64_t off = list_offset(T.tids + a, b - a);
+            if (off >= 0xFFFFFFF0ull) { delete ix; return fail(-1, "index too large"); }
+            recs.emplace_back(T.keys[j], (uint32_t)off);
             ix->npostings += b - a;
             ix->max_list = std::max<uint32_t>(ix->max_list, (uint32_t)(b - a));
-            const uint32_t key = T.keys[j];
-            uint64_t s = (uint32_t)(key * skq::HASH_MUL) >> (32 - log2cap);
-            while (S[s] != skq::EMPTY_SLOT) s = (s + 1) & (cap - 1);
-            S[s] = ((uint64_t)key << 32) | (uint32_t)off;
         }
+        const uint64_t nb64 = std::max<uint64_t>(64, (uint64_t)(recs.size() / (skq::BUCKET_MAX_RECORDS * 0.80)) + 1);
+        if (nb64 >= 0xFFFFFFFFull) { delete ix; return fail(-1, "index too large"); }
+        const uint32_t nb = (uint32_t)nb64;
+        tbase[t] = buckets.size() / skq::BUCKET_WORDS;
+        tnb[t] = nb;
+        buckets.resize(buckets.size() + (uint64_t)nb * skq::BUCKET_WORDS, 0);
+        uint32_t* B = buckets.data() + tbase[t] * skq::BUCKET_WORDS;
+        // place records in home-bucket order, each at the first bucket from home with room
+        std::vector<std::pair<uint32_t, uint32_t>> order;  // (home, record)
+        order.reserve(recs.size());
+        for (uint32_t j = 0; j < recs.size(); ++j) order.emplace_back(skq::home_bucket(recs[j].first, nb), j);
+        std::sort(order.begin(), order.end());
+        uint32_t maxd = 0;
+        for (const auto& [home, j] : order) {
+            uint32_t b = home, d = 0;
+            while ((B[(uint64_t)b * skq::BUCKET_WORDS] & 7u) == skq::BUCKET_MAX_RECORDS) {
+                B[(uint64_t)b * skq::BUCKET_WORDS] |= 8u;  // a key homed here or earlier continues
+                b = b + 1 == nb ? 0 : b + 1;
+                if (++d > nb) { delete ix; return fail(-1, "bucket table overflow"); }
+            }
+            maxd = std::max(maxd, d);
+            uint32_t* H = B + (uint64_t)b * skq::BUCKET_WORDS;
+            const uint32_t m = H[0] & 7u;
+            H[1 + m] = recs[j].first;
+            H[skq::BUCKET_LIST0 + m] = recs[j].second;
+            H[0] = (H[0] & ~7u) | (m + 1);
+        }
+        tprobe[t] = maxd + 1;
     }
-    post.resize(((post.size() + 3) & ~3ull) + 4, 0);  // a full uint4 is always readable
+    lists.resize(lists.size() + 4, 0);  // a uint4 read at any list start stays inside
     for (uint32_t i = 0; i < nk; ++i) {
         ix->tabs[i].present = 0;
         for (uint32_t t = 0; t < ntables; ++t)
             if (tables[t].k == ks[i]) {
-                ix->tabs[i].slot_base = tbase[t];
-                ix->tabs[i].log2cap = tlog[t];
+                ix->tabs[i].bucket_base = tbase[t];
+                ix->tabs[i].nbuckets = tnb[t];
+                ix->tabs[i].max_probe = tprobe[t];
                 ix->tabs[i].present = 1;
             }
     }
-    std::vector<uint64_t> roll((size_t)nk * 32, 0);
+    // per k slot: E[in*4 + out] = seed(in) ^ rot33^k(seed(out)) (one roll step's XOR), then the
+    // 4 seeds for the first window
+    std::vector<uint64_t> roll((size_t)nk * 16 + 4, 0);
     for (uint32_t i = 0; i < nk; ++i)
         for (uint32_t in = 0; in < 4; ++in)
-            for (uint32_t o = 0; o < 8; ++o)
-                roll[i * 32 + in * 8 + o] =
-                    skq::SEED33[in] ^ (o < 4 ? skq::rot33(skq::SEED33[o], ks[i]) : 0ull);
-    ix->nslots = slots.size();
-    ix->npost_words = post.size();
+            for (uint32_t o = 0; o < 4; ++o)
+                roll[i * 16 + in * 4 + o] = skq::SEED33[in] ^ skq::rot33(skq::SEED33[o], ks[i]);
+    for (uint32_t c = 0; c < 4; ++c) roll[(size_t)nk * 16 + c] = skq::SEED33[c];
+    ix->nbucket_words = buckets.size();
+    ix->nlist_words = lists.size();
     int rc = 0;
-    if ((rc = dev_alloc(&ix->d_slots, slots.size())) || (rc = dev_alloc(&ix->d_post, post.size())) ||
+    if ((rc = dev_alloc(&ix->d_buckets, buckets.size())) || (rc = dev_alloc(&ix->d_lists, lists.size())) ||
         (rc = dev_alloc(&ix->d_rolltab, roll.size()))) {
         skq_index_free(ix);
         return rc;
     }
-    if (hipMemcpy(ix->d_slots, slots.data(), slots.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ix->d_post, post.data(), post.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(ix->d_buckets, buckets.data(), buckets.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ix->d_lists, lists.data(), lists.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(ix->d_rolltab, roll.data(), roll.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
         skq_index_free(ix);
         return fail(-3, "index upload failed");
@@ -267,8 +300,8 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
 int skq_index_free(skq_index* ix) {
     if (!ix) return 0;
     DeviceGuard g(ix->device);
-    dev_free(ix->d_slots);
-    dev_free(ix->d_post);
+    dev_free(ix->d_buckets);
+    dev_free(ix->d_lists);
     dev_free(ix->d_rolltab);
     delete ix;
     return 0;
@@ -276,7 +309,7 @@ int skq_index_free(skq_index* ix) {
 
 int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npostings, uint32_t* max_list) {
     if (!ix) return fail(-1, "null index");
-    if (device_bytes) *device_bytes = ix->nslots * 8 + ix->npost_words * 4;
+    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4;
     if (npostings) *npostings = ix->npostings;
     if (max_list) *max_list = ix->max_list;
     return 0;
@@ -286,13 +319,13 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     if (!ix || !out) return fail(-1, "null argument");
     *out = nullptr;
     if (max_reads == 0) max_reads = 1;
-    if (max_reads > 0xFFFFFFFFull) return fail(-1, "max_reads must fit 32 bits");
+    if (max_reads > skq::MAX_BATCH) return fail(-1, "max_reads must be below 2^24 (split larger batches)");
     DeviceGuard g(ix->device);
     auto* s = new skq_session();
     s->idx = ix;
     s->max_reads = max_reads;
     s->max_len = std::max<uint32_t>(max_len, 1);
-    s->ovf_cap = (uint32_t)std::max<uint64_t>(65536, max_reads / 16);
+    s->ovf_cap = (uint32_t)max_reads;  // any read may take a slow path (e.g. > 4 k slots)
     const uint32_t Lc = std::min<uint32_t>(s->max_len, skq::LFAST);
     s->hash_ext_cap = std::max<uint64_t>(1ull << 24, (uint64_t)s->ovf_cap * 4);
     s->cand_ext_cap = 1ull << 22;
@@ -306,11 +339,13 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
         (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
         (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
+        (rc = dev_alloc(&s->tx_acc, ix->ntx)) ||
         (rc = dev_alloc(&s->ctrl, skq::C_WORDS)) || (rc = ensure_hashes(s, hcap0))) {
         skq_session_free(s);
         return rc;
     }
     if (hipMemset(s->tx_reads, 0, ix->ntx * 8ull) != hipSuccess ||
+        hipMemset(s->tx_acc, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->ctrl, 0, skq::C_WORDS * 4) != hipSuccess) {
         skq_session_free(s);
@@ -338,6 +373,7 @@ int skq_session_free(skq_session* s) {
     dev_free(s->cand_score);
     dev_free(s->cand_ext);
     dev_free(s->scratch);
+    dev_free(s->tx_acc);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -410,8 +446,8 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.hash_ext = s->hash_ext;
     p.hash_offs = hash_offs;
     p.present = present;
-    p.slots = ix->d_slots;
-    p.post = ix->d_post;
+    p.buckets = ix->d_buckets;
+    p.lists = ix->d_lists;
     for (uint32_t i = 0; i < ix->nk; ++i) p.tabs[i] = ix->tabs[i];
     p.cand_cnt = s->cand_cnt;
     p.cand_tid = s->cand_tid;
@@ -420,16 +456,20 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.cand_ext_cap = s->cand_ext_cap;
     p.scratch = s->scratch;
     p.scratch_cap = s->scratch_cap;
+    p.tx_acc = s->tx_acc;
     p.tx_reads = s->tx_reads;
     p.tx_score = s->tx_score;
     p.ctrl = s->ctrl;
     p.ovf2 = s->ovf2;
+    p.variant = s->variant;
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
     record(s, 1, &t0, st);
     if (skq::launch_chain(p, stream)) return fail(-3, "chain launch failed");
     record_stop(s, 1, t0, st);
     if (skq::launch_chain_slow(p, stream)) return fail(-3, "chain slow-path launch failed");
+    if (accumulate && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, ix->ntx, stream))
+        return fail(-3, "totals fold launch failed");
     return 0;
 }
 
@@ -505,6 +545,7 @@ int skq_session_reset_totals(skq_session* s, void* stream) {
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(hipMemsetAsync(s->tx_reads, 0, s->idx->ntx * 8ull, st));
+    HIP_TRY(hipMemsetAsync(s->tx_acc, 0, s->idx->ntx * 8ull, st));
     HIP_TRY(hipMemsetAsync(s->tx_score, 0, s->idx->ntx * 8ull, st));
     return 0;
 }
@@ -517,15 +558,18 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     DeviceGuard g(s->idx->device);
     const uint64_t n = s->n_reads;
     const uint32_t nk = s->idx->nk;
-    std::vector<uint32_t> hc(n * nk), cc(n);
+    std::vector<uint32_t> hc, cc(n);
     std::vector<uint8_t> st(n);
     if (n) {
-        HIP_TRY(hipMemcpy(hc.data(), s->hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(cc.data(), s->cand_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
-        if (s->have_sketch) HIP_TRY(hipMemcpy(st.data(), s->status, n, hipMemcpyDeviceToHost));
+        if (s->have_sketch) {
+            hc.resize(n * nk);  // [i][r]
+            HIP_TRY(hipMemcpy(hc.data(), s->hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(st.data(), s->status, n, hipMemcpyDeviceToHost));
+        }
     }
     uint64_t th = 0, tc = 0;
-    if (s->have_sketch) for (uint64_t v : hc) th += v;
+    for (uint64_t v : hc) th += v;
     for (uint64_t v : cc) tc += v;
     if (n_hashes) *n_hashes = th;
     if (n_cands) *n_cands = tc;
@@ -534,28 +578,31 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     if (hash_offs || hashes) {
         if (s->have_sketch) {
             const uint32_t hcap = s->hcap;
-            std::vector<uint32_t> pad(n * nk * hcap);
+            std::vector<uint32_t> pad((uint64_t)nk * hcap * n);  // [i][j][r]
             if (n) HIP_TRY(hipMemcpy(pad.data(), s->hashes, pad.size() * 4, hipMemcpyDeviceToHost));
             uint64_t at = 0;
-            for (uint64_t e = 0; e < n * nk; ++e) {
-                if (hash_offs) hash_offs[e] = at;
-                if (hashes) {
-                    if (hc[e] <= hcap) {
-                        std::copy(pad.begin() + e * hcap, pad.begin() + e * hcap + hc[e], hashes + at);
-                    } else {
-                        HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + pad[e * hcap], hc[e] * 4ull,
-                                          hipMemcpyDeviceToHost));
+            for (uint64_t r = 0; r < n; ++r)
+                for (uint32_t i = 0; i < nk; ++i) {
+                    const uint64_t e = r * nk + i;
+                    const uint32_t c = hc[(uint64_t)i * n + r];
+                    if (hash_offs) hash_offs[e] = at;
+                    if (hashes) {
+                        if (c <= hcap) {
+                            for (uint32_t j = 0; j < c; ++j) hashes[at + j] = pad[((uint64_t)i * hcap + j) * n + r];
+                        } else {
+                            HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + pad[(uint64_t)i * hcap * n + r], c * 4ull,
+                                              hipMemcpyDeviceToHost));
+                        }
                     }
+                    at += c;
                 }
-                at += hc[e];
-            }
             if (hash_offs) hash_offs[n * nk] = at;
         } else if (hash_offs) {
             for (uint64_t e = 0; e <= n * nk; ++e) hash_offs[e] = 0;
         }
     }
     if (cand_offs || cand_tid || cand_score) {
-        std::vector<uint32_t> t(n * skq::CCAP), sc(n * skq::CCAP);
+        std::vector<uint32_t> t((uint64_t)skq::CCAP * n), sc((uint64_t)skq::CCAP * n);  // [j][r]
         if (n) {
             HIP_TRY(hipMemcpy(t.data(), s->cand_tid, t.size() * 4, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(sc.data(), s->cand_score, sc.size() * 4, hipMemcpyDeviceToHost));
@@ -567,13 +614,12 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
             const uint32_t c = cc[r];
             if (c <= (uint32_t)skq::CCAP) {
                 for (uint32_t j = 0; j < c; ++j) {
-                    if (cand_tid) cand_tid[at + j] = t[r * skq::CCAP + j];
-                    if (cand_score) cand_score[at + j] = sc[r * skq::CCAP + j];
+                    if (cand_tid) cand_tid[at + j] = t[(uint64_t)j * n + r];
+                    if (cand_score) cand_score[at + j] = sc[(uint64_t)j * n + r];
                 }
             } else {
                 ext.resize(2ull * c);
-                HIP_TRY(hipMemcpy(ext.data(), s->cand_ext + 2ull * t[r * skq::CCAP], ext.size() * 4,
-                                  hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(ext.data(), s->cand_ext + 2ull * t[r], ext.size() * 4, hipMemcpyDeviceToHost));
                 for (uint32_t j = 0; j < c; ++j) {
                     if (cand_tid) cand_tid[at + j] = ext[2 * j];
                     if (cand_score) cand_score[at + j] = ext[2 * j + 1];
@@ -622,6 +668,12 @@ int skq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
 
 int skq_stream_sync(void* stream) {
     HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int skq_session_set_variant(skq_session* s, int variant) {
+    if (!s) return fail(-1, "null session");
+    s->variant = variant;
     return 0;
 }
 

@@ -11,10 +11,10 @@ constexpr int WG = 256;            // threads per workgroup for both kernels (4 
 constexpr int LFAST = 256;         // reads longer than this take the slow path
 constexpr int DCAP = 16;           // distinct transcripts per read on the fast chain path
 constexpr int CCAP = DCAP;         // candidate slots per read (fast path can't exceed DCAP)
-constexpr int HFAST = 16;          // hashes per (read, k) the fast chain path accepts
+constexpr int HFAST = 255;         // hashes per (read, k) the fast chain path accepts (8-bit counts)
 constexpr int NK_FAST = 4;         // k slots the fast chain path packs (8-bit counts)
-constexpr uint64_t EMPTY_SLOT = ~0ull;
 constexpr uint32_t HASH_MUL = 0x9E3779B1u;
+constexpr uint64_t MAX_BATCH = (1ull << 24) - 1;  // packed per-batch totals hold 24-bit counts
 
 // status flags above SKQ_STATUS_MASK (internal)
 constexpr uint8_t ST_SLOW1 = 0x10;  // sketch handled by the slow path
@@ -35,10 +35,27 @@ enum Err : uint32_t {
     E_OVF1_FULL = 1, E_OVF2_FULL = 2, E_HASH_EXT = 4, E_SCRATCH = 8, E_CAND_EXT = 16
 };
 
+// Device index. Postings lists are de-duplicated into equivalence classes: every distinct
+// transcript set is stored once in the `lists` array as [n, tid_0 .. tid_{n-1}] (16-B aligned),
+// and each k has a table of 64-byte buckets (16 u32 words) mapping keys to list offsets:
+//   word 0       header: bits 0-2 m = records in the bucket (0..7); bit 3 = "continue": some key
+//                homed at or before this bucket lives further on
+//   words 1..7   keys of records 0..m-1
+//   words 8..14  list offsets of records 0..m-1
+// A key's home bucket is (uint64)(key * HASH_MUL) * nbuckets >> 32; records are placed at the
+// first bucket from home with room (host build, in home order), so a probe reads one 64-B line
+// unless the home bucket is marked "continue"; the max displacement is kept per table.
+// A read usually hits 1-3 distinct lists, so k_chain counts per list, then expands.
+constexpr uint32_t BUCKET_WORDS = 16;
+constexpr uint32_t BUCKET_MAX_RECORDS = 7;
+constexpr uint32_t BUCKET_LIST0 = 8;  // word of record 0's list offset
+
 struct DevTable {
-    uint64_t slot_base;  // first slot of this k's table in the slot array
-    uint32_t log2cap;
-    uint32_t present;    // 0: the index has no table for this k (skipped, src/sparse_chaining.cpp:51-53)
+    uint64_t bucket_base;  // first bucket of this k's table in the bucket array
+    uint32_t nbuckets;
+    uint32_t max_probe;    // buckets a probe may have to read (displacement + 1)
+    uint32_t present;      // 0: the index has no table for this k (skipped, src/sparse_chaining.cpp:51-53)
+    uint32_t pad;
 };
 
 struct SketchParams {
@@ -53,7 +70,7 @@ struct SketchParams {
     uint32_t tile_chunks;  // 16-byte chunks staged per workgroup
     uint32_t hcap;
     uint32_t ovf_cap;
-    const uint64_t* rolltab;  // [nk][32] 33-bit entries: seed(in) ^ rot^k(seed(out)), out=4 => none
+    const uint64_t* rolltab;  // [nk][16] 33-bit seed(in) ^ rot^k(seed(out)) by (in*4 + out), then 4 seeds
     uint8_t* status;
     uint32_t* hash_cnt;
     uint32_t* hashes;
@@ -76,8 +93,8 @@ struct ChainParams {
     const uint32_t* hash_ext;
     const uint64_t* hash_offs; // null => padded layout
     const uint8_t* present;    // null => all k present
-    const uint64_t* slots;
-    const uint32_t* post;
+    const uint32_t* buckets;
+    const uint32_t* lists;    // [n, tid...] per distinct postings list
     DevTable tabs[SKQ_MAX_K];
     uint32_t* cand_cnt;
     uint32_t* cand_tid;
@@ -86,10 +103,12 @@ struct ChainParams {
     uint64_t cand_ext_cap;     // pairs
     uint64_t* scratch;
     uint64_t scratch_cap;      // u64 words
+    uint64_t* tx_acc;          // per batch: (reads << 40) | score, one atomic per candidate
     uint64_t* tx_reads;
     uint64_t* tx_score;
     uint32_t* ctrl;
     uint32_t* ovf2;
+    int variant;               // chain kernel variant (development A/B; 0 = default)
 };
 
 // records the message returned by skq_last_error(); returns code (skq_capi.hip)
@@ -100,6 +119,16 @@ int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream);
 int launch_chain(const ChainParams& p, void* stream);
 int launch_chain_slow(const ChainParams& p, void* stream);
+int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
+
+#ifdef __HIPCC__
+#define SKQ_HD __host__ __device__
+#else
+#define SKQ_HD
+#endif
+SKQ_HD inline uint32_t home_bucket(uint32_t key, uint32_t nbuckets) {
+    return (uint32_t)(((uint64_t)(uint32_t)(key * HASH_MUL) * nbuckets) >> 32);
+}
 size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap);
 
 // 33-bit ntHash lane (bits 0..32 of ntHash's split rotate evolve on their own)

@@ -4,19 +4,26 @@
 //                  Restates createSketch_FracMinhash_direct (reference src/sketch.cpp:24-39) and
 //                  the read filters of process_fastq_single_pass (src/main.cpp:132-138).
 //                  One workgroup = 256 reads. The workgroup's byte span is staged once into LDS
-//                  with coalesced 16-B loads, converted to 2-bit codes + an invalid-base mask;
-//                  each lane then rolls the 33-bit ntHash lane over its own read.
+//                  with coalesced 16-B loads and converted to 2-bit codes + an invalid-base mask;
+//                  each lane then rolls the 33-bit ntHash lane over its own read, 16 windows per
+//                  step from two funnel-shifted code words (in-bases, out-bases).
 //   k_chain        per read: probe every retained hash in the device index, count per
 //                  (transcript, k), per-k max, keep transcripts with count >= fraction*max at
 //                  every k, score = sum of counts, sort (score desc, tid asc). Restates
-//                  sparse_chain (src/sparse_chaining.cpp:42-111). One lane per read; the count
-//                  table lives in registers (16 transcripts x packed 8-bit counts).
+//                  sparse_chain (src/sparse_chaining.cpp:42-111). One lane per read; each probe
+//                  reads one 64-B bucket mapping keys to postings-list equivalence classes;
+//                  counts are kept per distinct list, then expanded per transcript, in
+//                  register tables (packed 8-bit counts per k).
 //   *_slow         exact fallbacks for what the fast kernels do not bound (reads > 256 bp, more
-//                  than HCAP retained hashes, more than 16 distinct transcripts, > 4 k slots).
-//                  They run over device-side work lists with a fixed grid: no host round trip.
+//                  than HCAP raw retained hashes, more than 8 distinct lists or 16 distinct
+//                  transcripts, > 4 k slots). One workgroup per listed read, sorting in LDS; they walk device-side
+//                  work lists with a fixed grid, so no host round trip is needed.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "skq_internal.h"
+
 
 namespace skq {
 
@@ -46,6 +53,68 @@ __device__ __forceinline__ void bitonic_sort(T (&a)[N]) {
                     else cswap(a[l], a[i]);
                 }
             }
+        }
+    }
+}
+
+// ascending bitonic sort of a[0..n) in LDS by the whole workgroup (n a power of two)
+template <typename T>
+__device__ void block_sort(T* a, uint32_t n) {
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const T x = a[i], y = a[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        a[i] = y;
+                        a[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t pow2_at_least(uint32_t m) {
+    uint32_t n = 1;
+    while (n < m) n <<= 1;
+    return n;
+}
+
+// inclusive scan of one value per thread over the workgroup; also returns the total
+__device__ uint32_t block_incl_scan(uint32_t v, uint32_t* s, uint32_t& total) {
+    const uint32_t t = threadIdx.x;
+    s[t] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
+        const uint32_t add = t >= o ? s[t - o] : 0u;
+        __syncthreads();
+        s[t] += add;
+        __syncthreads();
+    }
+    const uint32_t r = s[t];
+    total = s[blockDim.x - 1];
+    __syncthreads();
+    return r;
+}
+
+// serial shell sort (Ciura gaps) for the rare oversized cases
+template <typename T>
+__device__ void serial_sort(T* a, uint64_t m) {
+    const uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+    for (int g = 0; g < 8; ++g) {
+        const uint64_t gap = gaps[g];
+        for (uint64_t x = gap; x < m; ++x) {
+            const T v = a[x];
+            uint64_t b = x;
+            while (b >= gap && a[b - gap] > v) {
+                a[b] = a[b - gap];
+                b -= gap;
+            }
+            a[b] = v;
         }
     }
 }
@@ -82,14 +151,26 @@ __device__ __forceinline__ void encode4(uint32_t w, uint32_t& codes8, uint32_t& 
     codes8 = (t | (t >> 6) | (t >> 12) | (t >> 18)) & 0xFFu;
 }
 
+// one roll step of the 33-bit lane kept as (lo: bits 0..31, hi: bit 32)
+__device__ __forceinline__ void roll33(uint32_t& lo, uint32_t& hi, uint64_t e) {
+    const uint32_t nlo = (lo << 1) | hi;
+    hi = (lo >> 31) ^ (uint32_t)(e >> 32);
+    lo = nlo ^ (uint32_t)e;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1: sketch
 
+// LDS layout: [tables: nk * 16 u64 (seed(in) ^ rot^k(seed(out))), 4 u64 seeds]
+//             [codes: tile_chunks + 1 u32] [bad: tile_chunks u16, padded to 16 B]
+//             [raw retained: HCAP x WG u32]
+__host__ __device__ inline size_t sketch_tab_bytes(uint32_t nk) { return ((size_t)nk * 16 + 4) * 8; }
+
 size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap) {
-    size_t b = (size_t)nk * 32 * 8;                         // roll tables
-    b += (size_t)tile_chunks * 4;                           // 2-bit codes
-    b += ((size_t)tile_chunks * 2 + 15) & ~(size_t)15;      // invalid-base masks
-    b += (size_t)hcap * WG * 4;                             // raw retained hashes
+    size_t b = sketch_tab_bytes(nk);
+    b += (((size_t)tile_chunks + 1) * 4 + 15) & ~(size_t)15;
+    b += ((size_t)tile_chunks * 2 + 15) & ~(size_t)15;
+    b += (size_t)hcap * WG * 4;
     return b;
 }
 
@@ -97,8 +178,10 @@ template <int HCAP>
 __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* s_tab = reinterpret_cast<uint64_t*>(smem);
-    uint32_t* s_codes = reinterpret_cast<uint32_t*>(smem + (size_t)p.nk * 32 * 8);
-    uint16_t* s_bad = reinterpret_cast<uint16_t*>(s_codes + p.tile_chunks);
+    const uint64_t* s_seed = s_tab + p.nk * 16;
+    uint32_t* s_codes = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(p.nk));
+    uint16_t* s_bad = reinterpret_cast<uint16_t*>(
+        reinterpret_cast<unsigned char*>(s_codes) + ((((size_t)p.tile_chunks + 1) * 4 + 15) & ~(size_t)15));
     uint32_t* s_raw = reinterpret_cast<uint32_t*>(
         reinterpret_cast<unsigned char*>(s_bad) + ((((size_t)p.tile_chunks * 2) + 15) & ~(size_t)15));
 
@@ -106,7 +189,8 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     const uint64_t r0 = (uint64_t)blockIdx.x * WG;
     const uint32_t nr = (uint32_t)min((uint64_t)WG, p.n - r0);
 
-    // workgroup byte span, in 16-byte chunks of the aligned-down base pointer
+    // workgroup byte span, in 16-byte chunks of the aligned-down base pointer (a 16-B aligned
+    // chunk holding at least one byte of the buffer never crosses a page)
     const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
     const uintptr_t abase = base & ~(uintptr_t)15;
     const uint64_t delta = base - abase;
@@ -127,7 +211,8 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
         s_codes[c] = a | (b << 8) | (cc << 16) | (d << 24);
         s_bad[c] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
     }
-    for (uint32_t e = tid; e < p.nk * 32; e += WG) s_tab[e] = p.rolltab[e];
+    if (tid == 0) s_codes[nch] = 0;
+    for (uint32_t e = tid; e < p.nk * 16 + 4; e += WG) s_tab[e] = p.rolltab[e];
     __syncthreads();
 
     if ((uint32_t)tid >= nr) return;
@@ -157,27 +242,45 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
 
     if (!slow && st == SKQ_READ_OK) {
         const uint32_t T = p.threshold;
+        const uint32_t L = (uint32_t)len;
+        // 16 codes starting at tile base q, funnel-shifted out of two code words
+        auto codes16 = [&](uint32_t q) -> uint32_t {
+            const uint32_t d = q >> 4;
+            return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
+        };
         for (uint32_t i = 0; i < p.nk && !slow; ++i) {
             const uint32_t k = p.ks[i];
-            const uint64_t* tab = s_tab + i * 32;
-            uint32_t hlo = 0, hhi = 0, nraw = 0;
-            // h <- rot33(h) ^ seed(in) ^ rot33^k(seed(out)); the first k steps have no out base,
-            // which builds the first window's hash from zero (NtHash::init).
-            for (uint32_t pos = 0; pos < (uint32_t)len; ++pos) {
-                const uint64_t qi = q0 + pos;
-                const uint32_t cin = (s_codes[qi >> 4] >> ((qi & 15) * 2)) & 3u;
-                uint32_t cout = 4u;
-                if (pos >= k) {
-                    const uint64_t qo = qi - k;
-                    cout = (s_codes[qo >> 4] >> ((qo & 15) * 2)) & 3u;
-                }
-                const uint64_t e = tab[cin * 8 + cout];
-                const uint32_t nlo = (hlo << 1) | hhi;
-                hhi = (hlo >> 31) ^ (uint32_t)(e >> 32);
-                hlo = nlo ^ (uint32_t)e;
-                if (pos + 1 >= k && hlo <= T) {  // src/sketch.cpp:33-35
-                    if (nraw < HCAP) s_raw[nraw * WG + tid] = hlo;
-                    ++nraw;
+            const uint64_t* tab = s_tab + i * 16;
+            // first window (NtHash::init): h = XOR_j rot^(k-1-j) seed(s_j)
+            uint32_t hlo = 0, hhi = 0;
+            for (uint32_t b = 0; b < k; b += 16) {
+                const uint32_t w = codes16((uint32_t)q0 + b);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (b + j < k) roll33(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
+            }
+            uint32_t nraw = 0;
+            if (hlo <= T) {  // src/sketch.cpp:33-35
+                s_raw[tid] = hlo;
+                nraw = 1;
+            }
+            // windows 1..nw-1: in-base at w + k - 1, out-base at w - 1
+            const uint32_t nw = L - k + 1;
+            const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
+            for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
+                const uint32_t win = codes16(qin + w0 - 1);
+                const uint32_t wout = codes16(qout + w0 - 1);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if (w0 + j < nw) {
+                        const uint32_t ci = (win >> (2 * j)) & 3u;
+                        const uint32_t co = (wout >> (2 * j)) & 3u;
+                        roll33(hlo, hhi, tab[ci * 4 + co]);
+                        if (hlo <= T) {
+                            if (nraw < HCAP) s_raw[nraw * WG + tid] = hlo;
+                            ++nraw;
+                        }
+                    }
                 }
             }
             if (nraw > HCAP) {
@@ -189,116 +292,271 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
             bitonic_sort<HCAP>(v);
-            uint32_t* out = p.hashes + (r * p.nk + i) * p.hcap;
+            // SoA layout: value j of (read r, k slot i) at hashes[(i*hcap + j)*n + r], so the
+            // wave's stores of one j are contiguous
+            uint32_t* out = p.hashes + (uint64_t)i * p.hcap * p.n + r;
             uint32_t m = 0;
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) {
                 const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
-                if (keep) out[m++] = v[j];
+                if (keep) out[(uint64_t)(m++) * p.n] = v[j];
             }
-            p.hash_cnt[r * p.nk + i] = m;
+            p.hash_cnt[(uint64_t)i * p.n + r] = m;
         }
     }
     if (slow) {
         st = ST_SLOW1;
         list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
     } else if (st != SKQ_READ_OK) {
-        for (uint32_t i = 0; i < p.nk; ++i) p.hash_cnt[r * p.nk + i] = 0;
+        for (uint32_t i = 0; i < p.nk; ++i) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
     }
     p.status[r] = st;
 }
 
-// Slow sketch path: one lane per listed read, straight from global memory. Retained hashes go
-// to a bump-allocated region sized by the read's window count, then are sorted in place.
-__global__ __launch_bounds__(64) void k_sketch_slow(SketchParams p) {
+// Slow sketch path: one workgroup per listed read. Windows are split into one contiguous
+// segment per thread (each thread rebuilds its segment's first hash, then rolls); retained
+// hashes land in LDS (and in a bump-allocated global region beyond SLOW_CAP), then are sorted
+// and de-duplicated by the workgroup.
+constexpr uint32_t SLOW_CAP = 4096;
+
+__global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
+    __shared__ uint32_t s_buf[SLOW_CAP];
+    __shared__ uint32_t s_scan[WG];
+    __shared__ uint32_t s_cnt, s_bad;
+    __shared__ unsigned long long s_at;
+    const uint32_t t = threadIdx.x;
     const uint32_t cnt = min(p.ctrl[C_OVF1], p.ovf_cap);
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
+    unsigned long long* bump = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
+    const uint64_t* seed = p.rolltab + p.nk * 16;
+    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
         const uint64_t r = p.ovf1[j];
         uint64_t start, len;
         read_extent(p.offs, p.fixed_len, r, start, len);
         const uint8_t* s = p.reads + start;
+        if (t == 0) s_bad = 0;
+        __syncthreads();
         bool bad = false;
-        for (uint64_t q = 0; q < len && !bad; ++q) {
+        for (uint64_t q = t; q < len; q += WG) {
             const uint8_t c = s[q];
-            bad = !(c == 'A' || c == 'C' || c == 'G' || c == 'T');
+            bad |= !(c == 'A' || c == 'C' || c == 'G' || c == 'T');
         }
-        uint8_t st = bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
-        for (uint32_t i = 0; i < p.nk; ++i) p.hash_cnt[r * p.nk + i] = 0;
+        if (bad) s_bad = 1;
+        __syncthreads();
+        const uint8_t st = s_bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
+        for (uint32_t i = t; i < p.nk; i += WG) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
         if (st == SKQ_READ_OK) {
             for (uint32_t i = 0; i < p.nk; ++i) {
                 const uint32_t k = p.ks[i];
                 const uint64_t nw = len - k + 1;
-                unsigned long long* bump = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
-                const uint64_t at = atomicAdd(bump, (unsigned long long)nw);
-                if (at + nw > p.hash_ext_cap) {
-                    atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
-                    break;
-                }
-                uint32_t* ext = p.hash_ext + at;
-                const uint64_t* tab = p.rolltab + i * 32;
-                uint32_t hlo = 0, hhi = 0;
-                uint64_t m = 0;
-                for (uint64_t pos = 0; pos < len; ++pos) {
-                    const uint32_t cin = (s[pos] >> 1) & 3u;
-                    const uint32_t cout = pos >= k ? ((s[pos - k] >> 1) & 3u) : 4u;
-                    const uint64_t e = tab[cin * 8 + cout];
-                    const uint32_t nlo = (hlo << 1) | hhi;
-                    hhi = (hlo >> 31) ^ (uint32_t)(e >> 32);
-                    hlo = nlo ^ (uint32_t)e;
-                    if (pos + 1 >= k && hlo <= p.threshold) ext[m++] = hlo;
-                }
-                // shell sort (Ciura gaps) + unique, in place
-                const uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
-                for (int g = 0; g < 8; ++g) {
-                    const uint64_t gap = gaps[g];
-                    for (uint64_t a = gap; a < m; ++a) {
-                        const uint32_t x = ext[a];
-                        uint64_t b = a;
-                        while (b >= gap && ext[b - gap] > x) {
-                            ext[b] = ext[b - gap];
-                            b -= gap;
-                        }
-                        ext[b] = x;
+                __syncthreads();
+                if (t == 0) {
+                    s_cnt = 0;
+                    s_at = ~0ull;
+                    if (nw > SLOW_CAP) {
+                        const unsigned long long at = atomicAdd(bump, (unsigned long long)nw);
+                        if (at + nw <= p.hash_ext_cap) s_at = at;
+                        else atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                     }
                 }
-                uint64_t u = 0;
-                for (uint64_t a = 0; a < m; ++a)
-                    if (a == 0 || ext[a] != ext[u - 1]) ext[u++] = ext[a];
-                uint32_t* slot = p.hashes + (r * p.nk + i) * p.hcap;
-                if (u <= p.hcap) {
-                    for (uint64_t a = 0; a < u; ++a) slot[a] = ext[a];
-                } else {
-                    slot[0] = (uint32_t)at;
+                __syncthreads();
+                if (nw > SLOW_CAP && s_at == ~0ull) continue;  // uniform; error recorded
+                uint32_t* ext = nw > SLOW_CAP ? p.hash_ext + s_at : nullptr;
+                uint32_t* buf = ext ? ext : s_buf;
+                const uint64_t* tab = p.rolltab + i * 16;
+                const uint64_t seg = (nw + WG - 1) / WG;
+                const uint64_t wa = t * seg, wb = min(nw, wa + seg);
+                if (wa < wb) {
+                    uint32_t hlo = 0, hhi = 0;
+                    for (uint64_t q = 0; q < k; ++q) roll33(hlo, hhi, seed[(s[wa + q] >> 1) & 3u]);
+                    for (uint64_t w = wa; w < wb; ++w) {
+                        if (w > wa)
+                            roll33(hlo, hhi, tab[((s[w + k - 1] >> 1) & 3u) * 4 + ((s[w - 1] >> 1) & 3u)]);
+                        if (hlo <= p.threshold) buf[atomicAdd(&s_cnt, 1u)] = hlo;
+                    }
                 }
-                p.hash_cnt[r * p.nk + i] = (uint32_t)u;
+                __syncthreads();
+                const uint32_t m = s_cnt;
+                uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * p.n + r;  // stride p.n
+                if (!ext) {
+                    const uint32_t n2 = pow2_at_least(m);
+                    for (uint32_t x = m + t; x < n2; x += WG) s_buf[x] = 0xFFFFFFFFu;
+                    __syncthreads();
+                    block_sort(s_buf, n2);
+                    // keep the first of every run; write the unique values to their destination
+                    const uint32_t per = (m + WG - 1) / WG;
+                    const uint32_t a = min(m, t * per), b = min(m, a + per);
+                    uint32_t mine = 0;
+                    for (uint32_t x = a; x < b; ++x) mine += (x == 0 || s_buf[x] != s_buf[x - 1]);
+                    uint32_t u = 0;
+                    const uint32_t incl = block_incl_scan(mine, s_scan, u);
+                    uint32_t* dst = slot;
+                    uint64_t dstride = p.n;
+                    if (u > p.hcap) {
+                        if (t == 0) {
+                            s_at = ~0ull;
+                            const unsigned long long at = atomicAdd(bump, (unsigned long long)u);
+                            if (at + u <= p.hash_ext_cap) s_at = at;
+                            else atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
+                        }
+                        __syncthreads();
+                        if (s_at == ~0ull) continue;  // uniform
+                        dst = p.hash_ext + s_at;
+                        dstride = 1;
+                        if (t == 0) slot[0] = (uint32_t)s_at;
+                    }
+                    uint32_t o = incl - mine;
+                    for (uint32_t x = a; x < b; ++x)
+                        if (x == 0 || s_buf[x] != s_buf[x - 1]) dst[(uint64_t)(o++) * dstride] = s_buf[x];
+                    if (t == 0) p.hash_cnt[(uint64_t)i * p.n + r] = u;
+                } else if (t == 0) {  // more windows than LDS holds: serial, in place
+                    serial_sort(ext, m);
+                    uint32_t u = 0;
+                    for (uint32_t x = 0; x < m; ++x)
+                        if (x == 0 || ext[x] != ext[u - 1]) ext[u++] = ext[x];
+                    if (u <= p.hcap) {
+                        for (uint32_t x = 0; x < u; ++x) slot[(uint64_t)x * p.n] = ext[x];
+                    } else {
+                        slot[0] = (uint32_t)s_at;
+                    }
+                    p.hash_cnt[(uint64_t)i * p.n + r] = u;
+                }
             }
         }
-        p.status[r] = st;
+        if (t == 0) p.status[r] = st;
+        __syncthreads();
     }
 }
 
 // ---------------------------------------------------------------------------------------------
 // K2: chain
 
+// the read's hash list at k slot i: (pointer, stride)
+__device__ __forceinline__ uint32_t hash_count(const ChainParams& p, uint64_t r, uint32_t i) {
+    return p.hash_offs ? p.hash_cnt[r * p.nk + i] : p.hash_cnt[(uint64_t)i * p.n + r];
+}
+
 __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint64_t r, uint32_t i,
-                                                     uint32_t cnt) {
+                                                     uint32_t cnt, uint64_t& stride) {
+    stride = 1;
     if (p.hash_offs) return p.hashes + p.hash_offs[r * p.nk + i];
-    const uint32_t* slot = p.hashes + (r * p.nk + i) * p.hcap;
-    return cnt <= p.hcap ? slot : p.hash_ext + slot[0];
-}
-
-// returns the postings offset of `key` in table t, or ~0u on a miss
-__device__ __forceinline__ uint32_t probe(const uint64_t* slots, const DevTable& t, uint32_t key) {
-    const uint64_t mask = (1ull << t.log2cap) - 1;
-    uint64_t s = (uint32_t)(key * HASH_MUL) >> (32 - t.log2cap);
-    for (;;) {
-        const uint64_t v = slots[t.slot_base + s];
-        if (v == EMPTY_SLOT) return ~0u;
-        if ((uint32_t)(v >> 32) == key) return (uint32_t)v;
-        s = (s + 1) & mask;
+    const uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * p.n + r;
+    if (cnt <= p.hcap) {
+        stride = p.n;
+        return slot;
     }
+    return p.hash_ext + slot[0];
 }
 
+// scalar probe (slow path): postings of `key` as (pointer, count)
+__device__ bool probe_list(const ChainParams& p, const DevTable& t, uint32_t key, const uint32_t*& ptr,
+                           uint32_t& n) {
+    uint32_t b = home_bucket(key, t.nbuckets);
+    for (uint32_t q = 0; q < t.max_probe; ++q) {
+        const uint32_t* B = p.buckets + (t.bucket_base + b) * BUCKET_WORDS;
+        const uint32_t hdr = B[0];
+        const uint32_t m = hdr & 7u;
+        for (uint32_t j = 0; j < m; ++j) {
+            if (B[1 + j] == key) {
+                const uint32_t* L = p.lists + B[BUCKET_LIST0 + j];
+                n = L[0];
+                ptr = L + 1;
+                return true;
+            }
+        }
+        if (!((hdr >> 3) & 1u)) return false;
+        b = b + 1 == t.nbuckets ? 0 : b + 1;
+    }
+    return false;
+}
+
+// Count table in registers: N (id, packed per-k counts) entries in banks of 4. A bank is
+// compared only when some lane of the wave uses it (wave-uniform test).
+template <int N>
+struct CountTable {
+    uint32_t ids[N], cnts[N];
+    uint32_t nd;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            ids[d] = 0xFFFFFFFFu;
+            cnts[d] = 0;
+        }
+        nd = 0;
+    }
+    // cnts[id] += inc (packed bytes); false when an (N+1)th distinct id shows up
+    __device__ __forceinline__ bool add(uint32_t x, uint32_t inc) {
+        bool found = false;
+#pragma unroll
+        for (int bank = 0; bank < N / 4; ++bank) {
+            if (bank == 0 || __any(nd > 4u * bank)) {
+#pragma unroll
+                for (int d = 4 * bank; d < 4 * bank + 4; ++d) {
+                    const bool hit = ids[d] == x;
+                    cnts[d] += hit ? inc : 0u;
+                    found |= hit;
+                }
+            }
+        }
+        if (__all(found)) return true;
+        if (!found && nd == (uint32_t)N) return false;
+#pragma unroll
+        for (int bank = 0; bank < N / 4; ++bank) {
+            if (__any(!found && (nd >> 2) == (uint32_t)bank)) {
+#pragma unroll
+                for (int d = 4 * bank; d < 4 * bank + 4; ++d) {
+                    if (!found && (uint32_t)d == nd) {
+                        ids[d] = x;
+                        cnts[d] = inc;
+                    }
+                }
+            }
+        }
+        nd += found ? 0u : 1u;
+        return true;
+    }
+};
+
+constexpr int DLISTS = 8;  // distinct postings lists per read on the fast path
+
+// Probe `key` (one 64-B bucket, 4 x 16-B loads of the same line; further buckets only while
+// the bucket is marked "continue"): returns the key's list offset, or ~0u on a miss.
+__device__ __forceinline__ uint32_t probe_ec(const uint32_t* tb, const DevTable& t, uint32_t key) {
+    uint32_t b = home_bucket(key, t.nbuckets);
+    for (uint32_t q = 0; q < t.max_probe; ++q) {
+        const uint4* B = reinterpret_cast<const uint4*>(tb + (uint64_t)b * BUCKET_WORDS);
+        const uint4 w0 = B[0], w1 = B[1], w2 = B[2], w3 = B[3];
+        const uint32_t m = w0.x & 7u;
+        const uint32_t keys[7] = {w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const uint32_t los[7] = {w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z};
+        uint32_t lo = ~0u;
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+            if ((uint32_t)j < m && keys[j] == key) lo = los[j];
+        if (lo != ~0u || !((w0.x >> 3) & 1u)) return lo;
+        b = b + 1 == t.nbuckets ? 0 : b + 1;
+    }
+    return ~0u;
+}
+
+// value `i` (lane-varying, < 8) of an 8-entry register array, via bit-mask selects (a ?: tree
+// would become an address select and push the array to scratch)
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t one, uint32_t zero) {
+    return (one & m) | (zero & ~m);
+}
+__device__ __forceinline__ uint32_t pick8(const uint32_t (&w)[8], uint32_t i) {
+    const uint32_t m0 = 0u - (i & 1u), m1 = 0u - ((i >> 1) & 1u), m2 = 0u - ((i >> 2) & 1u);
+    uint32_t a[4], b[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = bsel(m0, w[2 * q + 1], w[2 * q]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) b[q] = bsel(m1, a[2 * q + 1], a[2 * q]);
+    return bsel(m2, b[1], b[0]);
+}
+
+// Fast chain kernel: one lane per read. Probes give list offsets, counted per distinct list
+// (usually 1-3); each distinct list is then expanded into the per-transcript table with its
+// packed per-k counts: count(t, k) = sum over distinct lists L containing t of count(L, k),
+// exactly the reference's per-posting count.
 __global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
     if (r >= p.n) return;
@@ -306,64 +564,46 @@ __global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
         p.cand_cnt[r] = 0;
         return;
     }
-    uint32_t tids[DCAP], cnts[DCAP];
-#pragma unroll
-    for (int d = 0; d < DCAP; ++d) {
-        tids[d] = 0xFFFFFFFFu;
-        cnts[d] = 0;
-    }
-    uint32_t nd = 0;
+    CountTable<DLISTS> lt;  // list offset -> packed per-k counts
+    lt.init();
     bool slow = p.nk > (uint32_t)NK_FAST;
 
     for (uint32_t i = 0; i < p.nk && !slow; ++i) {
         const DevTable t = p.tabs[i];
         if (!t.present) continue;
         if (p.present && !p.present[r * p.nk + i]) continue;
-        const uint32_t cnt = p.hash_cnt[r * p.nk + i];
-        if (cnt > (uint32_t)HFAST) {
+        const uint32_t cnt = hash_count(p, r, i);
+        if (cnt > (uint32_t)HFAST) {  // counts are packed 8 bits per k
             slow = true;
             break;
         }
-        const uint32_t* hs = hash_list(p, r, i, cnt);
+        uint64_t hstride;
+        const uint32_t* hs = hash_list(p, r, i, cnt, hstride);
         const uint32_t inc = 1u << (8 * i);
-        for (uint32_t j0 = 0; j0 < cnt && !slow; j0 += 4) {
-            // issue up to 4 independent probes, then their postings headers
-            uint32_t off[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) off[u] = (j0 + u < cnt) ? probe(p.slots, t, hs[j0 + u]) : ~0u;
-            uint4 head[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                head[u] = off[u] != ~0u ? *reinterpret_cast<const uint4*>(p.post + off[u])
-                                        : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t np = head[u].x;
-                for (uint32_t e = 0; e < np; ++e) {
-                    const uint32_t x = e == 0 ? head[u].y : e == 1 ? head[u].z : e == 2 ? head[u].w
-                                                                                         : p.post[off[u] + 1 + e];
-                    bool found = false;
-#pragma unroll
-                    for (int d = 0; d < DCAP; ++d) {
-                        const bool hit = tids[d] == x;
-                        cnts[d] += hit ? inc : 0u;
-                        found |= hit;
-                    }
-                    if (!found) {
-                        if (nd == (uint32_t)DCAP) {
-                            slow = true;
-                            break;
-                        }
-#pragma unroll
-                        for (int d = 0; d < DCAP; ++d) {
-                            if ((uint32_t)d == nd) {
-                                tids[d] = x;
-                                cnts[d] = inc;
-                            }
-                        }
-                        ++nd;
-                    }
-                }
+        const uint32_t* tb = p.buckets + t.bucket_base * BUCKET_WORDS;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t lo = probe_ec(tb, t, hs[j * hstride]);
+            if (lo != ~0u && !lt.add(lo, inc)) {
+                slow = true;
+                break;
+            }
+        }
+    }
+    CountTable<DCAP> tab;  // transcript -> packed per-k counts
+    tab.init();
+    // expand the distinct lists (wave-uniform trip count)
+    for (uint32_t e = 0; e < (uint32_t)DLISTS && !slow; ++e) {
+        if (!__any(e < lt.nd && !slow)) break;
+        if (e >= lt.nd || slow) continue;
+        const uint32_t lo = pick8(lt.ids, e);
+        const uint32_t inc = pick8(lt.cnts, e);
+        const uint4 head = *reinterpret_cast<const uint4*>(p.lists + lo);
+        const uint32_t n = head.x;
+        for (uint32_t q = 0; q < n; ++q) {
+            const uint32_t x = q == 0 ? head.y : q == 1 ? head.z : q == 2 ? head.w : p.lists[lo + 1 + q];
+            if (!tab.add(x, inc)) {
+                slow = true;
+                break;
             }
         }
     }
@@ -372,171 +612,220 @@ __global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
         p.cand_cnt[r] = 0;
         return;
     }
-
     // per-k maximum (src/sparse_chaining.cpp:76-82) and the integer form of the double
     // threshold: (double)c >= fraction * max  <=>  c >= ceil(fraction * max)   (:84-87, :93)
-    // (counts here are <= HFAST, so a threshold clamped to 255 rejects the same transcripts; a
+    // (counts here are <= 255, so a threshold clamped to 256 rejects the same transcripts; a
     // NaN or non-positive threshold accepts everything, as `c < thr` is then false.)
-    uint32_t need = 0;  // packed per-k ceil thresholds
-    for (uint32_t i = 0; i < p.nk; ++i) {
+    uint32_t need[NK_FAST];
+#pragma unroll
+    for (int i = 0; i < NK_FAST; ++i) {
         uint32_t m = 0;
 #pragma unroll
-        for (int d = 0; d < DCAP; ++d) m = max(m, (cnts[d] >> (8 * i)) & 0xFFu);
+        for (int d = 0; d < DCAP; ++d) m = max(m, (tab.cnts[d] >> (8 * i)) & 0xFFu);
         const double thr = p.fraction * (double)m;
         uint32_t ti = 0;
-        if (thr > 0.0) ti = thr >= 255.0 ? 255u : (uint32_t)ceil(thr);
-        need |= ti << (8 * i);
+        if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+        need[i] = (uint32_t)i < p.nk ? ti : 0u;
     }
     uint64_t key[DCAP];
 #pragma unroll
     for (int d = 0; d < DCAP; ++d) {
-        bool ok = (uint32_t)d < nd;
+        bool ok = (uint32_t)d < tab.nd;
         uint32_t score = 0;
-        for (uint32_t i = 0; i < p.nk; ++i) {
-            const uint32_t c = (cnts[d] >> (8 * i)) & 0xFFu;
-            ok &= c >= ((need >> (8 * i)) & 0xFFu);
+#pragma unroll
+        for (int i = 0; i < NK_FAST; ++i) {
+            const uint32_t c = (tab.cnts[d] >> (8 * i)) & 0xFFu;
+            ok &= c >= need[i];
             score += c;
         }
         // sort key: score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
-        key[d] = ok ? (((uint64_t)(0xFFFFFFFFu - score) << 32) | tids[d]) : ~0ull;
+        key[d] = ok ? (((uint64_t)(0xFFFFFFFFu - score) << 32) | tab.ids[d]) : ~0ull;
     }
     bitonic_sort<DCAP>(key);
     uint32_t nc = 0;
-    uint32_t* ct = p.cand_tid + r * CCAP;
-    uint32_t* cs = p.cand_score + r * CCAP;
+    // SoA layout: candidate j of read r at cand_tid[j*n + r]
+    uint32_t* ct = p.cand_tid + r;
+    uint32_t* cs = p.cand_score + r;
 #pragma unroll
     for (int d = 0; d < DCAP; ++d) {
         if (key[d] != ~0ull) {
             const uint32_t tid = (uint32_t)key[d];
             const uint32_t score = 0xFFFFFFFFu - (uint32_t)(key[d] >> 32);
-            ct[d] = tid;
-            cs[d] = score;
+            ct[(uint64_t)d * p.n] = tid;
+            cs[(uint64_t)d * p.n] = score;
             ++nc;
-            if (p.accumulate) {
-                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid]), 1ull);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
-            }
+            // one packed atomic per candidate: reads in bits 40+, score below (<= 1020 per read)
+            if (p.accumulate)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[tid]), (1ull << 40) | score);
         }
     }
     p.cand_cnt[r] = nc;
 }
 
-// Slow chain path: one lane per listed read. Postings are gathered into a bump-allocated
-// scratch of (tid << 3 | k slot) words, sorted, run-length counted.
-__device__ void shell_sort_u64(uint64_t* a, uint64_t m) {
-    const uint32_t gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
-    for (int g = 0; g < 8; ++g) {
-        const uint64_t gap = gaps[g];
-        for (uint64_t x = gap; x < m; ++x) {
-            const uint64_t v = a[x];
-            uint64_t b = x;
-            while (b >= gap && a[b - gap] > v) {
-                a[b] = a[b - gap];
-                b -= gap;
-            }
-            a[b] = v;
-        }
-    }
-}
-
-__global__ __launch_bounds__(64) void k_chain_slow(ChainParams p) {
+// Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
+// LDS (global scratch beyond SLOW_CAP), sorted, and counted per transcript run.
+__global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
+    __shared__ uint64_t s_ent[SLOW_CAP];
+    __shared__ uint32_t s_max[SKQ_MAX_K];
+    __shared__ uint32_t s_cnt, s_nc;
+    __shared__ unsigned long long s_at;
+    const uint32_t t = threadIdx.x;
     const uint32_t cnt = min(p.ctrl[C_OVF2], p.ovf_cap);
     unsigned long long* bump_s = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_S);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_C);
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
+    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
         const uint64_t r = p.ovf2[j];
-        // pass 1: size
-        uint64_t P = 0;
+        __syncthreads();
+        // pass 1: postings count P
+        if (t == 0) s_cnt = 0;
+        if (t < SKQ_MAX_K) s_max[t] = 0;
+        __syncthreads();
         for (uint32_t i = 0; i < p.nk; ++i) {
             if (!p.tabs[i].present || (p.present && !p.present[r * p.nk + i])) continue;
-            const uint32_t hc = p.hash_cnt[r * p.nk + i];
-            const uint32_t* hs = hash_list(p, r, i, hc);
-            for (uint32_t h = 0; h < hc; ++h) {
-                const uint32_t off = probe(p.slots, p.tabs[i], hs[h]);
-                if (off != ~0u) P += p.post[off];
+            const uint32_t hc = hash_count(p, r, i);
+            uint64_t hstride;
+            const uint32_t* hs = hash_list(p, r, i, hc, hstride);
+            uint32_t mine = 0;
+            for (uint32_t h = t; h < hc; h += WG) {
+                const uint32_t* pp;
+                uint32_t np;
+                if (probe_list(p, p.tabs[i], hs[h * hstride], pp, np)) mine += np;
             }
+            if (mine) atomicAdd(&s_cnt, mine);
         }
-        const uint64_t need = 2 * P + 1;
-        const uint64_t at = atomicAdd(bump_s, (unsigned long long)need);
-        if (at + need > p.scratch_cap) {
-            atomicOr(&p.ctrl[C_ERR2], (uint32_t)E_SCRATCH);
-            p.cand_cnt[r] = 0;
+        __syncthreads();
+        const uint32_t P = s_cnt;
+        // entries + candidates: LDS when 2P fits, else 2P words of global scratch
+        const bool in_lds = 2 * (uint64_t)P <= SLOW_CAP;
+        __syncthreads();
+        if (t == 0) {
+            s_at = 0;
+            if (!in_lds) {
+                const unsigned long long at = atomicAdd(bump_s, (unsigned long long)(2 * (uint64_t)P + 1));
+                if (at + 2 * (uint64_t)P + 1 <= p.scratch_cap) s_at = at;
+                else {
+                    atomicOr(&p.ctrl[C_ERR2], (uint32_t)E_SCRATCH);
+                    s_at = ~0ull;
+                }
+            }
+            s_cnt = 0;
+            s_nc = 0;
+        }
+        __syncthreads();
+        if (s_at == ~0ull) {
+            if (t == 0) p.cand_cnt[r] = 0;
             continue;
         }
-        uint64_t* ent = p.scratch + at;
-        uint64_t* cand = ent + P;
-        uint64_t e = 0;
+        uint64_t* ent = in_lds ? s_ent : p.scratch + s_at;
+        // pass 2: gather
         for (uint32_t i = 0; i < p.nk; ++i) {
             if (!p.tabs[i].present || (p.present && !p.present[r * p.nk + i])) continue;
-            const uint32_t hc = p.hash_cnt[r * p.nk + i];
-            const uint32_t* hs = hash_list(p, r, i, hc);
-            for (uint32_t h = 0; h < hc; ++h) {
-                const uint32_t off = probe(p.slots, p.tabs[i], hs[h]);
-                if (off == ~0u) continue;
-                const uint32_t np = p.post[off];
-                for (uint32_t q = 0; q < np; ++q) ent[e++] = ((uint64_t)p.post[off + 1 + q] << 8) | i;
+            const uint32_t hc = hash_count(p, r, i);
+            uint64_t hstride;
+            const uint32_t* hs = hash_list(p, r, i, hc, hstride);
+            for (uint32_t h = t; h < hc; h += WG) {
+                const uint32_t* pp;
+                uint32_t np;
+                if (!probe_list(p, p.tabs[i], hs[h * hstride], pp, np)) continue;
+                const uint32_t at = atomicAdd(&s_cnt, np);
+                for (uint32_t q = 0; q < np; ++q) ent[at + q] = ((uint64_t)pp[q] << 8) | i;
             }
         }
-        shell_sort_u64(ent, P);
-        uint32_t maxc[SKQ_MAX_K];
-        for (uint32_t i = 0; i < p.nk; ++i) maxc[i] = 0;
-        for (uint64_t a = 0; a < P;) {
-            uint64_t b = a;
-            const uint64_t t = ent[a] >> 8;
-            uint32_t c[SKQ_MAX_K];
-            for (uint32_t i = 0; i < p.nk; ++i) c[i] = 0;
-            while (b < P && (ent[b] >> 8) == t) c[ent[b++] & 0xFF]++;
-            for (uint32_t i = 0; i < p.nk; ++i) maxc[i] = max(maxc[i], c[i]);
-            a = b;
+        __syncthreads();
+        uint32_t n2 = pow2_at_least(P);
+        if (in_lds && n2 <= SLOW_CAP) {
+            for (uint32_t x = P + t; x < n2; x += WG) s_ent[x] = ~0ull;
+            __syncthreads();
+            block_sort(s_ent, n2);
+        } else {
+            if (t == 0) serial_sort(ent, P);
+            __syncthreads();
         }
-        double thr[SKQ_MAX_K];
-        for (uint32_t i = 0; i < p.nk; ++i) thr[i] = p.fraction * (double)maxc[i];
-        uint64_t nc = 0;
-        for (uint64_t a = 0; a < P;) {
-            uint64_t b = a;
-            const uint64_t t = ent[a] >> 8;
+        // per-transcript runs: the thread owning a run's first word counts it
+        for (uint32_t a = t; a < P; a += WG) {
+            if (a > 0 && (ent[a] >> 8) == (ent[a - 1] >> 8)) continue;
             uint32_t c[SKQ_MAX_K];
             for (uint32_t i = 0; i < p.nk; ++i) c[i] = 0;
-            while (b < P && (ent[b] >> 8) == t) c[ent[b++] & 0xFF]++;
+            for (uint32_t b = a; b < P && (ent[b] >> 8) == (ent[a] >> 8); ++b) c[ent[b] & 0xFF]++;
+            for (uint32_t i = 0; i < p.nk; ++i) atomicMax(&s_max[i], c[i]);
+        }
+        __syncthreads();
+        double thr[SKQ_MAX_K];
+        for (uint32_t i = 0; i < p.nk; ++i) thr[i] = p.fraction * (double)s_max[i];
+        uint64_t* cand = ent + P;
+        for (uint32_t a = t; a < P; a += WG) {
+            if (a > 0 && (ent[a] >> 8) == (ent[a - 1] >> 8)) continue;
+            uint32_t c[SKQ_MAX_K];
+            for (uint32_t i = 0; i < p.nk; ++i) c[i] = 0;
+            for (uint32_t b = a; b < P && (ent[b] >> 8) == (ent[a] >> 8); ++b) c[ent[b] & 0xFF]++;
             bool ok = true;
             uint32_t score = 0;
-            for (uint32_t i = 0; i < p.nk; ++i) {
-                if ((double)c[i] < thr[i]) { ok = false; break; }
+            for (uint32_t i = 0; i < p.nk; ++i) {  // src/sparse_chaining.cpp:91-101
+                if ((double)c[i] < thr[i]) {
+                    ok = false;
+                    break;
+                }
                 score += c[i];
             }
-            if (ok) cand[nc++] = ((uint64_t)(0xFFFFFFFFu - score) << 32) | (uint32_t)t;
-            a = b;
+            if (ok) cand[atomicAdd(&s_nc, 1u)] = ((uint64_t)(0xFFFFFFFFu - score) << 32) | (uint32_t)(ent[a] >> 8);
         }
-        shell_sort_u64(cand, nc);
-        uint32_t* ct;
-        uint32_t* cs;
-        uint64_t stride = 1;
-        if (nc <= (uint64_t)CCAP) {
-            ct = p.cand_tid + r * CCAP;
-            cs = p.cand_score + r * CCAP;
+        __syncthreads();
+        const uint32_t nc = s_nc;
+        n2 = pow2_at_least(nc);
+        if (in_lds && P + n2 <= SLOW_CAP) {
+            for (uint32_t x = nc + t; x < n2; x += WG) cand[x] = ~0ull;
+            __syncthreads();
+            block_sort(cand, n2);
         } else {
-            const uint64_t cat = atomicAdd(bump_c, (unsigned long long)nc);
-            if (cat + nc > p.cand_ext_cap) {
-                atomicOr(&p.ctrl[C_ERR2], (uint32_t)E_CAND_EXT);
-                p.cand_cnt[r] = 0;
+            if (t == 0) serial_sort(cand, nc);
+            __syncthreads();
+        }
+        uint32_t* ct = p.cand_tid + r;
+        uint32_t* cs = p.cand_score + r;
+        uint64_t stride = p.n;
+        if (nc > (uint32_t)CCAP) {
+            if (t == 0) {
+                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)nc);
+                if (at + nc <= p.cand_ext_cap) {
+                    s_at = at;
+                    p.cand_tid[r] = (uint32_t)at;
+                } else {
+                    atomicOr(&p.ctrl[C_ERR2], (uint32_t)E_CAND_EXT);
+                    s_at = ~0ull;
+                }
+            }
+            __syncthreads();
+            if (s_at == ~0ull) {
+                if (t == 0) p.cand_cnt[r] = 0;
                 continue;
             }
-            p.cand_tid[r * CCAP] = (uint32_t)cat;
-            ct = p.cand_ext + 2 * cat;
+            ct = p.cand_ext + 2 * s_at;
             cs = ct + 1;
             stride = 2;
         }
-        for (uint64_t a = 0; a < nc; ++a) {
+        for (uint32_t a = t; a < nc; a += WG) {
             const uint32_t tid = (uint32_t)cand[a];
             const uint32_t score = 0xFFFFFFFFu - (uint32_t)(cand[a] >> 32);
             ct[a * stride] = tid;
             cs[a * stride] = score;
-            if (p.accumulate) {
+            if (p.accumulate) {  // not packed: slow-path scores are unbounded
                 atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid]), 1ull);
                 atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
             }
         }
-        p.cand_cnt[r] = (uint32_t)nc;
+        if (t == 0) p.cand_cnt[r] = nc;
+    }
+}
+
+// per-batch packed totals -> running (reads, score) totals
+__global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx) {
+    for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < ntx; t += gridDim.x * WG) {
+        const uint64_t a = acc[t];
+        if (a) {
+            reads[t] += a >> 40;
+            score[t] += a & ((1ull << 40) - 1);
+            acc[t] = 0;
+        }
     }
 }
 
@@ -566,7 +855,7 @@ int launch_sketch(const SketchParams& p, void* stream) {
 
 int launch_sketch_slow(const SketchParams& p, void* stream) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_sketch_slow, dim3(256), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_sketch_slow, dim3(512), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -579,7 +868,15 @@ int launch_chain(const ChainParams& p, void* stream) {
 
 int launch_chain_slow(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_chain_slow, dim3(256), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_chain_slow, dim3(512), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream) {
+    if (ntx == 0) return 0;
+    const unsigned grid = (unsigned)std::min<uint32_t>((ntx + WG - 1) / WG, 1024);
+    hipLaunchKernelGGL(k_fold_totals, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), acc, reads,
+                       score, ntx);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

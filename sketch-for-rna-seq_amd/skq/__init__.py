@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libskq.so")
+LIB_PATH = os.environ.get("SKQ_LIB") or os.path.join(PKG_DIR, "lib", "libskq.so")  # SKQ_LIB: dev builds
 
 SKQ_MAX_K = 8
 READ_OK, READ_INVALID, READ_SHORT = 0, 1, 2
@@ -68,6 +68,7 @@ def lib():
             "skq_memcpy_d2h": (i32, [vp, vp, C.c_size_t, vp]),
             "skq_stream_sync": (i32, [vp]),
             "skq_session_enable_timing": (i32, [vp, i32]),
+            "skq_session_set_variant": (i32, [vp, i32]),
             "skq_session_kernel_time": (i32, [vp, i32, C.POINTER(dbl), C.POINTER(u64)]),
             "skq_tables_build": (i32, [u32, vp, vp, u32, vp, u32, i32, C.POINTER(vp)]),
             "skq_tables_count": (u32, [vp]),
@@ -234,6 +235,9 @@ class Session:
 
     def reset_totals(self, stream=None):
         _check(lib().skq_session_reset_totals(self.h, stream))
+
+    def set_variant(self, v):
+        _check(lib().skq_session_set_variant(self.h, int(v)))
 
     def enable_timing(self, on=True):
         _check(lib().skq_session_enable_timing(self.h, int(on)))

@@ -278,3 +278,28 @@ def test_repeated_batches_accumulate_totals(tx300):
     s.reset_totals()
     a, _ = s.totals()
     assert a.sum() == 0
+
+
+def test_very_long_reads_and_large_postings():
+    # whole transcripts as reads (up to ~4 kb) plus 8-12 kb concatenations: the slow sketch path
+    # beyond its LDS capacity and the slow chain path beyond LDS (global scratch)
+    rng = np.random.default_rng(5)
+    tx = synth.transcriptome(60, seed=77)
+    seqs = [tx.seq(t) for t in range(tx.ntx)]
+    h, t = [], []
+    for tid, s in enumerate(seqs):
+        for x in orc.sketch(s, 31):
+            h.append(x)
+            t.append(tid)
+            if rng.random() < 0.5:
+                for extra in rng.choice(np.arange(60, 400), 30, replace=False):
+                    h.append(x)
+                    t.append(int(extra))
+    pairs = [(np.array(h, np.uint32), np.array(t, np.uint32))]
+    gi, oi = build([31], pairs=pairs, ntx=400)
+    reads = seqs[:20] + [b"".join(seqs[i:i + 4]) for i in range(0, 16, 4)]
+    thr = orc.threshold(0.9)  # > SLOW_CAP retained hashes for the long ones
+    for th in (None, thr):
+        out = run_gpu(gi, reads, thr=th)
+        ref = oi.map_batch(reads, thr=th)
+        compare(out, ref, len(reads), 1)

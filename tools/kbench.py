@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Per-kernel timing of variants on one data set (development tool; interleaved rounds in one
+process, as the CDNA guide's methodology asks). Prints one line per variant."""
+import argparse
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sketch-for-rna-seq_amd"))
+import skq  # noqa: E402
+from skq import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--ntx", type=int, default=200_000)
+ap.add_argument("--reads", type=int, default=10_000_000)
+ap.add_argument("--len", type=int, default=150)
+ap.add_argument("--ks", default="31")
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--variants", default="0", help="chain kernel variants to A/B (0 = default)")
+a = ap.parse_args()
+ks = [int(x) for x in a.ks.split(",")]
+t0 = time.time()
+tx = synth.transcriptome(a.ntx, seed=1)
+tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
+index = skq.Index(ks, tx.ntx, tables)
+bases, _, _ = synth.reads(tx, a.reads, a.len, seed=1000, err=0.001)
+dev = torch.device("cuda", 0)
+d = torch.from_numpy(bases).to(dev)
+s = skq.Session(index, a.reads, a.len)
+sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+print("setup %.1fs" % (time.time() - t0), flush=True)
+
+def run_variant(v, acc):
+    def f():
+        s.set_variant(v)
+        s.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=acc)
+    return f
+
+
+variants = {}
+for v in [int(x) for x in a.variants.split(",")]:
+    variants["v%d+acc" % v] = run_variant(v, True)
+    variants["v%d" % v] = run_variant(v, False)
+res = {k: [] for k in variants}
+for rnd in range(a.rounds + 1):
+    for name, fn in variants.items():
+        s.enable_timing(True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t) * 1e3
+        s.enable_timing(False)
+        k1 = s.kernel_time(0)[0]
+        k2 = s.kernel_time(1)[0]
+        if rnd:
+            res[name].append((wall, k1, k2))
+for name, v in res.items():
+    v = np.array(v)
+    med = np.median(v, axis=0)
+    print("%-10s wall %.3f ms  k_sketch %.3f  k_chain %.3f  -> %.2f G reads/s" % (
+        name, med[0], med[1], med[2], a.reads / med[0] / 1e6))
