@@ -76,6 +76,8 @@ struct skq_session {
     uint8_t* status = nullptr;
     uint32_t* hash_cnt = nullptr;
     uint32_t* hashes = nullptr;
+    uint32_t* lofs = nullptr;    // list offsets per probe (k_probe -> k_count), shaped like hashes
+    uint8_t* pflag = nullptr;
     uint32_t* hash_ext = nullptr;
     uint64_t hash_ext_cap = 0;
     uint32_t* ovf1 = nullptr;
@@ -148,7 +150,9 @@ int ensure_hashes(skq_session* s, uint32_t hcap) {
     if (s->hcap_alloc >= hcap) return 0;
     (void)hipDeviceSynchronize();
     dev_free(s->hashes);
+    dev_free(s->lofs);
     if (dev_alloc(&s->hashes, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
+    if (dev_alloc(&s->lofs, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
     s->hcap_alloc = hcap;
     return 0;
 }
@@ -335,6 +339,7 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     if ((rc = dev_alloc(&s->status, max_reads)) || (rc = dev_alloc(&s->hash_cnt, max_reads * ix->nk)) ||
         (rc = dev_alloc(&s->hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&s->ovf1, s->ovf_cap)) ||
         (rc = dev_alloc(&s->ovf2, s->ovf_cap)) || (rc = dev_alloc(&s->cand_cnt, max_reads)) ||
+        (rc = dev_alloc(&s->pflag, max_reads)) ||
         (rc = dev_alloc(&s->cand_tid, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
@@ -365,6 +370,8 @@ int skq_session_free(skq_session* s) {
     dev_free(s->status);
     dev_free(s->hash_cnt);
     dev_free(s->hashes);
+    dev_free(s->lofs);
+    dev_free(s->pflag);
     dev_free(s->hash_ext);
     dev_free(s->ovf1);
     dev_free(s->ovf2);
@@ -461,6 +468,9 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.tx_score = s->tx_score;
     p.ctrl = s->ctrl;
     p.ovf2 = s->ovf2;
+    p.lofs = s->lofs;
+    p.pflag = s->pflag;
+    p.lcap = std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
     p.variant = s->variant;
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};

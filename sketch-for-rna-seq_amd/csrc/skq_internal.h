@@ -108,7 +108,10 @@ struct ChainParams {
     uint64_t* tx_score;
     uint32_t* ctrl;
     uint32_t* ovf2;
-    int variant;               // chain kernel variant (development A/B; 0 = default)
+    uint32_t* lofs;            // k_probe -> k_count: list offset per probe, [(i*lcap + j)*n + r]
+    uint8_t* pflag;            // k_probe -> k_count: 1 = read listed for the slow path
+    uint32_t lcap;             // probes per (read, k) slot in lofs (reads above it: slow path)
+    int variant;               // development A/B switch (0 = default)
 };
 
 // records the message returned by skq_last_error(); returns code (skq_capi.hip)
@@ -117,7 +120,7 @@ int set_error(int code, const char* msg);
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream);
-int launch_chain(const ChainParams& p, void* stream);
+int launch_chain(const ChainParams& p, void* stream);  // k_probe + k_count
 int launch_chain_slow(const ChainParams& p, void* stream);
 int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
 

@@ -469,8 +469,9 @@ __device__ bool probe_list(const ChainParams& p, const DevTable& t, uint32_t key
     return false;
 }
 
-// Count table in registers: N (id, packed per-k counts) entries in banks of 4. A bank is
-// compared only when some lane of the wave uses it (wave-uniform test).
+// Count table in registers: N (id, packed per-k counts) entries. The first 8 entries are
+// always compared; entries 8.. only when some lane of the wave uses them (wave-uniform test),
+// so the common read (a handful of distinct ids) pays no ballots on the compare path.
 template <int N>
 struct CountTable {
     uint32_t ids[N], cnts[N];
@@ -485,29 +486,36 @@ struct CountTable {
     }
     // cnts[id] += inc (packed bytes); false when an (N+1)th distinct id shows up
     __device__ __forceinline__ bool add(uint32_t x, uint32_t inc) {
+        constexpr int N0 = N < 8 ? N : 8;
         bool found = false;
 #pragma unroll
-        for (int bank = 0; bank < N / 4; ++bank) {
-            if (bank == 0 || __any(nd > 4u * bank)) {
+        for (int d = 0; d < N0; ++d) {
+            const bool hit = ids[d] == x;
+            cnts[d] += hit ? inc : 0u;
+            found |= hit;
+        }
+        if (N > 8 && __any(nd > 8u)) {
 #pragma unroll
-                for (int d = 4 * bank; d < 4 * bank + 4; ++d) {
-                    const bool hit = ids[d] == x;
-                    cnts[d] += hit ? inc : 0u;
-                    found |= hit;
-                }
+            for (int d = N0; d < N; ++d) {
+                const bool hit = ids[d] == x;
+                cnts[d] += hit ? inc : 0u;
+                found |= hit;
             }
         }
-        if (__all(found)) return true;
         if (!found && nd == (uint32_t)N) return false;
 #pragma unroll
-        for (int bank = 0; bank < N / 4; ++bank) {
-            if (__any(!found && (nd >> 2) == (uint32_t)bank)) {
+        for (int d = 0; d < N0; ++d) {
+            if (!found && (uint32_t)d == nd) {
+                ids[d] = x;
+                cnts[d] = inc;
+            }
+        }
+        if (N > 8 && __any(!found && nd >= 8u)) {
 #pragma unroll
-                for (int d = 4 * bank; d < 4 * bank + 4; ++d) {
-                    if (!found && (uint32_t)d == nd) {
-                        ids[d] = x;
-                        cnts[d] = inc;
-                    }
+            for (int d = N0; d < N; ++d) {
+                if (!found && (uint32_t)d == nd) {
+                    ids[d] = x;
+                    cnts[d] = inc;
                 }
             }
         }
@@ -553,55 +561,225 @@ __device__ __forceinline__ uint32_t pick8(const uint32_t (&w)[8], uint32_t i) {
     return bsel(m2, b[1], b[0]);
 }
 
-// Fast chain kernel: one lane per read. Probes give list offsets, counted per distinct list
-// (usually 1-3); each distinct list is then expanded into the per-transcript table with its
-// packed per-k counts: count(t, k) = sum over distinct lists L containing t of count(L, k),
-// exactly the reference's per-posting count.
-__global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
+// quad-local lane exchange through DPP (a VALU modifier: no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t quad_bcast0(uint32_t v) { return quad_dpp<0x00>(v); }    // quad_perm(0,0,0,0)
+__device__ __forceinline__ uint32_t quad_or_all(uint32_t v) {
+    v |= quad_dpp<0xB1>(v);  // quad_perm(1,0,3,2): xor 1
+    v |= quad_dpp<0x4E>(v);  // quad_perm(2,3,0,1): xor 2
+    return v;
+}
+
+// inclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(v, o, 64);
+        if (lane >= o) v += x;
+    }
+    return v;
+}
+
+// probes per wave held in LDS: 512 per k slot (a 64-read wave of 150 bp reads averages ~384
+// at k = 31; a read that does not fit takes the slow path)
+__host__ __device__ inline uint32_t probe_cap(uint32_t nk) { return 512u * (nk < 1 ? 1 : (nk > 4 ? 4 : nk)); }
+size_t chain_lds_bytes(uint32_t nk) { return 256 + (size_t)(WG / 64) * probe_cap(nk) * 5; }
+
+// k_probe: every retained hash -> the offset of its postings list (equivalence class).
+//   1. each wave lists its 64 reads' retained hashes (the probes) in LDS (wave prefix sum);
+//   2. each quad of lanes resolves probes cooperatively: ONE coalesced 64-B load brings a
+//      bucket into the quad (16 B per lane), the key match and the list offset are combined
+//      with DPP quad permutes; QU loads per quad are kept in flight;
+//   3. each lane writes its read's list offsets out, SoA like the hashes (lofs[(i*lcap + j)*n
+//      + r]), and flags reads the fast path cannot take (pflag = 1, listed for k_chain_slow).
+__global__ __launch_bounds__(WG) void k_probe(ChainParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t PW_CAP = probe_cap(p.nk);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // table descriptors in LDS: indexing the kernel-argument array by a lane-varying k slot
+    // would load it from memory behind an s_waitcnt vmcnt(0), serialising the bucket loads
+    DevTable* s_tabs = reinterpret_cast<DevTable*>(smem);
+    uint32_t* sp = reinterpret_cast<uint32_t*>(smem + 256) + wv * PW_CAP;                  // keys, then list offsets
+    uint8_t* sk = smem + 256 + (size_t)(WG / 64) * PW_CAP * 4 + (size_t)wv * PW_CAP;       // k slot per probe
+    if (threadIdx.x < SKQ_MAX_K) s_tabs[threadIdx.x] = p.tabs[threadIdx.x];
+    const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
+    const bool live = r < p.n;
+    const bool ok = live && (!p.status || (p.status[r] & SKQ_STATUS_MASK) == SKQ_READ_OK);
+    bool slow = ok && p.nk > (uint32_t)NK_FAST;
+
+    // ---- 1. probe list
+    uint32_t cnt[NK_FAST];
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < NK_FAST; ++i) {
+        cnt[i] = 0;
+        if (!ok || slow || (uint32_t)i >= p.nk || !p.tabs[i].present || (p.present && !p.present[r * p.nk + i]))
+            continue;
+        cnt[i] = hash_count(p, r, i);
+        if (cnt[i] > p.lcap) slow = true;  // (lcap <= HFAST: counts are packed 8 bits per k)
+        h += cnt[i];
+    }
+    if (slow) h = 0;
+    const uint32_t incl = wave_incl_scan(h, lane);
+    const uint32_t base = incl - h;
+    if (incl > PW_CAP) slow = true;
+    // the reads that fit form a prefix of the wave (incl is monotone): probes end at the last one
+    const uint64_t fit = __ballot(incl <= PW_CAP);
+    const uint32_t H = fit ? __shfl(incl, 63 - __builtin_clzll(fit), 64) : 0u;
+    if (ok && !slow) {
+        uint32_t q = base;
+#pragma unroll
+        for (int i = 0; i < NK_FAST; ++i) {
+            if (!cnt[i]) continue;
+            uint64_t hstride;
+            const uint32_t* hs = hash_list(p, r, i, cnt[i], hstride);
+            for (uint32_t j0 = 0; j0 < cnt[i]; j0 += 8) {  // 8 loads in flight, then the LDS writes
+                uint32_t hv[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u) hv[u] = j0 + u < cnt[i] ? hs[(j0 + u) * hstride] : 0u;
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u) {
+                    if (j0 + u < cnt[i]) {
+                        sp[q] = hv[u];
+                        sk[q] = (uint8_t)i;
+                        ++q;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. quad-cooperative probes: key -> list offset (~0u: miss). Each quad keeps QU
+    //         independent bucket loads in flight, then resolves them.
+    {
+        constexpr uint32_t QU = 8;
+        const uint32_t c = lane & 3;
+        for (uint32_t p0 = (lane >> 2) * QU; p0 < H; p0 += 16 * QU) {
+            uint32_t key[QU], bk[QU], ks[QU];
+            uint4 v[QU];
+#pragma unroll
+            for (uint32_t u = 0; u < QU; ++u) {
+                const uint32_t pi = p0 + u;
+                key[u] = pi < H ? sp[pi] : 0u;
+                ks[u] = pi < H ? (sk[pi] & (SKQ_MAX_K - 1)) : 0u;
+                const DevTable& t = s_tabs[ks[u]];
+                bk[u] = home_bucket(key[u], t.nbuckets);
+                v[u] = pi < H ? *reinterpret_cast<const uint4*>(p.buckets + (t.bucket_base + bk[u]) * BUCKET_WORDS + 4 * c)
+                              : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < QU; ++u) {
+                const uint32_t pi = p0 + u;
+                if (pi >= H) break;  // uniform within the quad
+                uint32_t lo = ~0u;
+                uint4 vv = v[u];
+                const DevTable& t = s_tabs[ks[u]];
+                for (uint32_t q = 0; q < t.max_probe; ++q) {
+                    if (q) {
+                        bk[u] = bk[u] + 1 == t.nbuckets ? 0 : bk[u] + 1;
+                        vv = *reinterpret_cast<const uint4*>(p.buckets + (t.bucket_base + bk[u]) * BUCKET_WORDS + 4 * c);
+                    }
+                    const uint32_t hdr = quad_bcast0(vv.x);
+                    const uint32_t m = hdr & 7u;
+                    // words 1..m are keys, word BUCKET_LIST0 + j the list offset of key j
+                    const uint32_t wv4[4] = {vv.x, vv.y, vv.z, vv.w};
+                    uint32_t match = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint32_t w = 4 * c + e;
+                        if (w >= 1 && w <= m && wv4[e] == key[u]) match = w;  // record j = w - 1
+                    }
+                    match = quad_or_all(match);
+                    if (match) {
+                        const uint32_t lw = BUCKET_LIST0 + match - 1;  // word holding the list offset
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (4 * c + e == lw) x = wv4[e];
+                        lo = quad_or_all(x);
+                        break;
+                    }
+                    if (!((hdr >> 3) & 1u)) break;
+                }
+                if (c == 0) sp[pi] = lo;
+            }
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    if (ok && slow) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+    p.pflag[r] = slow ? 1 : 0;
+    if (!ok || slow) return;
+    uint32_t q = base;
+#pragma unroll
+    for (int i = 0; i < NK_FAST; ++i)
+        for (uint32_t j = 0; j < cnt[i]; ++j) p.lofs[((uint64_t)i * p.lcap + j) * p.n + r] = sp[q++];
+}
+
+// k_count: one lane per read. Counts the read's list offsets per distinct list (usually 1-3),
+// expands each distinct list into the per-transcript table with its packed per-k counts —
+// count(t, k) = sum over distinct lists L containing t of count(L, k), exactly the reference's
+// per-posting count (src/sparse_chaining.cpp:48-73) — then filters, scores and sorts.
+template <int NK>
+__global__ __launch_bounds__(WG) void k_count(ChainParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
     if (r >= p.n) return;
-    if (p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) {
-        p.cand_cnt[r] = 0;
+    if ((p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) || p.pflag[r]) {
+        p.cand_cnt[r] = 0;  // not sketched, or listed by k_probe for the slow path
         return;
     }
+    bool slow = false;
     CountTable<DLISTS> lt;  // list offset -> packed per-k counts
     lt.init();
-    bool slow = p.nk > (uint32_t)NK_FAST;
-
-    for (uint32_t i = 0; i < p.nk && !slow; ++i) {
-        const DevTable t = p.tabs[i];
-        if (!t.present) continue;
-        if (p.present && !p.present[r * p.nk + i]) continue;
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        if (!p.tabs[i].present || (p.present && !p.present[r * NK + i])) continue;
         const uint32_t cnt = hash_count(p, r, i);
-        if (cnt > (uint32_t)HFAST) {  // counts are packed 8 bits per k
-            slow = true;
-            break;
-        }
-        uint64_t hstride;
-        const uint32_t* hs = hash_list(p, r, i, cnt, hstride);
         const uint32_t inc = 1u << (8 * i);
-        const uint32_t* tb = p.buckets + t.bucket_base * BUCKET_WORDS;
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const uint32_t lo = probe_ec(tb, t, hs[j * hstride]);
-            if (lo != ~0u && !lt.add(lo, inc)) {
+        const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + r;
+        for (uint32_t j0 = 0; j0 < cnt && !slow; j0 += 4) {  // 4 coalesced loads in flight
+            uint32_t lv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) lv[u] = j0 + u < cnt ? lo_i[(uint64_t)(j0 + u) * p.n] : ~0u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (lv[u] != ~0u && !lt.add(lv[u], inc)) slow = true;
+        }
+    }
+    CountTable<DCAP> tab;  // transcript -> packed per-k counts
+    tab.init();
+    // expand the distinct lists: the first 4 heads ([n, t0, t1, t2]) are loaded together,
+    // lists beyond 4 (rare) one at a time
+    uint4 head[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        head[e] = (!slow && (uint32_t)e < lt.nd) ? *reinterpret_cast<const uint4*>(p.lists + lt.ids[e])
+                                                : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (!__any(!slow && (uint32_t)e < lt.nd)) break;
+        if (slow || (uint32_t)e >= lt.nd) continue;
+        const uint32_t n = head[e].x;
+        for (uint32_t q = 0; q < n; ++q) {
+            const uint32_t x = q == 0 ? head[e].y : q == 1 ? head[e].z : q == 2 ? head[e].w : p.lists[lt.ids[e] + 1 + q];
+            if (!tab.add(x, lt.cnts[e])) {
                 slow = true;
                 break;
             }
         }
     }
-    CountTable<DCAP> tab;  // transcript -> packed per-k counts
-    tab.init();
-    // expand the distinct lists (wave-uniform trip count)
-    for (uint32_t e = 0; e < (uint32_t)DLISTS && !slow; ++e) {
-        if (!__any(e < lt.nd && !slow)) break;
-        if (e >= lt.nd || slow) continue;
+    for (uint32_t e = 4; e < (uint32_t)DLISTS; ++e) {
+        if (!__any(!slow && e < lt.nd)) break;
+        if (slow || e >= lt.nd) continue;
         const uint32_t lo = pick8(lt.ids, e);
         const uint32_t inc = pick8(lt.cnts, e);
-        const uint4 head = *reinterpret_cast<const uint4*>(p.lists + lo);
-        const uint32_t n = head.x;
+        const uint32_t n = p.lists[lo];
         for (uint32_t q = 0; q < n; ++q) {
-            const uint32_t x = q == 0 ? head.y : q == 1 ? head.z : q == 2 ? head.w : p.lists[lo + 1 + q];
-            if (!tab.add(x, inc)) {
+            if (!tab.add(p.lists[lo + 1 + q], inc)) {
                 slow = true;
                 break;
             }
@@ -616,16 +794,16 @@ __global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
     // threshold: (double)c >= fraction * max  <=>  c >= ceil(fraction * max)   (:84-87, :93)
     // (counts here are <= 255, so a threshold clamped to 256 rejects the same transcripts; a
     // NaN or non-positive threshold accepts everything, as `c < thr` is then false.)
-    uint32_t need[NK_FAST];
+    uint32_t need[NK];
 #pragma unroll
-    for (int i = 0; i < NK_FAST; ++i) {
+    for (int i = 0; i < NK; ++i) {
         uint32_t m = 0;
 #pragma unroll
         for (int d = 0; d < DCAP; ++d) m = max(m, (tab.cnts[d] >> (8 * i)) & 0xFFu);
         const double thr = p.fraction * (double)m;
         uint32_t ti = 0;
         if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
-        need[i] = (uint32_t)i < p.nk ? ti : 0u;
+        need[i] = ti;
     }
     uint64_t key[DCAP];
 #pragma unroll
@@ -633,7 +811,7 @@ __global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
         bool ok = (uint32_t)d < tab.nd;
         uint32_t score = 0;
 #pragma unroll
-        for (int i = 0; i < NK_FAST; ++i) {
+        for (int i = 0; i < NK; ++i) {
             const uint32_t c = (tab.cnts[d] >> (8 * i)) & 0xFFu;
             ok &= c >= need[i];
             score += c;
@@ -641,7 +819,19 @@ __global__ __launch_bounds__(WG) void k_chain(ChainParams p) {
         // sort key: score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
         key[d] = ok ? (((uint64_t)(0xFFFFFFFFu - score) << 32) | tab.ids[d]) : ~0ull;
     }
-    bitonic_sort<DCAP>(key);
+    // only entries < nd can be candidates: sort 8 when no lane of the wave has more
+    if (__any(tab.nd > 8u)) {
+        bitonic_sort<DCAP>(key);
+    } else {
+        uint64_t k8[8];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) k8[d] = key[d];
+        bitonic_sort<8>(k8);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) key[d] = k8[d];
+#pragma unroll
+        for (int d = 8; d < DCAP; ++d) key[d] = ~0ull;
+    }
     uint32_t nc = 0;
     // SoA layout: candidate j of read r at cand_tid[j*n + r]
     uint32_t* ct = p.cand_tid + r;
@@ -862,7 +1052,15 @@ int launch_sketch_slow(const SketchParams& p, void* stream) {
 int launch_chain(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    hipLaunchKernelGGL(k_chain, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_probe, grid, dim3(WG), chain_lds_bytes(p.nk), reinterpret_cast<hipStream_t>(stream), p);
+    if (hipGetLastError() != hipSuccess) return -2;
+    switch (p.nk) {
+    case 1: hipLaunchKernelGGL(k_count<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 2: hipLaunchKernelGGL(k_count<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 3: hipLaunchKernelGGL(k_count<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 4: hipLaunchKernelGGL(k_count<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    default: break;  // > 4 k slots: every read was listed for the slow path by k_probe
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

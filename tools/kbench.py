@@ -44,7 +44,8 @@ def run_variant(v, acc):
 
 variants = {}
 for v in [int(x) for x in a.variants.split(",")]:
-    variants["v%d+acc" % v] = run_variant(v, True)
+    if v == 0:
+        variants["v%d+acc" % v] = run_variant(v, True)
     variants["v%d" % v] = run_variant(v, False)
 res = {k: [] for k in variants}
 for rnd in range(a.rounds + 1):
