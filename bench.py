@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[2], the metric's config): synthetic 150 bp forward-strand reads
 against a ~200k-transcript GENCODE-scale synthetic index, k = 31, sketch fraction (double)0.05f,
-chain fraction 0.9. One step = one pass of the hot path (k_sketch + k_chain, slow paths included)
+chain fraction 0.9. One step = one pass of the hot path (k_sketch, k_probe, k_count, slow paths included)
 over one batch of `--reads` reads already resident in HBM, plus — when N > 1 — the one RCCL
 all-reduce of the per-transcript totals (reads, score) over xGMI.
 
@@ -114,7 +114,8 @@ def main():
     for _ in range(args.warmup):
         step()
     sess.check(sp)
-    sess.kernel_time(0), sess.kernel_time(1)
+    for kind in range(3):
+        sess.kernel_time(kind)
     sess.enable_timing(True)
     if world > 1:
         dist.barrier()
@@ -128,8 +129,7 @@ def main():
     elapsed = time.perf_counter() - ts
     sess.enable_timing(False)
     sess.check(sp)
-    k1_ms, k1_n = sess.kernel_time(0)
-    k2_ms, k2_n = sess.kernel_time(1)
+    kt = [sess.kernel_time(kind) for kind in range(3)]  # (total ms, launches): sketch, probe, count
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -141,14 +141,27 @@ def main():
     st = per_read_stats(sess, tables, ks, ns)
     h, P, Cn = st["h"], st["P"], st["C"]
     nk = len(ks)
-    # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"):
-    b_sketch = L + 4 * h + 4 * nk + 1                  # read bases in; retained hashes, counts, status out
-    b_chain = 1 + 4 * nk + 4 * h + 8 * h + 4 * P + 8 * Cn + 4 + 16 * Cn
+    # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"); an index lookup is priced at
+    # the 8 B (key, list offset) it needs, a posting at its 4 B tid
+    b_kern = {
+        # read bases in; retained hashes, per-k counts, status out
+        "k_sketch": L + 4 * h + 4 * nk + 1,
+        # status + counts + hashes in, one lookup per hash, list offsets + slow flag out
+        "k_probe": 1 + 4 * nk + 4 * h + 8 * h + 4 * h + 1,
+        # status + flag + counts + list offsets in, postings, candidates (tid, score) + count out,
+        # one packed 8 B per-transcript total per candidate
+        "k_count": 2 + 4 * nk + 4 * h + 4 * P + 4 + 8 * Cn + 8 * Cn,
+    }
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
-    k1_avg = k1_ms / max(k1_n, 1)
-    k2_avg = k2_ms / max(k2_n, 1)
-    kern = ("k_chain", k2_avg, b_chain) if k2_avg >= k1_avg else ("k_sketch", k1_avg, b_sketch)
-    achieved = n * kern[2] / (kern[1] * 1e-3) / 1e9
+    avg = {name: ms / max(cnt, 1) for name, (ms, cnt) in zip(("k_sketch", "k_probe", "k_count"), kt)}
+    kname = max(avg, key=avg.get)                       # dominant kernel
+    achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    if os.path.exists(tf):                               # PMC FETCH/WRITE passes (tools/traffic.py)
+        tr = json.load(open(tf))
+        if kname in tr.get("kernels", {}):
+            traffic = tr["kernels"][kname]["hbm_bytes_per_read"] * n
     total_reads = n * world * args.steps
     value = total_reads / elapsed
 
@@ -180,12 +193,12 @@ def main():
                        "transcripts": tx.ntx, "ks": ks, "sketch_fraction": "(double)0.05f",
                        "chain_fraction": 0.9, "parallelism": "read-sharded x%d, index replicated" % world
                        + (", 1 all-reduce of per-transcript totals per step" if world > 1 else "")},
-            "roofline": {"bound": "hbm", "kernel": kern[0], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "bytes_per_read": kern[2], "avg_launch_ms": kern[1]},
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname]},
             "path": {"bytes_per_read": b_path, "achieved_GBps": value / world * b_path / 1e9,
                      "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
-                     "k_sketch_ms": k1_avg, "k_chain_ms": k2_avg, "h": h, "P": P, "C": Cn},
+                     "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn},
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)

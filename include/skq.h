@@ -66,6 +66,11 @@ int skq_index_free(skq_index* idx);
 /* device bytes held, total postings, longest postings list */
 int skq_index_stats(const skq_index* idx, uint64_t* device_bytes, uint64_t* npostings,
                     uint32_t* max_list);
+/* Probe mode of an index: 1 = direct tables (the sketch kernel probes each retained hash with one
+ * 4-B gather, DESIGN.md "Index"), 0 = bucket table only (k_probe). Direct tables are built when
+ * their total size (4 B x (largest key + 1) per k) fits SKQ_DIRECT_MB (environment, MiB, default
+ * 8192; 0 disables) and half the free device memory. Results are identical in both modes. */
+int skq_index_direct(const skq_index* ix);
 
 /* A session owns the device workspace for batches of up to max_reads reads of at most
  * max_len bases each (longer reads are still handled exactly, by the slow path). */
@@ -149,7 +154,7 @@ int skq_stream_sync(void* stream);
 /* Kernel timing: with timing enabled, every skq_sketch / skq_chain call records HIP events on
  * its stream around its fast kernel. skq_session_kernel_time waits for them and returns the
  * summed milliseconds and launch count of one kind since the last query (then forgets them).
- * kind: 0 = k_sketch, 1 = k_chain. Used by bench.py for the roofline figure. */
+ * kind: 0 = k_sketch, 1 = k_probe, 2 = k_count. Used by bench.py for the roofline figure. */
 int skq_session_enable_timing(skq_session* s, int enable);
 /* Development A/B switch for the chain kernel (0 = default). Not needed by users. */
 int skq_session_set_variant(skq_session* s, int variant);

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -58,6 +59,12 @@ struct skq_index {
     uint64_t* d_rolltab = nullptr;
     uint64_t nbucket_words = 0, nlist_words = 0, npostings = 0;
     uint32_t max_list = 0;
+    // direct tables (one per distinct k; slot i uses dir[i]): u32 list offset per possible key
+    uint32_t* d_dir_t[SKQ_MAX_K] = {};
+    const uint32_t* dir[SKQ_MAX_K] = {};
+    uint64_t dir_len[SKQ_MAX_K] = {};
+    uint64_t dir_bytes = 0;
+    bool direct = false;  // every slot with a table has a direct table: the sketch probes
 };
 
 struct TimedLaunch {
@@ -73,6 +80,7 @@ struct skq_session {
     uint32_t hcap_alloc = 0;   // stride the hashes buffer was sized for
     uint64_t n_reads = 0;      // reads in the current results
     bool have_sketch = false;
+    bool probed = false;       // the last skq_sketch also filled lofs/pflag (fused probe)
     uint8_t* status = nullptr;
     uint32_t* hash_cnt = nullptr;
     uint32_t* hashes = nullptr;
@@ -157,6 +165,54 @@ int ensure_hashes(skq_session* s, uint32_t hcap) {
     return 0;
 }
 
+// Direct tables: for each distinct k, dir[h] = list offset of key h (~0u = no key), for every h
+// up to the table's largest key, so the sketch kernel probes with one 4-B gather per retained
+// hash. At the reference's fraction (double)0.05f keys are <= 214748367: 859 MB per k, which
+// HBM3E holds easily. Built only while the total stays inside SKQ_DIRECT_MB (default 8192 MiB;
+// 0 disables) and half the free device memory; otherwise probes go through the bucket table.
+int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
+                 const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals) {
+    uint64_t budget = 8192ull << 20;
+    if (const char* e = std::getenv("SKQ_DIRECT_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
+    uint64_t need = 0, len[SKQ_MAX_K] = {};
+    for (uint32_t t = 0; t < ntables; ++t) {
+        len[t] = dkeys[t].empty() ? 0 : (uint64_t)dkeys[t].back() + 1;  // keys ascending
+        need += len[t] * 4;
+    }
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+    if (need == 0 || need > budget || need > fr / 2) return 0;
+    hipStream_t st = nullptr;
+    uint32_t *dk = nullptr, *dv = nullptr;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const uint64_t m = dkeys[t].size();
+        if (dev_alloc(&ix->d_dir_t[t], len[t]) || dev_alloc(&dk, m) || dev_alloc(&dv, m)) {
+            dev_free(dk);
+            dev_free(dv);
+            return fail(-3, "direct table allocation failed");
+        }
+        if (hipMemsetAsync(ix->d_dir_t[t], 0xFF, len[t] * 4, st) != hipSuccess ||
+            hipMemcpy(dk, dkeys[t].data(), m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dv, dvals[t].data(), m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            skq::launch_dir_scatter(ix->d_dir_t[t], dk, dv, m, st) || hipStreamSynchronize(st) != hipSuccess) {
+            dev_free(dk);
+            dev_free(dv);
+            return fail(-3, "direct table build failed");
+        }
+        dev_free(dk);
+        dev_free(dv);
+    }
+    ix->dir_bytes = need;
+    for (uint32_t i = 0; i < ix->nk; ++i)
+        for (uint32_t t = 0; t < ntables; ++t)
+            if (tables[t].k == ix->ks[i]) {
+                ix->dir[i] = ix->d_dir_t[t];
+                ix->dir_len[i] = len[t];
+            }
+    ix->direct = true;
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -214,6 +270,7 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
     };
     uint64_t tbase[SKQ_MAX_K] = {};
     uint32_t tnb[SKQ_MAX_K] = {}, tprobe[SKQ_MAX_K] = {};
+    std::vector<uint32_t> dkeys[SKQ_MAX_K], dvals[SKQ_MAX_K];  // per table, for the direct table
     for (uint32_t t = 0; t < ntables; ++t) {
         const skq_kmer_table& T = tables[t];
         for (uint32_t u = 0; u < t; ++u)
@@ -263,6 +320,12 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
             H[0] = (H[0] & ~7u) | (m + 1);
         }
         tprobe[t] = maxd + 1;
+        dkeys[t].reserve(recs.size());
+        dvals[t].reserve(recs.size());
+        for (const auto& [key, off] : recs) {
+            dkeys[t].push_back(key);
+            dvals[t].push_back(off);
+        }
     }
     lists.resize(lists.size() + 4, 0);  // a uint4 read at any list start stays inside
     for (uint32_t i = 0; i < nk; ++i) {
@@ -297,6 +360,10 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
         skq_index_free(ix);
         return fail(-3, "index upload failed");
     }
+    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals)) {
+        skq_index_free(ix);
+        return rc2;
+    }
     *out = ix;
     return 0;
 }
@@ -304,6 +371,7 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
 int skq_index_free(skq_index* ix) {
     if (!ix) return 0;
     DeviceGuard g(ix->device);
+    for (auto& d : ix->d_dir_t) dev_free(d);
     dev_free(ix->d_buckets);
     dev_free(ix->d_lists);
     dev_free(ix->d_rolltab);
@@ -313,11 +381,13 @@ int skq_index_free(skq_index* ix) {
 
 int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npostings, uint32_t* max_list) {
     if (!ix) return fail(-1, "null index");
-    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4;
+    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4 + ix->dir_bytes;
     if (npostings) *npostings = ix->npostings;
     if (max_list) *max_list = ix->max_list;
     return 0;
 }
+
+int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? 1 : 0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
     if (!ix || !out) return fail(-1, "null argument");
@@ -420,6 +490,13 @@ int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, u
     p.hash_ext_cap = s->hash_ext_cap;
     p.ctrl = s->ctrl;
     p.ovf1 = s->ovf1;
+    p.fuse = ix->direct ? 1 : 0;
+    for (uint32_t i = 0; i < ix->nk; ++i) {
+        p.dir[i] = ix->dir[i];
+        p.dir_len[i] = ix->dir_len[i];
+    }
+    p.lofs = s->lofs;
+    p.pflag = s->pflag;
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 8 * 4, st));
     hipEvent_t t0{};
     record(s, 0, &t0, st);
@@ -429,6 +506,7 @@ int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, u
     s->hcap = hcap;
     s->n_reads = n_reads;
     s->have_sketch = true;
+    s->probed = ix->direct;
     s->x_hashes = nullptr;
     s->x_offs = nullptr;
     return 0;
@@ -436,7 +514,7 @@ int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, u
 
 static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const uint32_t* hash_cnt,
                       const uint32_t* hashes, const uint64_t* hash_offs, const uint8_t* present,
-                      uint32_t hcap, double fraction, int accumulate, void* stream) {
+                      uint32_t hcap, double fraction, int accumulate, bool probed, void* stream) {
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const skq_index* ix = s->idx;
@@ -470,13 +548,19 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.ovf2 = s->ovf2;
     p.lofs = s->lofs;
     p.pflag = s->pflag;
-    p.lcap = std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
+    // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
+    p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
     p.variant = s->variant;
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
-    record(s, 1, &t0, st);
-    if (skq::launch_chain(p, stream)) return fail(-3, "chain launch failed");
-    record_stop(s, 1, t0, st);
+    if (!probed) {
+        record(s, 1, &t0, st);
+        if (skq::launch_probe(p, stream)) return fail(-3, "probe launch failed");
+        record_stop(s, 1, t0, st);
+    }
+    record(s, 2, &t0, st);
+    if (skq::launch_count(p, stream)) return fail(-3, "count launch failed");
+    record_stop(s, 2, t0, st);
     if (skq::launch_chain_slow(p, stream)) return fail(-3, "chain slow-path launch failed");
     if (accumulate && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, ix->ntx, stream))
         return fail(-3, "totals fold launch failed");
@@ -487,7 +571,7 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
     if (!s) return fail(-1, "null session");
     if (!s->have_sketch) return fail(-1, "no sketch to chain: call skq_sketch first");
     return chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap,
-                      fraction, accumulate, stream);
+                      fraction, accumulate, s->probed, stream);
 }
 
 int skq_map(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
@@ -505,11 +589,12 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
     if (n_reads && (!d_hashes || !d_hash_offs || !d_hash_cnt)) return fail(-1, "null sketch arrays");
     s->n_reads = n_reads;
     s->have_sketch = false;
+    s->probed = false;
     s->x_hashes = d_hashes;
     s->x_offs = d_hash_offs;
     // hash_cnt is read through p.hash_cnt; keep the session's status out of it (all sketched)
     return chain_impl(s, n_reads, nullptr, d_hash_cnt, d_hashes, d_hash_offs, d_present, 0, fraction,
-                      accumulate, stream);
+                      accumulate, false, stream);
 }
 
 int skq_session_results(skq_session* s, skq_results* o) {

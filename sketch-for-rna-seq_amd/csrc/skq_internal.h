@@ -78,6 +78,15 @@ struct SketchParams {
     uint64_t hash_ext_cap;
     uint32_t* ctrl;
     uint32_t* ovf1;
+    // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
+    // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
+    // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
+    // the slow chain path. Slots without a table (dir[i] null) are skipped by the chain.
+    int fuse;
+    const uint32_t* dir[SKQ_MAX_K];
+    uint64_t dir_len[SKQ_MAX_K];
+    uint32_t* lofs;
+    uint8_t* pflag;
 };
 
 struct ChainParams {
@@ -108,8 +117,9 @@ struct ChainParams {
     uint64_t* tx_score;
     uint32_t* ctrl;
     uint32_t* ovf2;
-    uint32_t* lofs;            // k_probe -> k_count: list offset per probe, [(i*lcap + j)*n + r]
-    uint8_t* pflag;            // k_probe -> k_count: 1 = read listed for the slow path
+    uint32_t* lofs;            // k_probe or fused k_sketch -> k_count: list offset per probe,
+                               // [(i*lcap + j)*n + r], ~0u = miss
+    uint8_t* pflag;            // -> k_count: 1 = read goes to the slow chain path
     uint32_t lcap;             // probes per (read, k) slot in lofs (reads above it: slow path)
     int variant;               // development A/B switch (0 = default)
 };
@@ -120,9 +130,11 @@ int set_error(int code, const char* msg);
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream);
-int launch_chain(const ChainParams& p, void* stream);  // k_probe + k_count
+int launch_probe(const ChainParams& p, void* stream);  // k_probe
+int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream);
 int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
+int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n, void* stream);
 
 #ifdef __HIPCC__
 #define SKQ_HD __host__ __device__

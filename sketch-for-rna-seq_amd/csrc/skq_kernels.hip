@@ -296,12 +296,31 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
             // wave's stores of one j are contiguous
             uint32_t* out = p.hashes + (uint64_t)i * p.hcap * p.n + r;
             uint32_t m = 0;
+            uint32_t keepm = 0;  // bit j: v[j] is the first of its run
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) {
                 const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
-                if (keep) out[(uint64_t)(m++) * p.n] = v[j];
+                if (keep) {
+                    out[(uint64_t)(m++) * p.n] = v[j];
+                    keepm |= 1u << j;
+                }
             }
             p.hash_cnt[(uint64_t)i * p.n + r] = m;
+            if (p.fuse && p.dir[i]) {
+                // fused probe: every kept hash's list offset, all loads in flight before the
+                // stores (a direct table is one 4-B gather per hash, no compare)
+                const uint32_t* dir = p.dir[i];
+                const uint64_t dl = p.dir_len[i];
+                uint32_t lo[HCAP];
+#pragma unroll
+                for (int j = 0; j < HCAP; ++j)
+                    lo[j] = ((keepm >> j) & 1u) && v[j] < dl ? dir[v[j]] : ~0u;
+                uint32_t* lout = p.lofs + (uint64_t)i * p.hcap * p.n + r;
+                uint32_t mm = 0;
+#pragma unroll
+                for (int j = 0; j < HCAP; ++j)
+                    if ((keepm >> j) & 1u) lout[(uint64_t)(mm++) * p.n] = lo[j];
+            }
         }
     }
     if (slow) {
@@ -311,6 +330,8 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
         for (uint32_t i = 0; i < p.nk; ++i) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
     }
     p.status[r] = st;
+    // reads sketched by the slow path, or with more k slots than k_count handles, chain slowly
+    if (p.fuse) p.pflag[r] = (slow || p.nk > (uint32_t)NK_FAST) ? 1 : 0;
 }
 
 // Slow sketch path: one workgroup per listed read. Windows are split into one contiguous
@@ -711,8 +732,7 @@ __global__ __launch_bounds__(WG) void k_probe(ChainParams p) {
     }
     __syncthreads();
     if (!live) return;
-    if (ok && slow) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
-    p.pflag[r] = slow ? 1 : 0;
+    p.pflag[r] = (ok && slow) ? 1 : 0;  // k_count lists it for k_chain_slow
     if (!ok || slow) return;
     uint32_t q = base;
 #pragma unroll
@@ -728,8 +748,13 @@ template <int NK>
 __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
     if (r >= p.n) return;
-    if ((p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) || p.pflag[r]) {
-        p.cand_cnt[r] = 0;  // not sketched, or listed by k_probe for the slow path
+    if (p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) {
+        p.cand_cnt[r] = 0;  // not sketched (invalid or short read)
+        return;
+    }
+    if (p.pflag[r]) {  // flagged by k_probe / the fused sketch: the slow chain path takes it
+        list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+        p.cand_cnt[r] = 0;
         return;
     }
     bool slow = false;
@@ -1049,11 +1074,16 @@ int launch_sketch_slow(const SketchParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_chain(const ChainParams& p, void* stream) {
+int launch_probe(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
     hipLaunchKernelGGL(k_probe, grid, dim3(WG), chain_lds_bytes(p.nk), reinterpret_cast<hipStream_t>(stream), p);
-    if (hipGetLastError() != hipSuccess) return -2;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_count(const ChainParams& p, void* stream) {
+    if (p.n == 0) return 0;
+    const dim3 grid((unsigned)((p.n + WG - 1) / WG));
     switch (p.nk) {
     case 1: hipLaunchKernelGGL(k_count<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
     case 2: hipLaunchKernelGGL(k_count<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
@@ -1067,6 +1097,18 @@ int launch_chain(const ChainParams& p, void* stream) {
 int launch_chain_slow(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     hipLaunchKernelGGL(k_chain_slow, dim3(512), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+__global__ void k_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
+        dir[keys[j]] = vals[j];
+}
+
+int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n, void* stream) {
+    if (n == 0) return 0;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + WG - 1) / WG, 4096);
+    hipLaunchKernelGGL(k_dir_scatter, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), dir, keys, vals, n);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -51,6 +51,7 @@ def lib():
             "skq_index_create": (i32, [i32, u32, u32, vp, u32, vp, C.POINTER(vp)]),
             "skq_index_free": (i32, [vp]),
             "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
+            "skq_index_direct": (i32, [vp]),
             "skq_session_create": (i32, [vp, u64, u32, C.POINTER(vp)]),
             "skq_session_free": (i32, [vp]),
             "skq_sketch": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
@@ -161,7 +162,8 @@ class Index:
     def stats(self):
         b, n, m = C.c_uint64(), C.c_uint64(), C.c_uint32()
         _check(lib().skq_index_stats(self.h, C.byref(b), C.byref(n), C.byref(m)))
-        return dict(device_bytes=b.value, postings=n.value, max_list=m.value)
+        return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
+                    direct=bool(lib().skq_index_direct(self.h)))
 
     def free(self):
         if self.h:

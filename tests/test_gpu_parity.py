@@ -15,6 +15,14 @@ from skq import synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["direct", "bucket"])
+def probe_mode(request, monkeypatch):
+    """Every test runs with both index probe modes: direct tables probed inside the sketch
+    kernel, and the bucket table probed by k_probe (SKQ_DIRECT_MB=0)."""
+    monkeypatch.setenv("SKQ_DIRECT_MB", "8192" if request.param == "direct" else "0")
+    return request.param
+
+
 def build(ks, seqs=None, tx=None, pairs=None, ntx=None):
     """(product device index, oracle index) over the same transcripts / postings."""
     if pairs is not None:
@@ -78,6 +86,14 @@ def totals_from(ref, n, ntx):
             tr[ref["cand_tid"][r, j]] += 1
             ts[ref["cand_tid"][r, j]] += ref["cand_score"][r, j]
     return tr, ts
+
+
+def test_probe_mode_is_selected(tx300, probe_mode):
+    gi, _ = build([21, 31], tx=tx300)
+    st = gi.stats()
+    assert st["direct"] == (probe_mode == "direct")
+    if st["direct"]:  # one u32 per possible key, per k
+        assert st["device_bytes"] > 2 * 4 * 100_000_000
 
 
 @pytest.fixture(scope="module")
