@@ -14,7 +14,7 @@ oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
 .PHONY: oracle
 
 HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o
+LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o
 HOST_CXX ?= g++
 HOSTFLAGS := $(CXXFLAGS_COMMON) -pthread
 
@@ -22,12 +22,16 @@ lib: $(OUT)/libskq.so
 $(OUT)/obj/%.o: $(CSRC)/%.hip $(CSRC)/skq_internal.h include/skq.h include/skq_host.h
 	@mkdir -p $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(OUT)/obj/%.o: $(CSRC)/%.cpp $(CSRC)/skq_internal.h include/skq.h include/skq_host.h
+$(OUT)/obj/%.o: $(CSRC)/%.cpp $(CSRC)/skq_internal.h include/skq.h include/skq_host.h $(wildcard include/dropin/*.h)
 	@mkdir -p $(OUT)/obj
 	$(HOST_CXX) $(HOSTFLAGS) -c $< -o $@
 $(OUT)/libskq.so: $(LIB_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(LIB_OBJS)
 
-all: lib oracle
+# test driver for the C++ drop-in signatures (tests/test_dropin.py)
+$(OUT)/skq_dropin_check: tests/dropin_check.cpp $(OUT)/libskq.so $(wildcard include/dropin/*.h)
+	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude/dropin $< -o $@ -L$(OUT) -lskq -Wl,-rpath,'$$ORIGIN'
+
+all: lib oracle $(OUT)/skq_dropin_check
 .PHONY: lib all
 .DEFAULT_GOAL := all

@@ -143,9 +143,11 @@ def main():
     nk = len(ks)
     # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"); an index lookup is priced at
     # the 8 B (key, list offset) it needs, a posting at its 4 B tid
+    fused = kt[1][1] == 0  # no k_probe launches: the sketch kernel probed (direct/rank table)
     b_kern = {
-        # read bases in; retained hashes, per-k counts, status out
-        "k_sketch": L + 4 * h + 4 * nk + 1,
+        # read bases in; retained hashes, per-k counts, status out (+ when fused: one lookup per
+        # hash, list offsets and the slow flag out)
+        "k_sketch": L + 4 * h + 4 * nk + 1 + ((8 * h + 4 * h + 1) if fused else 0),
         # status + counts + hashes in, one lookup per hash, list offsets + slow flag out
         "k_probe": 1 + 4 * nk + 4 * h + 8 * h + 4 * h + 1,
         # status + flag + counts + list offsets in, postings, candidates (tid, score) + count out,
@@ -153,7 +155,7 @@ def main():
         "k_count": 2 + 4 * nk + 4 * h + 4 * P + 4 + 8 * Cn + 8 * Cn,
     }
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
-    avg = {name: ms / max(cnt, 1) for name, (ms, cnt) in zip(("k_sketch", "k_probe", "k_count"), kt)}
+    avg = {name: ms / cnt for name, (ms, cnt) in zip(("k_sketch", "k_probe", "k_count"), kt) if cnt}
     kname = max(avg, key=avg.get)                       # dominant kernel
     achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
     traffic = None
@@ -196,7 +198,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname]},
-            "path": {"bytes_per_read": b_path, "achieved_GBps": value / world * b_path / 1e9,
+            "path": {"bytes_per_read": b_path, "probe": "fused in k_sketch" if fused else "k_probe",
+                     "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
                      "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn},
             "cpu_baseline": cpu,

@@ -84,6 +84,13 @@ int skq_session_free(skq_session* s);
  * threshold = (uint32_t)(UINT32_MAX * fraction) — skq_threshold(). */
 int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
                uint64_t n_reads, uint32_t max_len, uint32_t threshold, void* stream);
+/* createSketch_FracMinhash_direct semantics (include/sketch.h:47, src/sketch.cpp:24-39) on
+ * arbitrary sequences, e.g. transcripts or the C++ drop-in: no sequence is rejected (every
+ * status is SKQ_READ_OK), windows holding a byte outside ACGTUacgtu are skipped as ntHash skips
+ * them, lowercase hashes like uppercase and U like T, and a k longer than the sequence gives an
+ * empty set for that k. Same layout and session results as skq_sketch. */
+int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_offs, uint32_t fixed_len,
+                    uint64_t n_seqs, uint32_t max_len, uint32_t threshold, void* stream);
 /* Chain the session's current sketches; `fraction` as sparse_chain's (0.9 in quant).
  * accumulate != 0 adds each read's candidates into the per-transcript totals. */
 int skq_chain(skq_session* s, double fraction, int accumulate, void* stream);

@@ -63,7 +63,12 @@ struct skq_index {
     uint32_t* d_dir_t[SKQ_MAX_K] = {};
     const uint32_t* dir[SKQ_MAX_K] = {};
     uint64_t dir_len[SKQ_MAX_K] = {};
+    uint4* d_rank_t[SKQ_MAX_K] = {};
+    uint32_t* d_rovf_t[SKQ_MAX_K] = {};
+    const uint32_t* rank[SKQ_MAX_K] = {};
+    const uint32_t* rovf[SKQ_MAX_K] = {};
     uint64_t dir_bytes = 0;
+    int mode = 0;         // 1 = dir tables, 2 = rank tables (the sketch probes)
     bool direct = false;  // every slot with a table has a direct table: the sketch probes
 };
 
@@ -81,6 +86,7 @@ struct skq_session {
     uint64_t n_reads = 0;      // reads in the current results
     bool have_sketch = false;
     bool probed = false;       // the last skq_sketch also filled lofs/pflag (fused probe)
+    bool have_chain = false;   // candidates belong to the current batch
     uint8_t* status = nullptr;
     uint32_t* hash_cnt = nullptr;
     uint32_t* hashes = nullptr;
@@ -170,10 +176,53 @@ int ensure_hashes(skq_session* s, uint32_t hcap) {
 // hash. At the reference's fraction (double)0.05f keys are <= 214748367: 859 MB per k, which
 // HBM3E holds easily. Built only while the total stays inside SKQ_DIRECT_MB (default 8192 MiB;
 // 0 disables) and half the free device memory; otherwise probes go through the bucket table.
+int build_rank(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
+               const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals) {
+    uint64_t need = 0;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (dkeys[t].empty()) continue;
+        const uint64_t nb = ((uint64_t)dkeys[t].back() >> 5) + 1;
+        std::vector<uint4> blk(nb, make_uint4(0, 0, ~0u, ~0u));
+        std::vector<uint32_t> ovf;
+        for (size_t j = 0; j < dkeys[t].size(); ++j) {
+            const uint32_t key = dkeys[t][j];
+            uint4& b = blk[key >> 5];
+            const uint32_t pos = __builtin_popcount(b.x);
+            if (pos == 0) b.z = dvals[t][j];
+            else if (pos == 1) b.w = dvals[t][j];
+            else {
+                if (pos == 2) b.y = (uint32_t)ovf.size();
+                ovf.push_back(dvals[t][j]);
+            }
+            b.x |= 1u << (key & 31);
+        }
+        ovf.push_back(0);
+        if (dev_alloc(&ix->d_rank_t[t], nb) || dev_alloc(&ix->d_rovf_t[t], ovf.size()))
+            return fail(-3, "rank table allocation failed");
+        if (hipMemcpy(ix->d_rank_t[t], blk.data(), nb * 16, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(ix->d_rovf_t[t], ovf.data(), ovf.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(-3, "rank table upload failed");
+        need += nb * 16 + ovf.size() * 4;
+        for (uint32_t i = 0; i < ix->nk; ++i)
+            if (tables[t].k == ix->ks[i]) {
+                ix->rank[i] = reinterpret_cast<const uint32_t*>(ix->d_rank_t[t]);
+                ix->rovf[i] = ix->d_rovf_t[t];
+                ix->dir_len[i] = nb;
+            }
+    }
+    ix->dir_bytes = need;
+    ix->mode = 2;
+    ix->direct = true;
+    return 0;
+}
+
 int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
                  const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals) {
     uint64_t budget = 8192ull << 20;
     if (const char* e = std::getenv("SKQ_DIRECT_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
+    if (budget == 0) return 0;
+    if (const char* e = std::getenv("SKQ_PROBE"))
+        if (!std::strcmp(e, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
     uint64_t need = 0, len[SKQ_MAX_K] = {};
     for (uint32_t t = 0; t < ntables; ++t) {
         len[t] = dkeys[t].empty() ? 0 : (uint64_t)dkeys[t].back() + 1;  // keys ascending
@@ -210,6 +259,7 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
                 ix->dir_len[i] = len[t];
             }
     ix->direct = true;
+    ix->mode = 1;
     return 0;
 }
 
@@ -372,6 +422,8 @@ int skq_index_free(skq_index* ix) {
     if (!ix) return 0;
     DeviceGuard g(ix->device);
     for (auto& d : ix->d_dir_t) dev_free(d);
+    for (auto& d : ix->d_rank_t) dev_free(d);
+    for (auto& d : ix->d_rovf_t) dev_free(d);
     dev_free(ix->d_buckets);
     dev_free(ix->d_lists);
     dev_free(ix->d_rolltab);
@@ -405,6 +457,7 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     s->cand_ext_cap = 1ull << 22;
     s->scratch_cap = 1ull << 24;
     const uint32_t hcap0 = pick_hcap(Lc, ix->mink, skq_threshold((double)0.05f));
+    if (const char* e = std::getenv("SKQ_VARIANT")) s->variant = std::atoi(e);  // development A/B
     int rc = 0;
     if ((rc = dev_alloc(&s->status, max_reads)) || (rc = dev_alloc(&s->hash_cnt, max_reads * ix->nk)) ||
         (rc = dev_alloc(&s->hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&s->ovf1, s->ovf_cap)) ||
@@ -458,8 +511,8 @@ int skq_session_free(skq_session* s) {
     return 0;
 }
 
-int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
-               uint64_t n_reads, uint32_t max_len, uint32_t threshold, void* stream) {
+static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+                       uint64_t n_reads, uint32_t max_len, uint32_t threshold, int nthash, void* stream) {
     if (!s) return fail(-1, "null session");
     if (n_reads > s->max_reads) return fail(-1, "batch larger than the session's max_reads");
     if (n_reads && !d_reads) return fail(-1, "null reads");
@@ -490,13 +543,17 @@ int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, u
     p.hash_ext_cap = s->hash_ext_cap;
     p.ctrl = s->ctrl;
     p.ovf1 = s->ovf1;
-    p.fuse = ix->direct ? 1 : 0;
+    p.fuse = ix->mode;
     for (uint32_t i = 0; i < ix->nk; ++i) {
         p.dir[i] = ix->dir[i];
         p.dir_len[i] = ix->dir_len[i];
+        p.rank[i] = ix->rank[i];
+        p.rovf[i] = ix->rovf[i];
     }
     p.lofs = s->lofs;
     p.pflag = s->pflag;
+    p.variant = s->variant;
+    p.nthash = nthash;
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 8 * 4, st));
     hipEvent_t t0{};
     record(s, 0, &t0, st);
@@ -506,10 +563,21 @@ int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, u
     s->hcap = hcap;
     s->n_reads = n_reads;
     s->have_sketch = true;
+    s->have_chain = false;
     s->probed = ix->direct;
     s->x_hashes = nullptr;
     s->x_offs = nullptr;
     return 0;
+}
+
+int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+               uint64_t n_reads, uint32_t max_len, uint32_t threshold, void* stream) {
+    return sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream);
+}
+
+int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_offs, uint32_t fixed_len,
+                    uint64_t n_seqs, uint32_t max_len, uint32_t threshold, void* stream) {
+    return sketch_impl(s, d_seqs, d_offs, fixed_len, n_seqs, max_len, threshold, 1, stream);
 }
 
 static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const uint32_t* hash_cnt,
@@ -551,6 +619,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
     p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
     p.variant = s->variant;
+    p.ntx = ix->ntx;
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
     if (!probed) {
@@ -564,6 +633,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     if (skq::launch_chain_slow(p, stream)) return fail(-3, "chain slow-path launch failed");
     if (accumulate && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, ix->ntx, stream))
         return fail(-3, "totals fold launch failed");
+    s->have_chain = true;
     return 0;
 }
 
@@ -589,6 +659,7 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
     if (n_reads && (!d_hashes || !d_hash_offs || !d_hash_cnt)) return fail(-1, "null sketch arrays");
     s->n_reads = n_reads;
     s->have_sketch = false;
+    s->have_chain = false;
     s->probed = false;
     s->x_hashes = d_hashes;
     s->x_offs = d_hash_offs;
@@ -656,7 +727,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     std::vector<uint32_t> hc, cc(n);
     std::vector<uint8_t> st(n);
     if (n) {
-        HIP_TRY(hipMemcpy(cc.data(), s->cand_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
+        if (s->have_chain) HIP_TRY(hipMemcpy(cc.data(), s->cand_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
         if (s->have_sketch) {
             hc.resize(n * nk);  // [i][r]
             HIP_TRY(hipMemcpy(hc.data(), s->hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
@@ -698,7 +769,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     }
     if (cand_offs || cand_tid || cand_score) {
         std::vector<uint32_t> t((uint64_t)skq::CCAP * n), sc((uint64_t)skq::CCAP * n);  // [j][r]
-        if (n) {
+        if (n && s->have_chain) {
             HIP_TRY(hipMemcpy(t.data(), s->cand_tid, t.size() * 4, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(sc.data(), s->cand_score, sc.size() * 4, hipMemcpyDeviceToHost));
         }

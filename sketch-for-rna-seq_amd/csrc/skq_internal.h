@@ -82,11 +82,18 @@ struct SketchParams {
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
     // the slow chain path. Slots without a table (dir[i] null) are skipped by the chain.
-    int fuse;
+    int fuse;                        // 1 = dir tables, 2 = rank tables
     const uint32_t* dir[SKQ_MAX_K];
-    uint64_t dir_len[SKQ_MAX_K];
+    uint64_t dir_len[SKQ_MAX_K];     // dir: entries; rank: blocks
+    const uint32_t* rank[SKQ_MAX_K]; // rank table, 16-B blocks {bitmap of 32 keys, overflow base, v0, v1}
+    const uint32_t* rovf[SKQ_MAX_K]; // list offsets of the 3rd+ key of a block
     uint32_t* lofs;
     uint8_t* pflag;
+    int variant;  // development A/B switch (0 = default)
+    // ntHash mode (createSketch_FracMinhash_direct on arbitrary sequences, transcripts): no read
+    // is rejected; windows holding a byte outside ACGTUacgtu are skipped (src/sketch.cpp:31-36
+    // through ntHash); a k longer than the sequence yields an empty set for that k.
+    int nthash;
 };
 
 struct ChainParams {
@@ -121,6 +128,7 @@ struct ChainParams {
                                // [(i*lcap + j)*n + r], ~0u = miss
     uint8_t* pflag;            // -> k_count: 1 = read goes to the slow chain path
     uint32_t lcap;             // probes per (read, k) slot in lofs (reads above it: slow path)
+    uint32_t ntx;              // transcripts in the index
     int variant;               // development A/B switch (0 = default)
 };
 

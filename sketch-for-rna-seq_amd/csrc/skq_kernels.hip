@@ -151,6 +151,23 @@ __device__ __forceinline__ void encode4(uint32_t w, uint32_t& codes8, uint32_t& 
     codes8 = (t | (t >> 6) | (t >> 12) | (t >> 18)) & 0xFFu;
 }
 
+// 4-bit mask of bytes ntHash treats as invalid: anything but A C G T U, either case
+__device__ __forceinline__ uint32_t ntbad4(uint32_t w) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t c = ((w >> (8 * b)) & 0xFFu) | 0x20u;
+        const bool ok = c == 'a' || c == 'c' || c == 'g' || c == 't' || c == 'u';
+        m |= ok ? 0u : (1u << b);
+    }
+    return m;
+}
+
+__device__ __forceinline__ bool ntvalid(uint8_t b) {
+    const uint32_t c = b | 0x20u;
+    return c == 'a' || c == 'c' || c == 'g' || c == 't' || c == 'u';
+}
+
 // one roll step of the 33-bit lane kept as (lo: bits 0..31, hi: bit 32)
 __device__ __forceinline__ void roll33(uint32_t& lo, uint32_t& hi, uint64_t e) {
     const uint32_t nlo = (lo << 1) | hi;
@@ -174,7 +191,7 @@ size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap) {
     return b;
 }
 
-template <int HCAP>
+template <int HCAP, bool NTH>
 __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* s_tab = reinterpret_cast<uint64_t*>(smem);
@@ -208,6 +225,12 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
         encode4(v.y, b, bb);
         encode4(v.z, cc, bc);
         encode4(v.w, d, bd);
+        if (NTH) {
+            ba = ntbad4(v.x);
+            bb = ntbad4(v.y);
+            bc = ntbad4(v.z);
+            bd = ntbad4(v.w);
+        }
         s_codes[c] = a | (b << 8) | (cc << 16) | (d << 24);
         s_bad[c] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
     }
@@ -236,8 +259,9 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
                 bad |= m != 0;
             }
         }
+        if (NTH) bad = false;  // ntHash mode: invalid bases only skip windows
         if (bad) st = SKQ_READ_INVALID;
-        else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
+        else if (!NTH && len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
     }
 
     if (!slow && st == SKQ_READ_OK) {
@@ -248,19 +272,35 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
             const uint32_t d = q >> 4;
             return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
         };
+        // ntHash mode: invalid-base bits of 16 bases from tile position q
+        auto bad16 = [&](uint32_t q) -> uint32_t {
+            const uint32_t d = q >> 4;
+            const uint32_t hi = d + 1 < nch ? (uint32_t)s_bad[d + 1] : 0xFFFFu;
+            return ((hi << 16 | (uint32_t)s_bad[d]) >> (q & 15)) & 0xFFFFu;
+        };
         for (uint32_t i = 0; i < p.nk && !slow; ++i) {
             const uint32_t k = p.ks[i];
             const uint64_t* tab = s_tab + i * 16;
+            if (NTH && L < k) {  // createSketch on a sequence shorter than k: nothing to hash
+                p.hash_cnt[(uint64_t)i * p.n + r] = 0;
+                continue;
+            }
             // first window (NtHash::init): h = XOR_j rot^(k-1-j) seed(s_j)
             uint32_t hlo = 0, hhi = 0;
+            uint32_t nextok = 0;  // ntHash mode: first window start past the last invalid base
             for (uint32_t b = 0; b < k; b += 16) {
                 const uint32_t w = codes16((uint32_t)q0 + b);
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
                     if (b + j < k) roll33(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
+                if (NTH) {
+                    uint32_t bb = bad16((uint32_t)q0 + b);
+                    if (k - b < 16) bb &= (1u << (k - b)) - 1u;
+                    if (bb) nextok = b + 32 - __builtin_clz(bb);  // (highest bad) + 1
+                }
             }
             uint32_t nraw = 0;
-            if (hlo <= T) {  // src/sketch.cpp:33-35
+            if (hlo <= T && (!NTH || nextok == 0)) {  // src/sketch.cpp:33-35
                 s_raw[tid] = hlo;
                 nraw = 1;
             }
@@ -270,13 +310,17 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
             for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
                 const uint32_t win = codes16(qin + w0 - 1);
                 const uint32_t wout = codes16(qout + w0 - 1);
+                const uint32_t bin = NTH ? bad16(qin + w0 - 1) : 0u;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     if (w0 + j < nw) {
                         const uint32_t ci = (win >> (2 * j)) & 3u;
                         const uint32_t co = (wout >> (2 * j)) & 3u;
+                        // an invalid base rolls in and out with the same seed, so its term
+                        // cancels once it has left the window; windows holding it are skipped
                         roll33(hlo, hhi, tab[ci * 4 + co]);
-                        if (hlo <= T) {
+                        if (NTH && ((bin >> j) & 1u)) nextok = w0 + j + k;
+                        if (hlo <= T && (!NTH || w0 + j >= nextok)) {
                             if (nraw < HCAP) s_raw[nraw * WG + tid] = hlo;
                             ++nraw;
                         }
@@ -296,17 +340,47 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
             // wave's stores of one j are contiguous
             uint32_t* out = p.hashes + (uint64_t)i * p.hcap * p.n + r;
             uint32_t m = 0;
-            uint32_t keepm = 0;  // bit j: v[j] is the first of its run
+            uint64_t keepm = 0;  // bit j: v[j] is the first of its run (HCAP <= 64)
+            static_assert(HCAP <= 64, "keep mask is 64 bits");
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) {
                 const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
                 if (keep) {
                     out[(uint64_t)(m++) * p.n] = v[j];
-                    keepm |= 1u << j;
+                    keepm |= 1ull << j;
                 }
             }
             p.hash_cnt[(uint64_t)i * p.n + r] = m;
-            if (p.fuse && p.dir[i]) {
+            if (p.fuse == 2 && p.rank[i]) {
+                // fused probe, rank table: block h>>5 holds the bitmap of its 32 keys and the
+                // first two keys' list offsets; the rare 3rd+ key reads the overflow array
+                const uint4* rk = reinterpret_cast<const uint4*>(p.rank[i]);
+                const uint32_t* ro = p.rovf[i];
+                const uint64_t nb = p.dir_len[i];
+                uint32_t* lout = p.lofs + (uint64_t)i * p.hcap * p.n + r;
+                uint32_t mm = 0;
+#pragma unroll
+                for (int j0 = 0; j0 < HCAP; j0 += 8) {
+                    if (!__any((keepm >> j0) & 0xFFull)) break;
+                    uint4 bk[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const bool want = (keepm >> (j0 + u)) & 1ull;
+                        const uint32_t b = v[j0 + u] >> 5;
+                        bk[u] = want && b < nb ? rk[b] : make_uint4(0, 0, 0, 0);
+                    }
+                    uint32_t lo[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t bit = v[j0 + u] & 31u;
+                        const uint32_t pos = __builtin_popcount(bk[u].x & ((1u << bit) - 1u));
+                        lo[u] = !((bk[u].x >> bit) & 1u) ? ~0u : pos == 0 ? bk[u].z : pos == 1 ? bk[u].w : ro[bk[u].y + pos - 2];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if ((keepm >> (j0 + u)) & 1ull) lout[(uint64_t)(mm++) * p.n] = lo[u];
+                }
+            } else if (p.fuse && p.dir[i]) {
                 // fused probe: every kept hash's list offset, all loads in flight before the
                 // stores (a direct table is one 4-B gather per hash, no compare)
                 const uint32_t* dir = p.dir[i];
@@ -314,12 +388,19 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
                 uint32_t lo[HCAP];
 #pragma unroll
                 for (int j = 0; j < HCAP; ++j)
-                    lo[j] = ((keepm >> j) & 1u) && v[j] < dl ? dir[v[j]] : ~0u;
+                    lo[j] = ((keepm >> j) & 1ull) && v[j] < dl ? (p.variant == 1 ? v[j] : dir[v[j]]) : ~0u;
                 uint32_t* lout = p.lofs + (uint64_t)i * p.hcap * p.n + r;
                 uint32_t mm = 0;
+                if (p.variant == 2) {
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int j = 0; j < HCAP; ++j) x ^= lo[j];
+                    if (x == 0x12345678u) lout[0] = x;
+                } else {
 #pragma unroll
                 for (int j = 0; j < HCAP; ++j)
-                    if ((keepm >> j) & 1u) lout[(uint64_t)(mm++) * p.n] = lo[j];
+                    if ((keepm >> j) & 1ull) lout[(uint64_t)(mm++) * p.n] = lo[j];
+                }
             }
         }
     }
@@ -357,17 +438,19 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
         if (t == 0) s_bad = 0;
         __syncthreads();
         bool bad = false;
-        for (uint64_t q = t; q < len; q += WG) {
+        for (uint64_t q = t; q < len && !p.nthash; q += WG) {
             const uint8_t c = s[q];
             bad |= !(c == 'A' || c == 'C' || c == 'G' || c == 'T');
         }
         if (bad) s_bad = 1;
         __syncthreads();
-        const uint8_t st = s_bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
+        const uint8_t st = p.nthash ? SKQ_READ_OK
+                                    : s_bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
         for (uint32_t i = t; i < p.nk; i += WG) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
         if (st == SKQ_READ_OK) {
             for (uint32_t i = 0; i < p.nk; ++i) {
                 const uint32_t k = p.ks[i];
+                if (len < k) continue;  // (ntHash mode only: quant reads are >= every k)
                 const uint64_t nw = len - k + 1;
                 __syncthreads();
                 if (t == 0) {
@@ -388,11 +471,17 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                 const uint64_t wa = t * seg, wb = min(nw, wa + seg);
                 if (wa < wb) {
                     uint32_t hlo = 0, hhi = 0;
-                    for (uint64_t q = 0; q < k; ++q) roll33(hlo, hhi, seed[(s[wa + q] >> 1) & 3u]);
+                    uint64_t nextok = wa;  // ntHash mode: windows before it hold an invalid base
+                    for (uint64_t q = 0; q < k; ++q) {
+                        roll33(hlo, hhi, seed[(s[wa + q] >> 1) & 3u]);
+                        if (p.nthash && !ntvalid(s[wa + q])) nextok = wa + q + 1;
+                    }
                     for (uint64_t w = wa; w < wb; ++w) {
-                        if (w > wa)
+                        if (w > wa) {
                             roll33(hlo, hhi, tab[((s[w + k - 1] >> 1) & 3u) * 4 + ((s[w - 1] >> 1) & 3u)]);
-                        if (hlo <= p.threshold) buf[atomicAdd(&s_cnt, 1u)] = hlo;
+                            if (p.nthash && !ntvalid(s[w + k - 1])) nextok = w + k;
+                        }
+                        if (hlo <= p.threshold && w >= nextok) buf[atomicAdd(&s_cnt, 1u)] = hlo;
                     }
                 }
                 __syncthreads();
@@ -752,6 +841,10 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
         p.cand_cnt[r] = 0;  // not sketched (invalid or short read)
         return;
     }
+    if (p.variant >= 1 && p.variant <= 2) {  // sketch-side timing variants: lofs hold no offsets
+        p.cand_cnt[r] = 0;
+        return;
+    }
     if (p.pflag[r]) {  // flagged by k_probe / the fused sketch: the slow chain path takes it
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
@@ -870,6 +963,139 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
             cs[(uint64_t)d * p.n] = score;
             ++nc;
             // one packed atomic per candidate: reads in bits 40+, score below (<= 1020 per read)
+            if (p.accumulate)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[tid]), (1ull << 40) | score);
+        }
+    }
+    p.cand_cnt[r] = nc;
+}
+
+// k_count3: one lane per read, like k_count, with
+//   * the read's list offsets de-duplicated by a register sorting network (equal offsets form
+//     runs; a run of length c adds c to each transcript of that list at this k),
+//   * per-read transcript counts in a lane-private open-addressing table in LDS (slot s of
+//     lane t at [s][t]: bank-conflict free), so an insert is one probe in the common case,
+//   * 32-bit sort keys ((1023 - score) << 22 | tid; needs ntx <= 2^22, scores <= 4 * 255).
+constexpr int TS = 16;  // distinct transcripts per read on the fast path
+
+template <int NK>
+__global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
+    __shared__ uint32_t s_tid[TS][WG];
+    __shared__ uint32_t s_cnt[TS][WG];
+    const uint32_t t = threadIdx.x;
+    const uint64_t r = (uint64_t)blockIdx.x * WG + t;
+    if (r >= p.n) return;  // (no workgroup barriers below)
+    if (p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) {
+        p.cand_cnt[r] = 0;
+        return;
+    }
+    if (p.pflag[r]) {
+        list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+        p.cand_cnt[r] = 0;
+        return;
+    }
+    uint32_t occ = 0;  // bit s: slot s of this lane's table holds a transcript
+    bool slow = false;
+    auto insert = [&](uint32_t x, uint32_t inc) {
+        uint32_t sl = (x * 0x9E3779B1u) >> 28;
+        for (int q = 0; q < TS; ++q) {
+            if (!((occ >> sl) & 1u)) {
+                s_tid[sl][t] = x;
+                s_cnt[sl][t] = inc;
+                occ |= 1u << sl;
+                return;
+            }
+            if (s_tid[sl][t] == x) {
+                s_cnt[sl][t] += inc;
+                return;
+            }
+            sl = (sl + 1) & (TS - 1);
+        }
+        slow = true;  // more than TS distinct transcripts
+    };
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        if (!p.tabs[i].present || (p.present && !p.present[r * NK + i])) continue;
+        const uint32_t cnt = hash_count(p, r, i);
+        const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + r;
+        for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
+            uint32_t lv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) lv[u] = j0 + u < cnt ? lo_i[(uint64_t)(j0 + u) * p.n] : ~0u;
+            bitonic_sort<8>(lv);  // misses (~0u) sort last
+            uint32_t rl[8];
+            rl[7] = 1;
+#pragma unroll
+            for (int u = 6; u >= 0; --u) rl[u] = lv[u] == lv[u + 1] ? rl[u + 1] + 1 : 1;
+            uint4 head[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const bool start = lv[u] != ~0u && (u == 0 || lv[u] != lv[u - 1]);
+                head[u] = start ? *reinterpret_cast<const uint4*>(p.lists + lv[u]) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t n = head[u].x;  // 0 unless a run starts here
+                if (!n) continue;
+                const uint32_t inc = rl[u] << (8 * i);
+                insert(head[u].y, inc);
+                if (n > 1) insert(head[u].z, inc);
+                if (n > 2) insert(head[u].w, inc);
+                for (uint32_t q = 3; q < n; ++q) insert(p.lists[lv[u] + 1 + q], inc);
+            }
+        }
+    }
+    if (slow) {
+        list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+        p.cand_cnt[r] = 0;
+        return;
+    }
+    uint32_t tv[TS], cv[TS];
+#pragma unroll
+    for (int sl = 0; sl < TS; ++sl) {
+        const bool used = (occ >> sl) & 1u;
+        tv[sl] = used ? s_tid[sl][t] : 0u;
+        cv[sl] = used ? s_cnt[sl][t] : 0u;
+    }
+    // per-k maximum (src/sparse_chaining.cpp:76-82); (double)c >= fraction * max  <=>
+    // c >= ceil(fraction * max)   (:84-87, :93), as in k_count
+    uint32_t need[NK];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int sl = 0; sl < TS; ++sl) m = max(m, (cv[sl] >> (8 * i)) & 0xFFu);
+        const double thr = p.fraction * (double)m;
+        uint32_t ti = 0;
+        if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+        need[i] = ti;
+    }
+    uint32_t key[TS];
+#pragma unroll
+    for (int sl = 0; sl < TS; ++sl) {
+        bool ok = (occ >> sl) & 1u;
+        uint32_t score = 0;
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            const uint32_t c = (cv[sl] >> (8 * i)) & 0xFFu;
+            ok &= c >= need[i];
+            score += c;
+        }
+        // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
+        key[sl] = ok ? ((1023u - score) << 22) | tv[sl] : ~0u;
+    }
+    bitonic_sort<TS>(key);
+    uint32_t nc = 0;
+    uint32_t* ct = p.cand_tid + r;
+    uint32_t* cs = p.cand_score + r;
+#pragma unroll
+    for (int d = 0; d < TS; ++d) {
+        if (key[d] != ~0u) {
+            const uint32_t tid = key[d] & 0x3FFFFFu;
+            const uint32_t score = 1023u - (key[d] >> 22);
+            ct[(uint64_t)d * p.n] = tid;
+            cs[(uint64_t)d * p.n] = score;
+            ++nc;
             if (p.accumulate)
                 atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[tid]), (1ull << 40) | score);
         }
@@ -1059,10 +1285,13 @@ int launch_sketch(const SketchParams& p, void* stream) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, grid, dim3(WG), lds, s, p);
     };
-    switch (p.hcap) {
-    case 16: go(k_sketch<16>); break;
-    case 32: go(k_sketch<32>); break;
-    case 64: go(k_sketch<64>); break;
+    switch (p.hcap * 2 + (p.nthash ? 1 : 0)) {
+    case 32: go(k_sketch<16, false>); break;
+    case 64: go(k_sketch<32, false>); break;
+    case 128: go(k_sketch<64, false>); break;
+    case 33: go(k_sketch<16, true>); break;
+    case 65: go(k_sketch<32, true>); break;
+    case 129: go(k_sketch<64, true>); break;
     default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -1084,6 +1313,16 @@ int launch_probe(const ChainParams& p, void* stream) {
 int launch_count(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
+    if (p.variant == 3 && p.ntx <= (1u << 22)) {
+        switch (p.nk) {
+        case 1: hipLaunchKernelGGL(k_count3<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+        case 2: hipLaunchKernelGGL(k_count3<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+        case 3: hipLaunchKernelGGL(k_count3<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+        case 4: hipLaunchKernelGGL(k_count3<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+        default: break;
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     switch (p.nk) {
     case 1: hipLaunchKernelGGL(k_count<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
     case 2: hipLaunchKernelGGL(k_count<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;

@@ -55,6 +55,7 @@ def lib():
             "skq_session_create": (i32, [vp, u64, u32, C.POINTER(vp)]),
             "skq_session_free": (i32, [vp]),
             "skq_sketch": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
+            "skq_sketch_seqs": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
             "skq_chain": (i32, [vp, dbl, i32, vp]),
             "skq_map": (i32, [vp, vp, vp, u32, u64, u32, u32, dbl, i32, vp]),
             "skq_chain_sketches": (i32, [vp, u64, vp, vp, vp, vp, dbl, i32, vp]),
@@ -183,9 +184,13 @@ class Session:
         self.h = C.c_void_p()
         _check(lib().skq_session_create(index.h, int(max_reads), int(max_len), C.byref(self.h)))
 
-    def sketch(self, d_reads, d_offs, n_reads, max_len, fixed_len=0, thr=None, stream=None):
+    def sketch(self, d_reads, d_offs, n_reads, max_len, fixed_len=0, thr=None, stream=None,
+               nthash=False):
+        """nthash=False: quant reads (invalid/short reads rejected); True: createSketch on any
+        sequence (invalid-base windows skipped)."""
         thr = threshold() if thr is None else thr
-        _check(lib().skq_sketch(self.h, d_reads, d_offs, fixed_len, n_reads, max_len, thr, stream))
+        f = lib().skq_sketch_seqs if nthash else lib().skq_sketch
+        _check(f(self.h, d_reads, d_offs, fixed_len, n_reads, max_len, thr, stream))
 
     def chain(self, fraction=0.9, accumulate=True, stream=None):
         _check(lib().skq_chain(self.h, fraction, int(accumulate), stream))

@@ -88,6 +88,15 @@ def sketch(seq: bytes, k: int, thr=None):
     return [int(x) for x in out[:m]]
 
 
+def all_hashes(seq: bytes, k: int):
+    """extract_and_hash_kmers_nthash (src/kmer.cpp:19-35): every window's low 32 bits."""
+    out = np.zeros(max(len(seq), 1), np.uint32)
+    m = lib().orc_all_hashes(seq, len(seq), k, ptr(out))
+    if m == C.c_size_t(-1).value:
+        raise ValueError("len < k")
+    return [int(x) for x in out[:m]]
+
+
 class Index:
     """Oracle inverted index (build_kmer_to_transcript_map restated)."""
 
