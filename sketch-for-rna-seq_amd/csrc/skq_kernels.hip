@@ -168,6 +168,14 @@ __device__ __forceinline__ bool ntvalid(uint8_t b) {
     return c == 'a' || c == 'c' || c == 'g' || c == 't' || c == 'u';
 }
 
+// one roll step of the 33-bit lane kept as (lo: bits 0..31, hi31: bit 32 held in bit 31):
+// rot33 is one funnel shift, then the XOR with the roll term e
+__device__ __forceinline__ void roll33b(uint32_t& lo, uint32_t& hi31, uint2 e) {
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi31, 31);
+    hi31 = (lo & 0x80000000u) ^ e.y;
+    lo = nlo ^ e.x;
+}
+
 // one roll step of the 33-bit lane kept as (lo: bits 0..31, hi: bit 32)
 __device__ __forceinline__ void roll33(uint32_t& lo, uint32_t& hi, uint64_t e) {
     const uint32_t nlo = (lo << 1) | hi;
@@ -187,15 +195,16 @@ size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap) {
     size_t b = sketch_tab_bytes(nk);
     b += (((size_t)tile_chunks + 1) * 4 + 15) & ~(size_t)15;
     b += ((size_t)tile_chunks * 2 + 15) & ~(size_t)15;
-    b += (size_t)hcap * WG * 4;
+    b += ((size_t)hcap + 1) * WG * 4;  // + one spare slot per lane for windows not retained
     return b;
 }
 
 template <int HCAP, bool NTH>
 __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t* s_tab = reinterpret_cast<uint64_t*>(smem);
-    const uint64_t* s_seed = s_tab + p.nk * 16;
+    // roll terms as {bits 0..31, bit 32 moved to bit 31}
+    uint2* s_tab = reinterpret_cast<uint2*>(smem);
+    const uint2* s_seed = s_tab + p.nk * 16;
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(p.nk));
     uint16_t* s_bad = reinterpret_cast<uint16_t*>(
         reinterpret_cast<unsigned char*>(s_codes) + ((((size_t)p.tile_chunks + 1) * 4 + 15) & ~(size_t)15));
@@ -235,7 +244,10 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
         s_bad[c] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
     }
     if (tid == 0) s_codes[nch] = 0;
-    for (uint32_t e = tid; e < p.nk * 16 + 4; e += WG) s_tab[e] = p.rolltab[e];
+    for (uint32_t e = tid; e < p.nk * 16 + 4; e += WG) {
+        const uint64_t v = p.rolltab[e];
+        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
+    }
     __syncthreads();
 
     if ((uint32_t)tid >= nr) return;
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
         };
         for (uint32_t i = 0; i < p.nk && !slow; ++i) {
             const uint32_t k = p.ks[i];
-            const uint64_t* tab = s_tab + i * 16;
+            const uint2* tab = s_tab + i * 16;
             if (NTH && L < k) {  // createSketch on a sequence shorter than k: nothing to hash
                 p.hash_cnt[(uint64_t)i * p.n + r] = 0;
                 continue;
@@ -292,39 +304,47 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
                 const uint32_t w = codes16((uint32_t)q0 + b);
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
-                    if (b + j < k) roll33(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
+                    if (b + j < k) roll33b(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
                 if (NTH) {
                     uint32_t bb = bad16((uint32_t)q0 + b);
                     if (k - b < 16) bb &= (1u << (k - b)) - 1u;
                     if (bb) nextok = b + 32 - __builtin_clz(bb);  // (highest bad) + 1
                 }
             }
+            uint32_t* raw = s_raw + tid;
             uint32_t nraw = 0;
-            if (hlo <= T && (!NTH || nextok == 0)) {  // src/sketch.cpp:33-35
-                s_raw[tid] = hlo;
-                nraw = 1;
+            {   // src/sketch.cpp:33-35
+                const bool rec = hlo <= T && (!NTH || nextok == 0);
+                raw[0] = hlo;
+                nraw = rec ? 1u : 0u;
             }
-            // windows 1..nw-1: in-base at w + k - 1, out-base at w - 1
+            // windows 1..nw-1, 16 per block: in-base at w + k - 1, out-base at w - 1. The block's
+            // 16 roll terms depend only on the bases, so they are read from LDS before the serial
+            // roll; every window's value is stored at slot min(nraw, HCAP) (HCAP is a spare
+            // slot), so the block has no branches. Windows past nw roll garbage that is never
+            // recorded.
             const uint32_t nw = L - k + 1;
             const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
             for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
                 const uint32_t win = codes16(qin + w0 - 1);
                 const uint32_t wout = codes16(qout + w0 - 1);
                 const uint32_t bin = NTH ? bad16(qin + w0 - 1) : 0u;
+                const uint32_t jn = nw - w0;  // windows left (this block takes min(jn, 16))
+                uint2 e[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    e[j] = tab[((win >> (2 * j)) & 3u) * 4 + ((wout >> (2 * j)) & 3u)];
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    if (w0 + j < nw) {
-                        const uint32_t ci = (win >> (2 * j)) & 3u;
-                        const uint32_t co = (wout >> (2 * j)) & 3u;
-                        // an invalid base rolls in and out with the same seed, so its term
-                        // cancels once it has left the window; windows holding it are skipped
-                        roll33(hlo, hhi, tab[ci * 4 + co]);
-                        if (NTH && ((bin >> j) & 1u)) nextok = w0 + j + k;
-                        if (hlo <= T && (!NTH || w0 + j >= nextok)) {
-                            if (nraw < HCAP) s_raw[nraw * WG + tid] = hlo;
-                            ++nraw;
-                        }
-                    }
+                    // an invalid base (ntHash mode) rolls in and out with the same term, so it
+                    // cancels once it has left the window; windows holding it are skipped
+                    roll33b(hlo, hhi, e[j]);
+                    if (NTH) nextok = ((bin >> j) & 1u) ? w0 + j + k : nextok;
+                    const bool rec = hlo <= T && (uint32_t)j < jn && (!NTH || w0 + j >= nextok);
+                    // written at slot nraw either way: only a retained value advances nraw, an
+                    // unretained one is overwritten later or lies past nraw
+                    raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
+                    nraw += rec ? 1u : 0u;
                 }
             }
             if (nraw > HCAP) {
