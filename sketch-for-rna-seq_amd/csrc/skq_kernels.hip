@@ -227,8 +227,21 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     const uint64_t c1 = (sl + ll + delta + 15) >> 4;
     const uint32_t nch = (uint32_t)min((uint64_t)p.tile_chunks, c1 - c0);
 
-    for (uint32_t c = tid; c < nch; c += WG) {
-        const uint4 v = *reinterpret_cast<const uint4*>(abase + (c0 + c) * 16);
+    // staging: SU loads per lane in flight before any is used (a load inside a guarded loop body
+    // would be waited for before the next one issues); indices past the span are clamped to
+    // its last chunk, which is valid memory
+    const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
+    constexpr uint32_t SU = 8;
+    for (uint32_t cb = tid; cb < nch; cb += SU * WG) {
+        uint4 vv[SU];
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * WG, nch - 1)];
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) {
+        // encoded unconditionally (only the LDS stores are guarded), so no load can be sunk
+        // behind a branch and waited for on its own
+        const uint32_t c = cb + u * WG;
+        const uint4 v = vv[u];
         uint32_t a, b, cc, d, ba, bb, bc, bd;
         encode4(v.x, a, ba);
         encode4(v.y, b, bb);
@@ -240,8 +253,11 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
             bc = ntbad4(v.z);
             bd = ntbad4(v.w);
         }
-        s_codes[c] = a | (b << 8) | (cc << 16) | (d << 24);
-        s_bad[c] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
+        if (c < nch) {
+            s_codes[c] = a | (b << 8) | (cc << 16) | (d << 24);
+            s_bad[c] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
+        }
+        }
     }
     if (tid == 0) s_codes[nch] = 0;
     for (uint32_t e = tid; e < p.nk * 16 + 4; e += WG) {
@@ -385,9 +401,9 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
                     uint4 bk[8];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        const bool want = (keepm >> (j0 + u)) & 1ull;
-                        const uint32_t b = v[j0 + u] >> 5;
-                        bk[u] = want && b < nb ? rk[b] : make_uint4(0, 0, 0, 0);
+                        const bool want = ((keepm >> (j0 + u)) & 1ull) && (v[j0 + u] >> 5) < nb;
+                        const uint4 x = rk[want ? v[j0 + u] >> 5 : 0u];  // unconditional: all in flight
+                        bk[u] = want ? x : make_uint4(0, 0, 0, 0);
                     }
                     uint32_t lo[8];
 #pragma unroll
@@ -407,8 +423,13 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
                 const uint64_t dl = p.dir_len[i];
                 uint32_t lo[HCAP];
 #pragma unroll
-                for (int j = 0; j < HCAP; ++j)
-                    lo[j] = ((keepm >> j) & 1ull) && v[j] < dl ? (p.variant == 1 ? v[j] : dir[v[j]]) : ~0u;
+                for (int j = 0; j < HCAP; ++j) {
+                    // every gather issues (index 0 when there is nothing to probe) so all are in
+                    // flight together; a guarded load would be waited for one at a time
+                    const bool want = ((keepm >> j) & 1ull) && v[j] < dl;
+                    const uint32_t x = p.variant == 1 ? v[j] : dir[want ? v[j] : 0u];
+                    lo[j] = want ? x : ~0u;
+                }
                 uint32_t* lout = p.lofs + (uint64_t)i * p.hcap * p.n + r;
                 uint32_t mm = 0;
                 if (p.variant == 2) {
@@ -857,7 +878,13 @@ template <int NK>
 __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
     if (r >= p.n) return;
-    if (p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) {
+    // the per-read words are loaded together, before anything branches on them
+    uint32_t cnts[NK];
+    const uint8_t st = p.status ? p.status[r] : (uint8_t)SKQ_READ_OK;
+    const uint8_t pf = p.pflag[r];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, r, i);
+    if ((st & SKQ_STATUS_MASK) != SKQ_READ_OK) {
         p.cand_cnt[r] = 0;  // not sketched (invalid or short read)
         return;
     }
@@ -865,7 +892,7 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
         p.cand_cnt[r] = 0;
         return;
     }
-    if (p.pflag[r]) {  // flagged by k_probe / the fused sketch: the slow chain path takes it
+    if (pf) {  // flagged by k_probe / the fused sketch: the slow chain path takes it
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
         return;
@@ -876,7 +903,7 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
         if (!p.tabs[i].present || (p.present && !p.present[r * NK + i])) continue;
-        const uint32_t cnt = hash_count(p, r, i);
+        const uint32_t cnt = cnts[i];
         const uint32_t inc = 1u << (8 * i);
         const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + r;
         for (uint32_t j0 = 0; j0 < cnt && !slow; j0 += 4) {  // 4 coalesced loads in flight
@@ -1005,11 +1032,16 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
     const uint32_t t = threadIdx.x;
     const uint64_t r = (uint64_t)blockIdx.x * WG + t;
     if (r >= p.n) return;  // (no workgroup barriers below)
-    if (p.status && (p.status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK) {
+    uint32_t cnts[NK];
+    const uint8_t st = p.status ? p.status[r] : (uint8_t)SKQ_READ_OK;
+    const uint8_t pf = p.pflag[r];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, r, i);
+    if ((st & SKQ_STATUS_MASK) != SKQ_READ_OK) {
         p.cand_cnt[r] = 0;
         return;
     }
-    if (p.pflag[r]) {
+    if (pf) {
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
         return;
@@ -1036,7 +1068,7 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
         if (!p.tabs[i].present || (p.present && !p.present[r * NK + i])) continue;
-        const uint32_t cnt = hash_count(p, r, i);
+        const uint32_t cnt = cnts[i];
         const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + r;
         for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
             uint32_t lv[8];
