@@ -1021,22 +1021,35 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
 //   * the read's list offsets de-duplicated by a register sorting network (equal offsets form
 //     runs; a run of length c adds c to each transcript of that list at this k),
 //   * per-read transcript counts in a lane-private open-addressing table in LDS (slot s of
-//     lane t at [s][t]: bank-conflict free), so an insert is one probe in the common case,
+//     lane t at [s][t]: bank-conflict free; one word (tid << 8 | count) per slot when there is
+//     one k, else a tid word and a packed-counts word). Every insert makes one branch-free
+//     probe (a write that does not land goes to the lane's sink slot); items whose slot is
+//     taken by another transcript are parked in a per-lane pending list and placed by one
+//     probing loop at the end,
+//   * the per-read words and the first 8 list offsets loaded together up front, and the list
+//     heads and second quads (tids 3..6) gathered in batches,
 //   * 32-bit sort keys ((1023 - score) << 22 | tid; needs ntx <= 2^22, scores <= 4 * 255).
-constexpr int TS = 16;  // distinct transcripts per read on the fast path
+constexpr int TS = 16;    // distinct transcripts per read on the fast path (slot TS: sink)
+constexpr int PEND = 8;   // parked collisions per read (slot PEND: sink)
 
 template <int NK>
 __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
-    __shared__ uint32_t s_tid[TS][WG];
-    __shared__ uint32_t s_cnt[TS][WG];
+    constexpr int W = NK == 1 ? 1 : 2;  // LDS words per slot
+    __shared__ uint32_t s_tab[(TS + 1) * W][WG];
+    __shared__ uint32_t s_pend[PEND + 1][WG];
     const uint32_t t = threadIdx.x;
     const uint64_t r = (uint64_t)blockIdx.x * WG + t;
     if (r >= p.n) return;  // (no workgroup barriers below)
+    // one round trip for everything the read needs first: offsets past the read's count are
+    // read and ignored (the lofs array spans lcap >= 16 slots per k)
     uint32_t cnts[NK];
     const uint8_t st = p.status ? p.status[r] : (uint8_t)SKQ_READ_OK;
     const uint8_t pf = p.pflag[r];
 #pragma unroll
     for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, r, i);
+    uint32_t lv0[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) lv0[u] = p.lofs[(uint64_t)u * p.n + r];
     if ((st & SKQ_STATUS_MASK) != SKQ_READ_OK) {
         p.cand_cnt[r] = 0;
         return;
@@ -1046,24 +1059,35 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
         p.cand_cnt[r] = 0;
         return;
     }
-    uint32_t occ = 0;  // bit s: slot s of this lane's table holds a transcript
-    bool slow = false;
-    auto insert = [&](uint32_t x, uint32_t inc) {
-        uint32_t sl = (x * 0x9E3779B1u) >> 28;
-        for (int q = 0; q < TS; ++q) {
-            if (!((occ >> sl) & 1u)) {
-                s_tid[sl][t] = x;
-                s_cnt[sl][t] = inc;
-                occ |= 1u << sl;
-                return;
-            }
-            if (s_tid[sl][t] == x) {
-                s_cnt[sl][t] += inc;
-                return;
-            }
-            sl = (sl + 1) & (TS - 1);
+    uint32_t occ = 0;  // bit s: slot s holds a transcript
+    uint32_t np = 0;   // parked items
+    auto slot_of = [](uint32_t x) -> uint32_t { return (x * 0x9E3779B1u) >> 28; };
+    // item: transcript x gains rl at k slot i
+    auto insert = [&](uint32_t x, uint32_t rl, int i, bool valid) {
+        const uint32_t sl = slot_of(x);
+        const bool used = (occ >> sl) & 1u;
+        bool hit;
+        if (W == 1) {
+            const uint32_t e = s_tab[sl][t];
+            hit = used && (e >> 8) == x;
+            const bool take = valid && (!used || hit);
+            s_tab[take ? sl : (uint32_t)TS][t] = hit ? e + rl : (x << 8) | rl;
+            occ |= take ? (1u << sl) : 0u;
+            const bool park = valid && !take;
+            s_pend[min(np, (uint32_t)PEND)][t] = x | (rl << 22) | ((uint32_t)i << 29);
+            np += park ? 1u : 0u;
+        } else {
+            const uint32_t tx = s_tab[2 * sl][t], cx = s_tab[2 * sl + 1][t];
+            hit = used && tx == x;
+            const bool take = valid && (!used || hit);
+            const uint32_t ws = take ? sl : (uint32_t)TS;
+            s_tab[2 * ws][t] = x;
+            s_tab[2 * ws + 1][t] = (hit ? cx : 0u) + (rl << (8 * i));
+            occ |= take ? (1u << sl) : 0u;
+            const bool park = valid && !take;
+            s_pend[min(np, (uint32_t)PEND)][t] = x | (rl << 22) | ((uint32_t)i << 29);
+            np += park ? 1u : 0u;
         }
-        slow = true;  // more than TS distinct transcripts
     };
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
@@ -1073,68 +1097,145 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
         for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
             uint32_t lv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) lv[u] = j0 + u < cnt ? lo_i[(uint64_t)(j0 + u) * p.n] : ~0u;
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t x = (i == 0 && j0 == 0) ? lv0[u] : lo_i[(uint64_t)min(j0 + u, p.lcap - 1) * p.n];
+                lv[u] = j0 + u < cnt ? x : ~0u;
+            }
             bitonic_sort<8>(lv);  // misses (~0u) sort last
             uint32_t rl[8];
             rl[7] = 1;
 #pragma unroll
             for (int u = 6; u >= 0; --u) rl[u] = lv[u] == lv[u + 1] ? rl[u + 1] + 1 : 1;
-            uint4 head[8];
+            // compact the distinct lists to the front: (offset << 3 | run - 1) for run starts
+            // (offsets < 2^29 words, runs <= 8), everything else sorts last
+            uint32_t dl[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const bool start = lv[u] != ~0u && (u == 0 || lv[u] != lv[u - 1]);
-                head[u] = start ? *reinterpret_cast<const uint4*>(p.lists + lv[u]) : make_uint4(0, 0, 0, 0);
+                dl[u] = start ? (lv[u] << 3) | (rl[u] - 1) : ~0u;
             }
+            bitonic_sort<8>(dl);
+            // distinct lists 4 at a time: heads, then the second quads (tids 3..6) of the
+            // lists longer than 3, each batch in flight together
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t n = head[u].x;  // 0 unless a run starts here
-                if (!n) continue;
-                const uint32_t inc = rl[u] << (8 * i);
-                insert(head[u].y, inc);
-                if (n > 1) insert(head[u].z, inc);
-                if (n > 2) insert(head[u].w, inc);
-                for (uint32_t q = 3; q < n; ++q) insert(p.lists[lv[u] + 1 + q], inc);
+            for (int u0 = 0; u0 < 8; u0 += 4) {
+                if (u0 && !__any(dl[u0] != ~0u)) break;
+                uint4 head[4], more[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool v = dl[u0 + u] != ~0u;
+                    const uint4 h = *reinterpret_cast<const uint4*>(p.lists + (v ? dl[u0 + u] >> 3 : 0u));
+                    head[u] = v ? h : make_uint4(0, 0, 0, 0);
+                }
+                bool lng = false;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) lng |= head[u].x > 3;
+                const bool any_long = __any(lng);
+                if (any_long) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool l = head[u].x > 3;
+                        const uint4 h = *reinterpret_cast<const uint4*>(p.lists + (l ? (dl[u0 + u] >> 3) + 4 : 0u));
+                        more[u] = l ? h : make_uint4(0, 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t n = head[u].x;  // 0 past the distinct lists
+                    const uint32_t run = (dl[u0 + u] & 7u) + 1;
+                    insert(head[u].y, run, i, n > 0);
+                    insert(head[u].z, run, i, n > 1);
+                    insert(head[u].w, run, i, n > 2);
+                    if (any_long) {
+                        insert(more[u].x, run, i, n > 3);
+                        insert(more[u].y, run, i, n > 4);
+                        insert(more[u].z, run, i, n > 5);
+                        insert(more[u].w, run, i, n > 6);
+                    }
+                }
+                // lists longer than 7 (rare): one at a time
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (__any(head[u].x > 7))
+                        for (uint32_t q = 7; q < head[u].x; ++q)
+                            insert(p.lists[(dl[u0 + u] >> 3) + 1 + q], (dl[u0 + u] & 7u) + 1, i, true);
             }
         }
+    }
+    // parked items: full linear probing
+    bool slow = np > (uint32_t)PEND;
+    for (uint32_t e = 0; e < np && !slow; ++e) {
+        const uint32_t it = s_pend[e][t];
+        const uint32_t x = it & 0x3FFFFFu, rl = (it >> 22) & 0x7Fu;
+        const int i = (int)(it >> 29);
+        uint32_t q = slot_of(x);
+        bool done = false;
+        for (int z = 0; z < TS && !done; ++z) {
+            const bool used = (occ >> q) & 1u;
+            if (W == 1) {
+                const uint32_t ev = s_tab[q][t];
+                if (!used || (ev >> 8) == x) {
+                    s_tab[q][t] = used ? ev + rl : (x << 8) | rl;
+                    occ |= 1u << q;
+                    done = true;
+                }
+            } else {
+                const uint32_t tx = s_tab[2 * q][t];
+                if (!used || tx == x) {
+                    s_tab[2 * q][t] = x;
+                    s_tab[2 * q + 1][t] = (used ? s_tab[2 * q + 1][t] : 0u) + (rl << (8 * i));
+                    occ |= 1u << q;
+                    done = true;
+                }
+            }
+            q = (q + 1) & (TS - 1);
+        }
+        slow = !done;  // more than TS distinct transcripts
     }
     if (slow) {
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
         return;
     }
-    uint32_t tv[TS], cv[TS];
-#pragma unroll
-    for (int sl = 0; sl < TS; ++sl) {
-        const bool used = (occ >> sl) & 1u;
-        tv[sl] = used ? s_tid[sl][t] : 0u;
-        cv[sl] = used ? s_cnt[sl][t] : 0u;
-    }
-    // per-k maximum (src/sparse_chaining.cpp:76-82); (double)c >= fraction * max  <=>
-    // c >= ceil(fraction * max)   (:84-87, :93), as in k_count
+    // two passes over the table (the slots are re-read rather than held in registers):
+    // per-k maximum (src/sparse_chaining.cpp:76-82), then the filter
+    // (double)c >= fraction * max  <=>  c >= ceil(fraction * max)  (:84-87, :93), as in k_count
+    auto slot_counts = [&](int sl) -> uint32_t {
+        const uint32_t c = W == 1 ? s_tab[sl][t] & 0xFFu : s_tab[2 * sl + 1][t];
+        return ((occ >> sl) & 1u) ? c : 0u;
+    };
     uint32_t need[NK];
+    {
+        uint32_t m[NK] = {};
 #pragma unroll
-    for (int i = 0; i < NK; ++i) {
-        uint32_t m = 0;
+        for (int sl = 0; sl < TS; ++sl) {
+            const uint32_t c = slot_counts(sl);
 #pragma unroll
-        for (int sl = 0; sl < TS; ++sl) m = max(m, (cv[sl] >> (8 * i)) & 0xFFu);
-        const double thr = p.fraction * (double)m;
-        uint32_t ti = 0;
-        if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
-        need[i] = ti;
+            for (int i = 0; i < NK; ++i) m[i] = max(m[i], (c >> (8 * i)) & 0xFFu);
+        }
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            const double thr = p.fraction * (double)m[i];
+            uint32_t ti = 0;
+            if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+            need[i] = ti;
+        }
     }
     uint32_t key[TS];
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) {
+        const uint32_t c = slot_counts(sl);
+        const uint32_t tid = W == 1 ? s_tab[sl][t] >> 8 : s_tab[2 * sl][t];
         bool ok = (occ >> sl) & 1u;
         uint32_t score = 0;
 #pragma unroll
         for (int i = 0; i < NK; ++i) {
-            const uint32_t c = (cv[sl] >> (8 * i)) & 0xFFu;
-            ok &= c >= need[i];
-            score += c;
+            const uint32_t ci = (c >> (8 * i)) & 0xFFu;
+            ok &= ci >= need[i];
+            score += ci;
         }
         // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
-        key[sl] = ok ? ((1023u - score) << 22) | tv[sl] : ~0u;
+        key[sl] = ok ? ((1023u - score) << 22) | tid : ~0u;
     }
     bitonic_sort<TS>(key);
     uint32_t nc = 0;
@@ -1365,7 +1466,9 @@ int launch_probe(const ChainParams& p, void* stream) {
 int launch_count(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    if (p.variant == 3 && p.ntx <= (1u << 22)) {
+    // k_count3 (32-bit sort keys) unless transcript ids need more than 22 bits; variant 4 forces
+    // the wide kernel for A/B timing
+    if (p.ntx <= (1u << 22) && p.variant != 4) {
         switch (p.nk) {
         case 1: hipLaunchKernelGGL(k_count3<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
         case 2: hipLaunchKernelGGL(k_count3<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;

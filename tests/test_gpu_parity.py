@@ -263,6 +263,28 @@ def test_index_without_some_k():
     compare(out, ref, len(reads), 2)
 
 
+def test_wide_transcript_ids_take_the_64bit_key_kernel():
+    """ntx > 2^22: candidates are sorted with 64-bit keys (k_count); ids near the top of the
+    range must come back intact."""
+    rng = np.random.default_rng(8)
+    ntx = (1 << 22) + 50
+    tx = synth.transcriptome(60, seed=9)
+    seqs = [tx.seq(t) for t in range(tx.ntx)]
+    remap = np.array(sorted(rng.choice(ntx, size=len(seqs), replace=False)), np.uint32)
+    remap[-3:] = [ntx - 3, ntx - 2, ntx - 1]
+    oi0 = orc.Index([31], seqs=seqs)
+    keys, offs, tids = oi0.csr(0)
+    h = np.repeat(keys, np.diff(offs.astype(np.int64)))
+    pairs = [(h, remap[tids])]
+    gi, oi = build([31], pairs=pairs, ntx=ntx)
+    bases, _, _ = synth.reads(tx, 300, 150, seed=10)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(300)]
+    out = run_gpu(gi, reads)
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), 1)
+    assert int(out["cand_tid"].max()) >= (1 << 22)
+
+
 def test_chain_sketches_entry_point(tx300):
     gi, oi = build([21, 31], tx=tx300)
     bases, _, _ = synth.reads(tx300, 500, 150, seed=30)
