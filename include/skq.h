@@ -161,11 +161,14 @@ int skq_stream_sync(void* stream);
 /* Kernel timing: with timing enabled, every skq_sketch / skq_chain call records HIP events on
  * its stream around its fast kernel. skq_session_kernel_time waits for them and returns the
  * summed milliseconds and launch count of one kind since the last query (then forgets them).
- * kind: 0 = k_sketch, 1 = k_probe, 2 = k_count. Used by bench.py for the roofline figure. */
+ * kind: 0 = k_sketch, 1 = k_probe, 2 = k_count, 3 = per-transcript totals (k_bin + k_bin_sum +
+ * k_fold_totals). Used by bench.py for the roofline figure. */
 int skq_session_enable_timing(skq_session* s, int enable);
 /* Development A/B switch for the chain kernel (0 = default). Not needed by users. */
 int skq_session_set_variant(skq_session* s, int variant);
 int skq_session_kernel_time(skq_session* s, int kind, double* total_ms, uint64_t* launches);
+/* Reads of the last batch that took the slow sketch / slow chain path (synchronous). */
+int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chain_slow);
 
 #ifdef __cplusplus
 }

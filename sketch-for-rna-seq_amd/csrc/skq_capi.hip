@@ -105,6 +105,10 @@ struct skq_session {
     uint64_t* scratch = nullptr;
     uint64_t scratch_cap = 0;
     uint64_t* tx_acc = nullptr;
+    // per-transcript totals by buckets of 2^bin_bits ids (k_bin / k_bin_sum); bin_nb = 0: direct
+    uint32_t bin_bits = 13, bin_nb = 0;
+    uint32_t* bin_hdr = nullptr;
+    uint32_t* bin_region = nullptr;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     uint32_t* ctrl = nullptr;
@@ -439,6 +443,16 @@ int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npost
     return 0;
 }
 
+int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chain_slow) {
+    if (!s) return fail(-1, "null session");
+    DeviceGuard g(s->idx->device);
+    uint32_t c[skq::C_WORDS];
+    HIP_TRY(hipMemcpy(c, s->ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    if (sketch_slow) *sketch_slow = c[skq::C_OVF1];
+    if (chain_slow) *chain_slow = c[skq::C_OVF2];
+    return 0;
+}
+
 int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? 1 : 0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
@@ -469,6 +483,15 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
         (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
         (rc = dev_alloc(&s->tx_acc, ix->ntx)) ||
         (rc = dev_alloc(&s->ctrl, skq::C_WORDS)) || (rc = ensure_hashes(s, hcap0))) {
+        skq_session_free(s);
+        return rc;
+    }
+    // totals buckets: at most WG buckets of at most 2^14 ids (the LDS histogram), else direct
+    while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
+    s->bin_nb = s->bin_bits <= 14 ? (uint32_t)(((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits) : 0u;
+    const uint64_t nW = (max_reads + skq::WG - 1) / skq::WG;
+    if (s->bin_nb && ((rc = dev_alloc(&s->bin_hdr, (uint64_t)(s->bin_nb + 1) * nW)) ||
+                      (rc = dev_alloc(&s->bin_region, nW * skq::WG * skq::CCAP)))) {
         skq_session_free(s);
         return rc;
     }
@@ -504,6 +527,8 @@ int skq_session_free(skq_session* s) {
     dev_free(s->cand_ext);
     dev_free(s->scratch);
     dev_free(s->tx_acc);
+    dev_free(s->bin_hdr);
+    dev_free(s->bin_region);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -620,6 +645,11 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
     p.variant = s->variant;
     p.ntx = ix->ntx;
+    p.bin_bits = s->bin_bits;
+    p.bin_nb = s->bin_nb;
+    p.bin_hdr = s->bin_hdr;
+    p.bin_region = s->bin_region;
+    p.slow_totals = accumulate && skq::count_bins(p);
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
     if (!probed) {
@@ -631,8 +661,14 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     if (skq::launch_count(p, stream)) return fail(-3, "count launch failed");
     record_stop(s, 2, t0, st);
     if (skq::launch_chain_slow(p, stream)) return fail(-3, "chain slow-path launch failed");
-    if (accumulate && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, ix->ntx, stream))
-        return fail(-3, "totals fold launch failed");
+    if (accumulate) {
+        record(s, 3, &t0, st);
+        if (skq::launch_bin(p, p.slow_totals, stream))
+            return fail(-3, "totals launch failed");
+        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, ix->ntx, stream))
+            return fail(-3, "totals fold launch failed");
+        record_stop(s, 3, t0, st);
+    }
     s->have_chain = true;
     return 0;
 }

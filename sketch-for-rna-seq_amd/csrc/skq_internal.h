@@ -129,6 +129,12 @@ struct ChainParams {
     uint8_t* pflag;            // -> k_count: 1 = read goes to the slow chain path
     uint32_t lcap;             // probes per (read, k) slot in lofs (reads above it: slow path)
     uint32_t ntx;              // transcripts in the index
+    // per-transcript totals by buckets of 2^bin_bits ids (k_count3 or k_bin, then k_bin_sum);
+    // slow_totals: k_chain_slow adds its reads' totals itself (the count kernel binned)
+    uint32_t bin_bits, bin_nb;
+    uint32_t* bin_hdr;
+    uint32_t* bin_region;
+    int slow_totals;
     int variant;               // development A/B switch (0 = default)
 };
 
@@ -142,6 +148,11 @@ int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream);
 int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
+// per-transcript totals of the batch's final candidates into p.tx_acc (k_bin + k_bin_sum)
+// (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs)
+int launch_bin(const ChainParams& p, int binned, void* stream);
+// whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)
+bool count_bins(const ChainParams& p);
 int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n, void* stream);
 
 #ifdef __HIPCC__

@@ -1009,12 +1009,19 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
             ct[(uint64_t)d * p.n] = tid;
             cs[(uint64_t)d * p.n] = score;
             ++nc;
-            // one packed atomic per candidate: reads in bits 40+, score below (<= 1020 per read)
-            if (p.accumulate)
-                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[tid]), (1ull << 40) | score);
         }
     }
     p.cand_cnt[r] = nc;
+}
+
+// More k slots than the count kernels take (NK_FAST): every sketched read goes to the slow chain
+// path; the others get no candidates.
+__global__ __launch_bounds__(WG) void k_route_slow(ChainParams p) {
+    const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
+    if (r >= p.n) return;
+    p.cand_cnt[r] = 0;
+    if (!p.status || (p.status[r] & SKQ_STATUS_MASK) == SKQ_READ_OK)
+        list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
 }
 
 // k_count3: one lane per read, like k_count, with
@@ -1032,14 +1039,12 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
 constexpr int TS = 16;    // distinct transcripts per read on the fast path (slot TS: sink)
 constexpr int PEND = 8;   // parked collisions per read (slot PEND: sink)
 
+// one read of k_count3: writes its candidates (and cand_cnt) and returns their number, the
+// first nc of key[] holding them in output order
 template <int NK>
-__global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
+__device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r, uint32_t t, uint32_t (*s_tab)[WG],
+                                               uint32_t (*s_pend)[WG], uint32_t (&key)[TS]) {
     constexpr int W = NK == 1 ? 1 : 2;  // LDS words per slot
-    __shared__ uint32_t s_tab[(TS + 1) * W][WG];
-    __shared__ uint32_t s_pend[PEND + 1][WG];
-    const uint32_t t = threadIdx.x;
-    const uint64_t r = (uint64_t)blockIdx.x * WG + t;
-    if (r >= p.n) return;  // (no workgroup barriers below)
     // one round trip for everything the read needs first: offsets past the read's count are
     // read and ignored (the lofs array spans lcap >= 16 slots per k)
     uint32_t cnts[NK];
@@ -1052,12 +1057,12 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
     for (int u = 0; u < 8; ++u) lv0[u] = p.lofs[(uint64_t)u * p.n + r];
     if ((st & SKQ_STATUS_MASK) != SKQ_READ_OK) {
         p.cand_cnt[r] = 0;
-        return;
+        return 0;
     }
     if (pf) {
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
-        return;
+        return 0;
     }
     uint32_t occ = 0;  // bit s: slot s holds a transcript
     uint32_t np = 0;   // parked items
@@ -1195,7 +1200,7 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
     if (slow) {
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
-        return;
+        return 0;
     }
     // two passes over the table (the slots are re-read rather than held in registers):
     // per-k maximum (src/sparse_chaining.cpp:76-82), then the filter
@@ -1221,7 +1226,6 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
             need[i] = ti;
         }
     }
-    uint32_t key[TS];
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) {
         const uint32_t c = slot_counts(sl);
@@ -1249,11 +1253,75 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
             ct[(uint64_t)d * p.n] = tid;
             cs[(uint64_t)d * p.n] = score;
             ++nc;
-            if (p.accumulate)
-                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[tid]), (1ull << 40) | score);
         }
     }
     p.cand_cnt[r] = nc;
+    return nc;
+}
+
+// The count kernel: count_read per lane, then (totals requested) the workgroup's candidates are
+// binned for k_bin_sum as k_bin does, straight from registers: counts per transcript bucket in
+// LDS, one wave scans them (hdr), entries are placed in LDS (reusing the dead count tables) and
+// the region leaves in coalesced 16-B stores.
+template <int NK>
+__global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
+    constexpr int W = NK == 1 ? 1 : 2;
+    constexpr int WORDS = ((TS + 1) * W + PEND + 1) * WG;
+    static_assert(WORDS >= WG * CCAP, "the region staging reuses the count tables");
+    __shared__ __attribute__((aligned(16))) uint32_t s_mem[WORDS];
+    __shared__ uint32_t s_bc[WG + 1];
+    auto s_tab = reinterpret_cast<uint32_t(*)[WG]>(s_mem);
+    auto s_pend = reinterpret_cast<uint32_t(*)[WG]>(s_mem + (TS + 1) * W * WG);
+    const uint32_t t = threadIdx.x, w = blockIdx.x;
+    const uint64_t r = (uint64_t)w * WG + t;
+    const bool bin = p.accumulate && p.bin_nb;  // uniform
+    if (bin) {
+        s_bc[t] = 0;
+        __syncthreads();
+    }
+    uint32_t key[TS];
+    uint32_t nc = 0;
+    if (r < p.n) nc = count_read<NK>(p, r, t, s_tab, s_pend, key);
+    if (!bin) return;
+    const uint32_t bits = p.bin_bits, nb = p.bin_nb, nW = gridDim.x;
+#pragma unroll
+    for (int d = 0; d < TS; ++d)
+        if ((uint32_t)d < nc) atomicAdd(&s_bc[(key[d] & 0x3FFFFFu) >> bits], 1u);
+    __syncthreads();
+    if (t < 64) {  // one wave scans the (<= 256) bucket counts, 4 per lane
+        uint32_t c4[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = 4 * t + u;
+            c4[u] = b < nb ? s_bc[b] : 0u;
+            sum += c4[u];
+        }
+        const uint32_t incl = wave_incl_scan(sum, t);
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = 4 * t + u;
+            if (b < nb) {
+                p.bin_hdr[(uint64_t)b * nW + w] = run;
+                s_bc[b] = run;
+            }
+            run += c4[u];
+        }
+        if (t == 63) p.bin_hdr[(uint64_t)nb * nW + w] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < TS; ++d) {
+        if ((uint32_t)d >= nc) continue;
+        const uint32_t tid = key[d] & 0x3FFFFFu, score = 1023u - (key[d] >> 22);
+        const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
+        s_mem[pos] = (tid & ((1u << bits) - 1u)) | (score << bits);
+    }
+    __syncthreads();
+    const uint32_t total = s_bc[nb - 1];
+    uint4* reg = reinterpret_cast<uint4*>(p.bin_region + (uint64_t)w * (WG * CCAP));
+    const uint4* sr = reinterpret_cast<const uint4*>(s_mem);
+    for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
@@ -1402,7 +1470,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
             const uint32_t score = 0xFFFFFFFFu - (uint32_t)(cand[a] >> 32);
             ct[a * stride] = tid;
             cs[a * stride] = score;
-            if (p.accumulate) {  // not packed: slow-path scores are unbounded
+            if (p.accumulate && p.slow_totals) {  // the count kernel binned the fast reads' totals
                 atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid]), 1ull);
                 atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
             }
@@ -1412,6 +1480,134 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
 }
 
 // per-batch packed totals -> running (reads, score) totals
+// Per-transcript totals without one scattered atomic per candidate (those run at the fabric's
+// random-request rate). Pass 1, one workgroup per 256 reads: the workgroup's candidates are
+// grouped by transcript bucket (2^bits ids) with LDS counters and a scan and written, packed as
+// (tid & (2^bits - 1)) | score << bits, into the workgroup's own region; hdr[b * nW + w] is
+// where bucket b starts in region w (b = nb: the region's total). Candidates that do not pack
+// (overflow lists, huge scores) are added directly. Pass 2, one workgroup per (chunk of
+// regions, bucket): an LDS histogram of the bucket, flushed with one coalesced atomic per
+// non-empty bin into tx_acc ((reads << 40) | score).
+__global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW, uint32_t* hdr,
+                                           uint32_t* region) {
+    __shared__ uint32_t s_cnt[WG + 1], s_fill[WG + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s_reg[WG * CCAP];  // the region, staged
+    const uint32_t t = threadIdx.x, w = blockIdx.x;
+    const uint64_t r = (uint64_t)w * WG + t;
+    if (nb == 0) {  // index too large to bin (> 256 buckets of 2^14): every candidate added directly
+        const uint32_t cnt = r < p.n ? p.cand_cnt[r] : 0u;
+        const bool ext = cnt > (uint32_t)CCAP;
+        const uint32_t* e = ext ? p.cand_ext + 2ull * p.cand_tid[r] : nullptr;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t x = ext ? e[2 * j] : p.cand_tid[(uint64_t)j * p.n + r];
+            const uint32_t y = ext ? e[2 * j + 1] : p.cand_score[(uint64_t)j * p.n + r];
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[x]), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[x]), (unsigned long long)y);
+        }
+        return;
+    }
+    s_cnt[t] = 0;
+    s_fill[t] = 0;
+    if (t == 0) s_cnt[WG] = 0;
+    __syncthreads();
+    uint32_t cnt = r < p.n ? p.cand_cnt[r] : 0u;
+    if (cnt > (uint32_t)CCAP) {  // overflow list (k_chain_slow): added directly
+        const uint32_t* e = p.cand_ext + 2ull * p.cand_tid[r];
+        for (uint32_t j = 0; j < cnt; ++j) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[e[2 * j]]), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[e[2 * j]]), (unsigned long long)e[2 * j + 1]);
+        }
+        cnt = 0;
+    }
+    uint32_t tid[CCAP], sc[CCAP];
+    const uint32_t smax = 1u << (32 - bits);
+    // all CCAP slots are loaded (they exist for every read; stale ones are masked), so the loads
+    // are in flight together
+    const uint64_t rr = r < p.n ? r : 0;
+#pragma unroll
+    for (int j = 0; j < CCAP; ++j) {
+        const uint32_t a = p.cand_tid[(uint64_t)j * p.n + rr], b = p.cand_score[(uint64_t)j * p.n + rr];
+        tid[j] = (uint32_t)j < cnt ? a : 0u;
+        sc[j] = (uint32_t)j < cnt ? b : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < CCAP; ++j) {
+        if ((uint32_t)j >= cnt) continue;
+        if (sc[j] >= smax) {  // does not pack: added directly
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid[j]]), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid[j]]), (unsigned long long)sc[j]);
+            continue;
+        }
+        atomicAdd(&s_cnt[tid[j] >> bits], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {  // one wave scans the (<= 256) bucket counts, 4 per lane
+        uint32_t c4[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = 4 * t + u;
+            c4[u] = b < nb ? s_cnt[b] : 0u;
+            sum += c4[u];
+        }
+        const uint32_t incl = wave_incl_scan(sum, t);
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = 4 * t + u;
+            if (b < nb) {
+                hdr[(uint64_t)b * nW + w] = run;
+                s_fill[b] = run;  // running position per bucket
+            }
+            run += c4[u];
+        }
+        if (t == 63) hdr[(uint64_t)nb * nW + w] = incl;  // the region's total
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CCAP; ++j) {
+        if ((uint32_t)j >= cnt || sc[j] >= smax) continue;
+        const uint32_t b = tid[j] >> bits;
+        const uint32_t pos = atomicAdd(&s_fill[b], 1u);
+        s_reg[pos] = (tid[j] & ((1u << bits) - 1u)) | (sc[j] << bits);
+    }
+    __syncthreads();
+    // the region leaves in 16-B coalesced stores (scattered 4-B stores would each cost a
+    // memory request)
+    const uint32_t total = s_fill[nb - 1];  // end of the last bucket = entries in the region
+    uint4* reg = reinterpret_cast<uint4*>(region + (uint64_t)w * (WG * CCAP));
+    const uint4* sr = reinterpret_cast<const uint4*>(s_reg);
+    for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
+}
+
+__global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nb, uint32_t nW,
+                                               uint32_t chunk, const uint32_t* hdr, const uint32_t* region) {
+    extern __shared__ unsigned long long s_bins[];
+    const uint32_t t = threadIdx.x, b = blockIdx.y;
+    const uint32_t bs = 1u << bits;
+    for (uint32_t i = t; i < bs; i += WG) s_bins[i] = 0;
+    __syncthreads();
+    const uint32_t w0 = blockIdx.x * chunk, w1 = min(nW, w0 + chunk);
+    // one lane per region (the header loads of WG regions are coalesced), 4 entries in flight
+    for (uint32_t w = w0 + t; w < w1; w += WG) {
+        const uint32_t s0 = hdr[(uint64_t)b * nW + w], s1 = hdr[(uint64_t)(b + 1) * nW + w];
+        const uint32_t* reg = region + (uint64_t)w * (WG * CCAP);
+        for (uint32_t q = s0; q < s1; q += 4) {
+            uint32_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = reg[min(q + u, s1 - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (q + u < s1) atomicAdd(&s_bins[x[u] & (bs - 1u)], (1ull << 40) | (unsigned long long)(x[u] >> bits));
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < bs; i += WG) {
+        const unsigned long long a = s_bins[i];
+        const uint32_t tx = b * bs + i;
+        if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
+    }
+}
+
 __global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx) {
     for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < ntx; t += gridDim.x * WG) {
         const uint64_t a = acc[t];
@@ -1425,6 +1621,10 @@ __global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* rea
 
 // ---------------------------------------------------------------------------------------------
 // launchers
+
+static bool use_count3(const ChainParams& p) { return p.ntx <= (1u << 22) && p.variant != 4; }
+
+bool count_bins(const ChainParams& p) { return use_count3(p) && p.nk <= (uint32_t)NK_FAST && p.bin_nb > 0; }
 
 int launch_sketch(const SketchParams& p, void* stream) {
     if (p.n == 0) return 0;
@@ -1452,7 +1652,7 @@ int launch_sketch(const SketchParams& p, void* stream) {
 
 int launch_sketch_slow(const SketchParams& p, void* stream) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_sketch_slow, dim3(512), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_sketch_slow, dim3(2048), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1468,13 +1668,13 @@ int launch_count(const ChainParams& p, void* stream) {
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
     // k_count3 (32-bit sort keys) unless transcript ids need more than 22 bits; variant 4 forces
     // the wide kernel for A/B timing
-    if (p.ntx <= (1u << 22) && p.variant != 4) {
+    if (use_count3(p)) {
         switch (p.nk) {
         case 1: hipLaunchKernelGGL(k_count3<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
         case 2: hipLaunchKernelGGL(k_count3<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
         case 3: hipLaunchKernelGGL(k_count3<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
         case 4: hipLaunchKernelGGL(k_count3<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-        default: break;
+        default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
         }
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
@@ -1483,14 +1683,14 @@ int launch_count(const ChainParams& p, void* stream) {
     case 2: hipLaunchKernelGGL(k_count<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
     case 3: hipLaunchKernelGGL(k_count<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
     case 4: hipLaunchKernelGGL(k_count<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-    default: break;  // > 4 k slots: every read was listed for the slow path by k_probe
+    default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int launch_chain_slow(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_chain_slow, dim3(512), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_chain_slow, dim3(2048), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1503,6 +1703,31 @@ int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals
     if (n == 0) return 0;
     const unsigned grid = (unsigned)std::min<uint64_t>((n + WG - 1) / WG, 4096);
     hipLaunchKernelGGL(k_dir_scatter, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), dir, keys, vals, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_bin(const ChainParams& p, int binned, void* stream) {
+    if (p.n == 0) return 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t nW = (uint32_t)((p.n + WG - 1) / WG);
+    const uint32_t bits = p.bin_bits, nb = p.bin_nb;
+    uint32_t* hdr = p.bin_hdr;
+    const uint32_t* region = p.bin_region;
+    if (nb > (uint32_t)WG) return -1;
+    if (!binned) {
+        hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+        if (hipGetLastError() != hipSuccess) return -2;
+    }
+    if (nb == 0) return 0;
+    // about two workgroups per CU in flight: chunks * nb ~ 512
+    const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nW, 512 / nb));
+    const uint32_t chunk = (nW + chunks - 1) / chunks;
+    const size_t lds = (size_t)8 << bits;
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits, nb,
+                       nW, chunk, hdr, region);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

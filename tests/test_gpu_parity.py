@@ -100,7 +100,7 @@ def tx300():
     return synth.transcriptome(300, seed=21)
 
 
-@pytest.mark.parametrize("ks", [[31], [21, 25, 31], [31, 31], [19]])
+@pytest.mark.parametrize("ks", [[31], [21, 25, 31], [31, 31], [19], [17, 19, 21, 25, 31]])
 @pytest.mark.parametrize("read_len", [100, 150])
 def test_random_reads_match_oracle(tx300, ks, read_len):
     gi, oi = build(ks, tx=tx300)

@@ -60,10 +60,12 @@ for rnd in range(a.rounds + 1):
         k1 = s.kernel_time(0)[0]
         k2 = s.kernel_time(1)[0]
         k3 = s.kernel_time(2)[0]
+        k4 = s.kernel_time(3)[0]
         if rnd:
-            res[name].append((wall, k1, k2, k3))
+            res[name].append((wall, k1, k2, k3, k4))
+print("slow reads (sketch, chain) of the last batch:", s.slow_reads())
 for name, v in res.items():
     v = np.array(v)
     med = np.median(v, axis=0)
-    print("%-10s wall %.3f ms  k_sketch %.3f  k_probe %.3f  k_count %.3f  -> %.2f G reads/s" % (
-        name, med[0], med[1], med[2], med[3], a.reads / med[0] / 1e6))
+    print("%-10s wall %.3f ms  k_sketch %.3f  k_probe %.3f  k_count %.3f  totals %.3f  -> %.2f G reads/s" % (
+        name, med[0], med[1], med[2], med[3], med[4], a.reads / med[0] / 1e6))
