@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
-    ap.add_argument("--cpu-reads", type=int, default=1_000_000, help="CPU-baseline sample size")
+    ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="CPU-baseline sample size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
@@ -114,7 +114,7 @@ def main():
     for _ in range(args.warmup):
         step()
     sess.check(sp)
-    for kind in range(3):
+    for kind in range(4):
         sess.kernel_time(kind)
     sess.enable_timing(True)
     if world > 1:
@@ -129,7 +129,8 @@ def main():
     elapsed = time.perf_counter() - ts
     sess.enable_timing(False)
     sess.check(sp)
-    kt = [sess.kernel_time(kind) for kind in range(3)]  # (total ms, launches): sketch, probe, count
+    # (total ms, launches): sketch, probe, count, totals (k_bin_sum + fold)
+    kt = [sess.kernel_time(kind) for kind in range(4)]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -144,6 +145,8 @@ def main():
     # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"); an index lookup is priced at
     # the 8 B (key, list offset) it needs, a posting at its 4 B tid
     fused = kt[1][1] == 0  # no k_probe launches: the sketch kernel probed (direct/rank table)
+    # the count kernel: k_count3 (32-bit keys, bins the totals) unless ids need > 22 bits
+    count_name = "k_count3" if tx.ntx <= (1 << 22) and os.environ.get("SKQ_VARIANT") != "4" else "k_count"
     b_kern = {
         # read bases in; retained hashes, per-k counts, status out (+ when fused: one lookup per
         # hash, list offsets and the slow flag out)
@@ -151,11 +154,13 @@ def main():
         # status + counts + hashes in, one lookup per hash, list offsets + slow flag out
         "k_probe": 1 + 4 * nk + 4 * h + 8 * h + 4 * h + 1,
         # status + flag + counts + list offsets in, postings, candidates (tid, score) + count out,
-        # one packed 8 B per-transcript total per candidate
-        "k_count": 2 + 4 * nk + 4 * h + 4 * P + 4 + 8 * Cn + 8 * Cn,
+        # and each candidate's 4 B binned (tid, score) for the totals
+        count_name: 2 + 4 * nk + 4 * h + 4 * P + 4 + 8 * Cn + 4 * Cn,
+        # binned candidates in (4 B each), per-transcript sums out (amortised: 16 B x ntx / n)
+        "totals": 4 * Cn + 16.0 * tx.ntx / n,
     }
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
-    avg = {name: ms / cnt for name, (ms, cnt) in zip(("k_sketch", "k_probe", "k_count"), kt) if cnt}
+    avg = {name: ms / cnt for name, (ms, cnt) in zip(("k_sketch", "k_probe", count_name, "totals"), kt) if cnt}
     kname = max(avg, key=avg.get)                       # dominant kernel
     achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
     traffic = None
