@@ -24,6 +24,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sketch-for-rna-seq_amd"))
 import skq  # noqa: E402
+from skq import dist as sdist  # noqa: E402
 from skq import synth  # noqa: E402
 
 METRIC = "reads/sec (quant, 150 bp, k=31) at 1/2/4/8 MI355X; % HBM roofline"
@@ -77,24 +78,29 @@ def main():
     ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
     ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="CPU-baseline sample size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                         "several ranks on one GPU)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.reads:
         cfg["reads"] = args.reads
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    rank, world, local = sdist.world()
+    gpu = local % max(torch.cuda.device_count(), 1)  # one GPU per rank on a full node
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     L, ks, n = cfg["read_len"], cfg["ks"], cfg["reads"]
     t0 = time.time()
     tx = synth.transcriptome(cfg["ntx"], seed=1)  # identical on every rank: replicated index
     tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
-    index = skq.Index(ks, tx.ntx, tables, device=local)
+    index = skq.Index(ks, tx.ntx, tables, device=gpu)
     bases, _, _ = synth.reads(tx, n, L, seed=1000 + rank, err=0.001)  # rank's shard
     d_reads = torch.from_numpy(bases).to(dev)
     sess = skq.Session(index, n, L)
@@ -107,9 +113,9 @@ def main():
 
     def step():
         sess.map(d_reads.data_ptr(), None, n, L, fixed_len=L, stream=sp)
-        if world > 1:
+        if world > 1:  # the one collective: per-transcript totals, summed over ranks (RCCL)
             sess.totals_to_device(totals[0].data_ptr(), totals[1].data_ptr(), stream=sp)
-            dist.all_reduce(totals)
+            sdist.allreduce_totals(totals)
 
     for _ in range(args.warmup):
         step()
@@ -131,10 +137,7 @@ def main():
     sess.check(sp)
     # (total ms, launches): sketch, probe, count, totals (k_bin_sum + fold)
     kt = [sess.kernel_time(kind) for kind in range(4)]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = sdist.max_over_ranks(elapsed, device=dev)  # the slowest rank's time
 
     # per-read workload figures on a 1M-read slice of this rank's batch
     ns = min(n, 1_000_000)
