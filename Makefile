@@ -14,7 +14,8 @@ oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
 .PHONY: oracle
 
 HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o
+LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o \
+            $(OUT)/obj/skq_io.o
 HOST_CXX ?= g++
 HOSTFLAGS := $(CXXFLAGS_COMMON) -pthread
 
@@ -28,10 +29,14 @@ $(OUT)/obj/%.o: $(CSRC)/%.cpp $(CSRC)/skq_internal.h include/skq.h include/skq_h
 $(OUT)/libskq.so: $(LIB_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(LIB_OBJS)
 
+# the command line (index / quant), src/main.cpp's interface
+$(OUT)/skq: $(CSRC)/skq_cli.cpp $(OUT)/libskq.so include/skq.h include/skq_host.h
+	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude $< -o $@ -L$(OUT) -lskq -Wl,-rpath,'$$ORIGIN'
+
 # test driver for the C++ drop-in signatures (tests/test_dropin.py)
 $(OUT)/skq_dropin_check: tests/dropin_check.cpp $(OUT)/libskq.so $(wildcard include/dropin/*.h)
 	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude/dropin $< -o $@ -L$(OUT) -lskq -Wl,-rpath,'$$ORIGIN'
 
-all: lib oracle $(OUT)/skq_dropin_check
+all: lib oracle $(OUT)/skq $(OUT)/skq_dropin_check
 .PHONY: lib all
 .DEFAULT_GOAL := all

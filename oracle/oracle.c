@@ -7,6 +7,7 @@
  */
 #include "oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -410,4 +411,61 @@ uint64_t orc_map_batch_count(const orc_index* ix, const uint8_t* reads, const ui
     free(ctid);
     free(csc);
     return total;
+}
+
+/* ---- EM + assignment (src/isoform_assignment.cpp:9-97) ------------------------------------ */
+int orc_em(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+           const uint32_t* cand_score, uint32_t ntx, int max_iterations, double convergence,
+           double* pi) {
+    double* post = (double*)malloc(sizeof(double) * (ntx ? ntx : 1));
+    int it;
+    for (uint32_t t = 0; t < ntx; ++t) pi[t] = 1.0 / ntx;                      /* :17-20 */
+    for (it = 0; it < max_iterations; ++it) {                                    /* :23 */
+        double total_change = 0.0;
+        for (uint32_t t = 0; t < ntx; ++t) post[t] = 0.0;
+        for (uint64_t r = 0; r < nreads; ++r) {                                  /* :30-50 */
+            double denominator = 0.0;
+            for (uint64_t c = cand_offs[r]; c < cand_offs[r + 1]; ++c)
+                denominator += pi[cand_tid[c]] * (double)cand_score[c];
+            if (denominator > 1e-10) {
+                double inv = 1.0 / denominator;
+                for (uint64_t c = cand_offs[r]; c < cand_offs[r + 1]; ++c)
+                    post[cand_tid[c]] += pi[cand_tid[c]] * (double)cand_score[c] * inv;
+            }
+        }
+        {
+            float pseudocount = 0.01f;                                           /* :53-62 */
+            for (uint32_t t = 0; t < ntx; ++t) {
+                double new_pi = post[t] + pseudocount / (float)nreads + pseudocount;
+                total_change += fabs(new_pi - pi[t]);
+                pi[t] = new_pi;
+            }
+        }
+        if (total_change < convergence) {
+            ++it;
+            break;
+        }
+    }
+    free(post);
+    return it;
+}
+
+void orc_assign(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+                const uint32_t* cand_score, uint32_t ntx, const double* pi, double* counts,
+                uint8_t* assigned) {
+    for (uint32_t t = 0; t < ntx; ++t) {
+        counts[t] = 0.0;
+        assigned[t] = 0;
+    }
+    for (uint64_t r = 0; r < nreads; ++r) {                                      /* :73-94 */
+        double total = 0.0;
+        for (uint64_t c = cand_offs[r]; c < cand_offs[r + 1]; ++c)
+            total += pi[cand_tid[c]] * cand_score[c];
+        for (uint64_t c = cand_offs[r]; c < cand_offs[r + 1]; ++c) {
+            if (total > 0.0) {
+                counts[cand_tid[c]] += (pi[cand_tid[c]] * cand_score[c]) / total;
+                assigned[cand_tid[c]] = 1;
+            }
+        }
+    }
 }

@@ -94,6 +94,19 @@ int orc_map_batch(const orc_index* idx, const uint8_t* reads, const uint64_t* of
 uint64_t orc_map_batch_count(const orc_index* idx, const uint8_t* reads, const uint64_t* offs,
                              uint64_t n, uint32_t threshold, double fraction);
 
+/* EM over the reads' candidate lists (src/isoform_assignment.cpp:9-65): pi starts uniform over
+ * the ntx transcripts; E-step per read in order, posterior = pi*score * (1/denominator) when the
+ * denominator exceeds 1e-10; M-step pi = (posterior_sum + 0.01f/R) + 0.01f (float pseudocount,
+ * R = reads including those without candidates); stop after max_iterations or when the summed
+ * absolute change drops below convergence. Returns the iterations run. */
+int orc_em(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+           const uint32_t* cand_score, uint32_t ntx, int max_iterations, double convergence,
+           double* pi);
+/* assign_reads_to_isoforms (src/isoform_assignment.cpp:67-97) */
+void orc_assign(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+                const uint32_t* cand_score, uint32_t ntx, const double* pi, double* counts,
+                uint8_t* assigned);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,226 @@
+// skq — the reference's command line (src/main.cpp:24-276) on the MI355X path:
+//   skq [-h] [-k K1,K2,...] [-o index|quant] <args>
+//   -o index <reference.fasta> <index_output>
+//   -o quant <index_file> <reads.fastq> <output.csv>     (the default mode)
+// index: FASTA -> per-transcript FracMinHash sketches -> inverted index -> the legacy file.
+// quant: legacy file -> device index; FASTQ streamed in batches through skq_map (sketch +
+//        sparse chain on the GPU); the last valid record of every read id kept; EM (20 rounds,
+//        0.01) -> assignment -> CSV. As in the reference, quant uses the index's k list.
+#include <getopt.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "skq.h"
+#include "skq_host.h"
+
+namespace {
+
+void check(int rc, const char* what) {
+    if (rc != 0) throw std::runtime_error(std::string(what) + ": " + skq_last_error());
+}
+
+void print_help(const std::string& prog) {
+    std::cout << "Usage: " << prog << " [OPTIONS] <mode> [arguments]\n"
+              << "Modes:\n"
+              << "  index   Build index from reference genome\n"
+              << "  quant   Quantify using pre-built index and reads\n\n"
+              << "Options:\n"
+              << "  -h, --help              Show this help message and exit\n"
+              << "  -k, --kmer-length SIZE  Comma separated list of k-mer lengths (default: 31)\n"
+              << "  -o, --mode MODE         Mode: index or quant (default: quant)\n\n"
+              << "Index mode usage:\n"
+              << "  " << prog << " -o index <reference_genome.fasta> <index_output>\n\n"
+              << "Quant mode usage:\n"
+              << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
+              << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_BATCH (reads per batch).\n";
+}
+
+const float kSketchSize = 0.05f;  // src/main.cpp:43
+
+int device() {
+    const char* e = std::getenv("SKQ_DEVICE");
+    return e ? std::atoi(e) : 0;
+}
+
+void build_and_save_index(const std::string& fasta, const std::string& out, const std::vector<uint32_t>& ks) {
+    const auto t0 = std::chrono::steady_clock::now();
+    skq_seqs* tx = nullptr;
+    check(skq_fasta_load(fasta.c_str(), &tx), "load_fasta");
+    const uint8_t* bytes = nullptr;
+    const uint64_t* offs = nullptr;
+    check(skq_seqs_view(tx, &bytes, &offs, nullptr, nullptr), "sequences");
+    skq_tables* tabs = nullptr;
+    check(skq_tables_build((uint32_t)skq_seqs_count(tx), bytes, offs, (uint32_t)ks.size(), ks.data(),
+                           skq_threshold((double)kSketchSize), 0, &tabs),
+          "index build");
+    const std::chrono::duration<double> dt = std::chrono::steady_clock::now() - t0;
+    std::cout << "Index built in " << dt.count() << " seconds." << std::endl;
+    check(skq_legacy_index_write(out.c_str(), (uint32_t)ks.size(), ks.data(), tx, tabs), "save_index");
+    std::cout << "Index saved to " << out << std::endl;
+    skq_tables_free(tabs);
+    skq_seqs_free(tx);
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (p) skq_free(p);
+    }
+    void put(const void* src, size_t n) {
+        if (n > cap) {
+            if (p) skq_free(p);
+            p = nullptr;
+            cap = 0;
+            check(skq_malloc(device(), std::max<size_t>(n, 16), &p), "device allocation");
+            cap = std::max<size_t>(n, 16);
+        }
+        if (n) check(skq_memcpy_h2d(p, src, n, nullptr), "upload");
+    }
+};
+
+void quantification(const std::string& index_path, const std::string& reads_path, const std::string& out_path) {
+    skq_legacy_index* lx = nullptr;
+    check(skq_legacy_index_read(index_path.c_str(), &lx), "load_index");
+    std::cout << "Index loaded from " << index_path << std::endl;
+    std::cout << "Loading index completed" << std::endl;
+    uint32_t nk = 0;
+    const uint32_t* ks = nullptr;
+    const skq_seqs* tx = nullptr;
+    const skq_tables* tabs = nullptr;
+    check(skq_legacy_index_view(lx, &nk, &ks, &tx, &tabs), "index view");
+    if (nk == 0) throw std::runtime_error("the index holds no k-mer lengths");
+    const uint32_t ntx = (uint32_t)skq_seqs_count(tx);
+    skq_index* ix = nullptr;
+    check(skq_index_from_tables(device(), ntx, nk, ks, tabs, &ix), "device index");
+
+    uint64_t batch = 1u << 22;
+    if (const char* e = std::getenv("SKQ_BATCH")) batch = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    skq_session* s = nullptr;
+    check(skq_session_create(ix, batch, 256, &s), "session");
+    skq_fastq* q = nullptr;
+    check(skq_fastq_open(reads_path.c_str(), &q), "FASTQ");
+
+    // per record: status and candidates, kept until duplicates are resolved
+    std::vector<uint8_t> status;
+    std::vector<uint64_t> rec_offs{0};
+    std::vector<uint32_t> ctid, cscore;
+    DevBuf d_bytes, d_offs;
+    const uint32_t thr = skq_threshold((double)kSketchSize);
+    for (;;) {
+        uint64_t n = 0, first = 0;
+        const uint8_t* bytes = nullptr;
+        const uint64_t* offs = nullptr;
+        check(skq_fastq_next(q, batch, &n, &bytes, &offs, &first), "FASTQ read");
+        if (n == 0) break;
+        uint64_t maxlen = 0;
+        for (uint64_t r = 0; r < n; ++r) maxlen = std::max(maxlen, offs[r + 1] - offs[r]);
+        d_bytes.put(bytes, offs[n]);
+        d_offs.put(offs, (n + 1) * 8);
+        check(skq_map(s, static_cast<const uint8_t*>(d_bytes.p), static_cast<const uint64_t*>(d_offs.p), 0, n,
+                      (uint32_t)std::min<uint64_t>(maxlen, 0xFFFFFFFFu), thr, 0.9, 0, nullptr),
+              "sketch + sparse chain");
+        uint64_t nh = 0, nc = 0;
+        check(skq_session_export(s, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &nh, &nc), "export");
+        const size_t s0 = status.size(), c0 = ctid.size();
+        status.resize(s0 + n);
+        ctid.resize(c0 + nc);
+        cscore.resize(c0 + nc);
+        std::vector<uint64_t> co(n + 1);
+        check(skq_session_export(s, status.data() + s0, nullptr, nullptr, co.data(), ctid.data() + c0,
+                                 cscore.data() + c0, &nh, &nc),
+              "export");
+        for (uint64_t r = 0; r < n; ++r) rec_offs.push_back(c0 + co[r + 1]);
+        check(skq_fastq_mark(q, first, n, status.data() + s0), "FASTQ mark");
+    }
+    std::cout << "Loading read completed" << std::endl;
+    std::cout << "Sparse chaining completed" << std::endl;
+
+    // reads that reach sparse_chain: status OK, and the last such record of their id
+    std::vector<uint64_t> offs{0};
+    std::vector<uint32_t> t2, s2;
+    const uint64_t nrec = status.size();
+    for (uint64_t r = 0; r < nrec; ++r) {
+        if ((status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK || !skq_fastq_kept(q, r)) continue;
+        t2.insert(t2.end(), ctid.begin() + (ptrdiff_t)rec_offs[r], ctid.begin() + (ptrdiff_t)rec_offs[r + 1]);
+        s2.insert(s2.end(), cscore.begin() + (ptrdiff_t)rec_offs[r], cscore.begin() + (ptrdiff_t)rec_offs[r + 1]);
+        offs.push_back(t2.size());
+    }
+    const uint64_t R = offs.size() - 1;
+    std::vector<double> pi(ntx), counts(ntx);
+    std::vector<uint8_t> assigned(ntx);
+    int iters = 0;
+    check(skq_em(R, offs.data(), t2.data(), s2.data(), ntx, 20, 0.01, 0, pi.data(), &iters), "EM");
+    std::cout << "EM estimation completed" << std::endl;
+    check(skq_assign(R, offs.data(), t2.data(), s2.data(), ntx, pi.data(), counts.data(), assigned.data()), "assign");
+    std::cout << "Read assignment completed" << std::endl;
+    check(skq_csv_write(out_path.c_str(), tx, counts.data(), assigned.data(), pi.data()), "output_to_csv");
+    std::cout << "Output written to " << out_path << std::endl;
+    skq_fastq_close(q);
+    skq_session_free(s);
+    skq_index_free(ix);
+    skq_legacy_index_free(lx);
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    std::string mode = "quant";
+    std::vector<uint32_t> ks = {31};
+    static struct option long_options[] = {{"help", no_argument, 0, 'h'},
+                                           {"kmer-length", required_argument, 0, 'k'},
+                                           {"mode", required_argument, 0, 'o'},
+                                           {0, 0, 0, 0}};
+    int opt, option_index = 0;
+    while ((opt = getopt_long(argc, argv, "hk:o:", long_options, &option_index)) != -1) {
+        switch (opt) {
+        case 'h':
+            print_help(argv[0]);
+            return 0;
+        case 'k': {
+            ks.clear();
+            std::istringstream iss(optarg);
+            std::string tok;
+            while (std::getline(iss, tok, ','))
+                if (!tok.empty()) ks.push_back((uint32_t)std::stoul(tok));
+            break;
+        }
+        case 'o':
+            mode = optarg;
+            break;
+        default:
+            print_help(argv[0]);
+            return 1;
+        }
+    }
+    try {
+        if (mode == "index") {
+            if (optind + 2 > argc) {
+                std::cerr << "Usage: " << argv[0] << " index <reference_genome.fasta> <index_output>" << std::endl;
+                return 1;
+            }
+            build_and_save_index(argv[optind], argv[optind + 1], ks);
+        } else if (mode == "quant") {
+            if (optind + 3 > argc) {
+                std::cerr << "Usage: " << argv[0] << " quant <index_file> <reads.fastq> <output>" << std::endl;
+                return 1;
+            }
+            quantification(argv[optind], argv[optind + 1], argv[optind + 2]);
+        } else {
+            std::cerr << "Invalid mode. Please choose 'index' or 'quant'." << std::endl;
+            return 1;
+        }
+    } catch (const std::exception& e) {
+        std::cerr << "skq: " << e.what() << std::endl;
+        return 1;
+    }
+    return 0;
+}

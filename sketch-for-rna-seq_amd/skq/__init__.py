@@ -78,6 +78,24 @@ def lib():
             "skq_tables_get": (i32, [vp, u32, C.POINTER(_KmerTable)]),
             "skq_tables_free": (i32, [vp]),
             "skq_host_sketch": (C.c_int64, [vp, u64, u32, u32, vp]),
+            "skq_fasta_load": (i32, [C.c_char_p, C.POINTER(vp)]),
+            "skq_seqs_count": (u64, [vp]),
+            "skq_seqs_view": (i32, [vp] + [C.POINTER(vp)] * 4),
+            "skq_seqs_free": (i32, [vp]),
+            "skq_fastq_open": (i32, [C.c_char_p, C.POINTER(vp)]),
+            "skq_fastq_next": (i32, [vp, u64, C.POINTER(u64), C.POINTER(vp), C.POINTER(vp), C.POINTER(u64)]),
+            "skq_fastq_mark": (i32, [vp, u64, u64, vp]),
+            "skq_fastq_kept": (i32, [vp, u64]),
+            "skq_fastq_records": (u64, [vp]),
+            "skq_fastq_id": (i32, [vp, u64, C.POINTER(vp), C.POINTER(u64)]),
+            "skq_fastq_close": (i32, [vp]),
+            "skq_legacy_index_write": (i32, [C.c_char_p, u32, vp, vp, vp]),
+            "skq_legacy_index_read": (i32, [C.c_char_p, C.POINTER(vp)]),
+            "skq_legacy_index_view": (i32, [vp, C.POINTER(u32), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]),
+            "skq_legacy_index_free": (i32, [vp]),
+            "skq_em": (i32, [u64, vp, vp, vp, u32, i32, dbl, i32, vp, C.POINTER(i32)]),
+            "skq_assign": (i32, [u64, vp, vp, vp, u32, vp, vp, vp]),
+            "skq_csv_write": (i32, [C.c_char_p, vp, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -283,24 +301,124 @@ def build_tables(seqs, offs, ks, thr=None, nthreads=0):
     h = C.c_void_p()
     _check(lib().skq_tables_build(len(offs) - 1, _p(seqs), _p(offs), len(ka), _p(ka), thr, nthreads,
                                   C.byref(h)))
-    out = {}
     try:
-        for i in range(lib().skq_tables_count(h)):
-            t = _KmerTable()
-            _check(lib().skq_tables_get(h, i, C.byref(t)))
-            n = t.nkeys
-
-            def arr(ptr, ctype, count, dtype):
-                if count == 0:
-                    return np.zeros(0, dtype)
-                return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), (count,)).astype(dtype, copy=True)
-
-            offs_a = arr(t.offs, C.c_uint64, n + 1, np.uint64)
-            out[int(t.k)] = (arr(t.keys, C.c_uint32, n, np.uint32), offs_a,
-                             arr(t.tids, C.c_uint32, int(offs_a[-1]), np.uint32))
+        return _tables_dict(h)
     finally:
         lib().skq_tables_free(h)
+
+
+def _arr(ptr, ctype, count, dtype):
+    if count == 0:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), (count,)).astype(dtype, copy=True)
+
+
+def _tables_dict(h):
+    out = {}
+    for i in range(lib().skq_tables_count(h)):
+        t = _KmerTable()
+        _check(lib().skq_tables_get(h, i, C.byref(t)))
+        n = t.nkeys
+        offs_a = _arr(t.offs, C.c_uint64, n + 1, np.uint64)
+        out[int(t.k)] = (_arr(t.keys, C.c_uint32, n, np.uint32), offs_a,
+                         _arr(t.tids, C.c_uint32, int(offs_a[-1]), np.uint32))
     return out
+
+
+def _seqs(h):
+    """(names, sequences) of a skq_seqs handle, as lists of bytes."""
+    n = lib().skq_seqs_count(h)
+    sb, so, nb, no = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+    _check(lib().skq_seqs_view(h, C.byref(sb), C.byref(so), C.byref(nb), C.byref(no)))
+    so_a = _arr(so, C.c_uint64, n + 1, np.uint64)
+    no_a = _arr(no, C.c_uint64, n + 1, np.uint64)
+    seq_b = C.string_at(sb, int(so_a[-1])) if so_a[-1] else b""
+    name_b = C.string_at(nb, int(no_a[-1])) if no_a[-1] else b""
+    return ([name_b[no_a[i]:no_a[i + 1]] for i in range(n)], [seq_b[so_a[i]:so_a[i + 1]] for i in range(n)])
+
+
+def fasta_load(path):
+    """load_fasta (src/data_io.cpp:47-80): (names, sequences) in file order."""
+    h = C.c_void_p()
+    _check(lib().skq_fasta_load(str(path).encode(), C.byref(h)))
+    try:
+        return _seqs(h)
+    finally:
+        lib().skq_seqs_free(h)
+
+
+def legacy_index_read(path):
+    """load_index (src/data_io.cpp:233-304): (ks, names, sequences, {k: (keys, offs, tids)})."""
+    h = C.c_void_p()
+    _check(lib().skq_legacy_index_read(str(path).encode(), C.byref(h)))
+    try:
+        nk, ks, tx, tabs = C.c_uint32(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(lib().skq_legacy_index_view(h, C.byref(nk), C.byref(ks), C.byref(tx), C.byref(tabs)))
+        names, seqs = _seqs(tx)
+        return ([int(x) for x in _arr(ks, C.c_uint32, nk.value, np.uint32)], names, seqs, _tables_dict(tabs))
+    finally:
+        lib().skq_legacy_index_free(h)
+
+
+class FastqReader:
+    """process_fastq_single_pass's record reader (src/main.cpp:113-148), in batches."""
+
+    def __init__(self, path):
+        self.h = C.c_void_p()
+        _check(lib().skq_fastq_open(str(path).encode(), C.byref(self.h)))
+
+    def next(self, max_reads):
+        """(first ordinal, [sequence bytes]) of the next batch ([] at the end)."""
+        n, b, o, first = C.c_uint64(), C.c_void_p(), C.c_void_p(), C.c_uint64()
+        _check(lib().skq_fastq_next(self.h, max_reads, C.byref(n), C.byref(b), C.byref(o), C.byref(first)))
+        offs = _arr(o, C.c_uint64, n.value + 1, np.uint64) if n.value else np.zeros(1, np.uint64)
+        data = C.string_at(b, int(offs[-1])) if offs[-1] else b""
+        return first.value, [data[offs[i]:offs[i + 1]] for i in range(n.value)]
+
+    def mark(self, first, status):
+        st = np.ascontiguousarray(status, np.uint8)
+        _check(lib().skq_fastq_mark(self.h, first, len(st), _p(st)))
+
+    def kept(self, ordinal):
+        return bool(lib().skq_fastq_kept(self.h, ordinal))
+
+    def id(self, ordinal):
+        p, n = C.c_void_p(), C.c_uint64()
+        _check(lib().skq_fastq_id(self.h, ordinal, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value)
+
+    def close(self):
+        if self.h:
+            lib().skq_fastq_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+
+def _csr(cand_offs, cand_tid, cand_score):
+    return (np.ascontiguousarray(cand_offs, np.uint64), np.ascontiguousarray(cand_tid, np.uint32),
+            np.ascontiguousarray(cand_score, np.uint32))
+
+
+def em(cand_offs, cand_tid, cand_score, ntx, max_iterations=20, convergence=0.01, nthreads=0):
+    """estimate_isoform_abundance_em (src/isoform_assignment.cpp:9-65): (pi, iterations)."""
+    o, t, s = _csr(cand_offs, cand_tid, cand_score)
+    pi = np.zeros(max(ntx, 1), np.float64)
+    it = C.c_int()
+    _check(lib().skq_em(len(o) - 1, _p(o), _p(t), _p(s), ntx, max_iterations, convergence, nthreads, _p(pi),
+                        C.byref(it)))
+    return pi[:ntx], it.value
+
+
+def assign(cand_offs, cand_tid, cand_score, ntx, pi):
+    """assign_reads_to_isoforms (src/isoform_assignment.cpp:67-97): (counts, assigned)."""
+    o, t, s = _csr(cand_offs, cand_tid, cand_score)
+    pi = np.ascontiguousarray(pi, np.float64)
+    counts = np.zeros(max(ntx, 1), np.float64)
+    assigned = np.zeros(max(ntx, 1), np.uint8)
+    _check(lib().skq_assign(len(o) - 1, _p(o), _p(t), _p(s), ntx, _p(pi), _p(counts), _p(assigned)))
+    return counts[:ntx], assigned[:ntx].astype(bool)
 
 
 def host_sketch(seq: bytes, k: int, thr=None):

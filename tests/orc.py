@@ -53,6 +53,12 @@ def lib():
                                     C.c_double] + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 3 + [C.c_uint32]
         L.orc_map_batch_count.restype = C.c_uint64
         L.orc_map_batch_count.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_double]
+        L.orc_em.restype = C.c_int
+        L.orc_em.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.c_double,
+                             C.c_void_p]
+        L.orc_assign.restype = None
+        L.orc_assign.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                 C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -160,3 +166,24 @@ class Index:
         return dict(status=st[:n], hash_cnt=hc[:n * nk].reshape(n, nk),
                     hashes=hs[:n * nk * hcap].reshape(n, nk, hcap), cand_cnt=cc[:n],
                     cand_tid=ct[:n * ccap].reshape(n, ccap), cand_score=cs[:n * ccap].reshape(n, ccap))
+
+
+def em(cand_offs, cand_tid, cand_score, ntx, max_iterations=20, convergence=0.01):
+    """Oracle EM (src/isoform_assignment.cpp:9-65): (pi, iterations)."""
+    o = np.ascontiguousarray(cand_offs, np.uint64)
+    t = np.ascontiguousarray(cand_tid, np.uint32)
+    s = np.ascontiguousarray(cand_score, np.uint32)
+    pi = np.zeros(max(ntx, 1), np.float64)
+    it = lib().orc_em(len(o) - 1, ptr(o), ptr(t), ptr(s), ntx, max_iterations, convergence, ptr(pi))
+    return pi[:ntx], it
+
+
+def assign(cand_offs, cand_tid, cand_score, ntx, pi):
+    o = np.ascontiguousarray(cand_offs, np.uint64)
+    t = np.ascontiguousarray(cand_tid, np.uint32)
+    s = np.ascontiguousarray(cand_score, np.uint32)
+    pi = np.ascontiguousarray(pi, np.float64)
+    counts = np.zeros(max(ntx, 1), np.float64)
+    assigned = np.zeros(max(ntx, 1), np.uint8)
+    lib().orc_assign(len(o) - 1, ptr(o), ptr(t), ptr(s), ntx, ptr(pi), ptr(counts), ptr(assigned))
+    return counts[:ntx], assigned[:ntx].astype(bool)
