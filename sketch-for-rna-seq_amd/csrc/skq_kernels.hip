@@ -1059,6 +1059,10 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
         p.cand_cnt[r] = 0;
         return 0;
     }
+    if (p.variant == 1 || p.variant == 2) {  // sketch-side timing variants: lofs hold no offsets
+        p.cand_cnt[r] = 0;
+        return 0;
+    }
     if (pf) {
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
