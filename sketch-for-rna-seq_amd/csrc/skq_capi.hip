@@ -557,7 +557,7 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     p.maxk = ix->maxk;
     for (uint32_t i = 0; i < ix->nk; ++i) p.ks[i] = ix->ks[i];
     p.threshold = threshold;
-    p.tile_chunks = (skq::WG * Lc + 31) / 16 + 1;
+    p.tile_chunks = (64 * Lc + 31) / 16 + 1;  // per wave
     p.hcap = hcap;
     p.ovf_cap = s->ovf_cap;
     p.rolltab = ix->d_rolltab;
@@ -699,8 +699,11 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
     s->probed = false;
     s->x_hashes = d_hashes;
     s->x_offs = d_hash_offs;
-    // hash_cnt is read through p.hash_cnt; keep the session's status out of it (all sketched)
-    return chain_impl(s, n_reads, nullptr, d_hash_cnt, d_hashes, d_hash_offs, d_present, 0, fraction,
+    // every external sketch counts as sketched: the session's status array, set to SKQ_READ_OK,
+    // stands in (the count kernels read a status for every read)
+    if (n_reads)
+        HIP_TRY(hipMemsetAsync(s->status, SKQ_READ_OK, n_reads, reinterpret_cast<hipStream_t>(stream)));
+    return chain_impl(s, n_reads, s->status, d_hash_cnt, d_hashes, d_hash_offs, d_present, 0, fraction,
                       accumulate, false, stream);
 }
 

@@ -67,7 +67,7 @@ struct SketchParams {
     uint32_t maxk;
     uint32_t ks[SKQ_MAX_K];
     uint32_t threshold;
-    uint32_t tile_chunks;  // 16-byte chunks staged per workgroup
+    uint32_t tile_chunks;  // 16-byte chunks staged per wave (64 reads)
     uint32_t hcap;
     uint32_t ovf_cap;
     const uint64_t* rolltab;  // [nk][16] 33-bit seed(in) ^ rot^k(seed(out)) by (in*4 + out), then 4 seeds
@@ -163,7 +163,7 @@ int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals
 SKQ_HD inline uint32_t home_bucket(uint32_t key, uint32_t nbuckets) {
     return (uint32_t)(((uint64_t)(uint32_t)(key * HASH_MUL) * nbuckets) >> 32);
 }
-size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap);
+size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap, bool nthash);
 
 // 33-bit ntHash lane (bits 0..32 of ntHash's split rotate evolve on their own)
 constexpr uint64_t M33 = (1ull << 33) - 1;

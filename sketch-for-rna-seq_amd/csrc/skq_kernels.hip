@@ -187,14 +187,22 @@ __device__ __forceinline__ void roll33(uint32_t& lo, uint32_t& hi, uint64_t e) {
 // K1: sketch
 
 // LDS layout: [tables: nk * 16 u64 (seed(in) ^ rot^k(seed(out))), 4 u64 seeds]
-//             [codes: tile_chunks + 1 u32] [bad: tile_chunks u16, padded to 16 B]
-//             [raw retained: HCAP x WG u32]
+//             per wave: [codes: wave_chunks + 1 u32, padded to 16 B]
+//             per wave: [bad: wave_chunks u16, padded to 16 B]
+//             [raw retained: (HCAP + 1) x WG u32]
+// Each wave stages the bytes of its own 64 reads and synchronises only with itself, so a wave
+// waiting for its loads never holds up the other waves of the workgroup.
 __host__ __device__ inline size_t sketch_tab_bytes(uint32_t nk) { return ((size_t)nk * 16 + 4) * 8; }
+// (codes: wc chunks + the zero word at nch + a sink word; bad: ntHash mode one u16 mask per
+// chunk + a sink, quant mode one "any bad byte" bit per chunk)
+__host__ __device__ inline size_t sketch_codes_bytes(uint32_t wc) { return (((size_t)wc + 2) * 4 + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t sketch_bad_bytes(uint32_t wc, bool nthash) {
+    return nthash ? ((((size_t)wc + 1) * 2 + 15) & ~(size_t)15) : (((size_t)wc + 127) / 128) * 16;
+}
 
-size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap) {
+size_t sketch_lds_bytes(uint32_t nk, uint32_t wave_chunks, uint32_t hcap, bool nthash) {
     size_t b = sketch_tab_bytes(nk);
-    b += (((size_t)tile_chunks + 1) * 4 + 15) & ~(size_t)15;
-    b += ((size_t)tile_chunks * 2 + 15) & ~(size_t)15;
+    b += (WG / 64) * (sketch_codes_bytes(wave_chunks) + sketch_bad_bytes(wave_chunks, nthash));
     b += ((size_t)hcap + 1) * WG * 4;  // + one spare slot per lane for windows not retained
     return b;
 }
@@ -202,20 +210,29 @@ size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap) {
 template <int HCAP, bool NTH>
 __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    const uint32_t wc = p.tile_chunks;  // chunks per wave
     // roll terms as {bits 0..31, bit 32 moved to bit 31}
     uint2* s_tab = reinterpret_cast<uint2*>(smem);
     const uint2* s_seed = s_tab + p.nk * 16;
-    uint32_t* s_codes = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(p.nk));
-    uint16_t* s_bad = reinterpret_cast<uint16_t*>(
-        reinterpret_cast<unsigned char*>(s_codes) + ((((size_t)p.tile_chunks + 1) * 4 + 15) & ~(size_t)15));
-    uint32_t* s_raw = reinterpret_cast<uint32_t*>(
-        reinterpret_cast<unsigned char*>(s_bad) + ((((size_t)p.tile_chunks * 2) + 15) & ~(size_t)15));
+    unsigned char* s_wave = smem + sketch_tab_bytes(p.nk) + wv * (sketch_codes_bytes(wc) + sketch_bad_bytes(wc, NTH));
+    uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
+    uint16_t* s_bad = reinterpret_cast<uint16_t*>(s_wave + sketch_codes_bytes(wc));   // ntHash mode
+    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_wave + sketch_codes_bytes(wc));  // quant mode
+    uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(p.nk) +
+                                                  (WG / 64) * (sketch_codes_bytes(wc) + sketch_bad_bytes(wc, NTH)));
+    for (uint32_t e = tid; e < p.nk * 16 + 4; e += WG) {
+        const uint64_t v = p.rolltab[e];
+        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
+    }
+    __syncthreads();  // the only workgroup barrier: before any read bytes are loaded
 
-    const int tid = threadIdx.x;
-    const uint64_t r0 = (uint64_t)blockIdx.x * WG;
-    const uint32_t nr = (uint32_t)min((uint64_t)WG, p.n - r0);
+    const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
+    if (r0 >= p.n) return;
+    const uint32_t nr = (uint32_t)min((uint64_t)64, p.n - r0);
 
-    // workgroup byte span, in 16-byte chunks of the aligned-down base pointer (a 16-B aligned
+    // the wave's byte span, in 16-byte chunks of the aligned-down base pointer (a 16-B aligned
     // chunk holding at least one byte of the buffer never crosses a page)
     const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
     const uintptr_t abase = base & ~(uintptr_t)15;
@@ -225,71 +242,95 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     read_extent(p.offs, p.fixed_len, r0 + nr - 1, sl, ll);
     const uint64_t c0 = (s0 + delta) >> 4;
     const uint64_t c1 = (sl + ll + delta + 15) >> 4;
-    const uint32_t nch = (uint32_t)min((uint64_t)p.tile_chunks, c1 - c0);
+    const uint32_t nch = (uint32_t)min((uint64_t)wc, c1 - c0);
 
     // staging: SU loads per lane in flight before any is used (a load inside a guarded loop body
     // would be waited for before the next one issues); indices past the span are clamped to
     // its last chunk, which is valid memory
     const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
-    constexpr uint32_t SU = 8;
-    for (uint32_t cb = tid; cb < nch; cb += SU * WG) {
+    constexpr uint32_t SU = 10;
+    for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
         uint4 vv[SU];
 #pragma unroll
-        for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * WG, nch - 1)];
+        for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * 64, nch - 1)];
 #pragma unroll
         for (uint32_t u = 0; u < SU; ++u) {
-        // encoded unconditionally (only the LDS stores are guarded), so no load can be sunk
-        // behind a branch and waited for on its own
-        const uint32_t c = cb + u * WG;
+        const uint32_t c = cb + u * 64;
         const uint4 v = vv[u];
-        uint32_t a, b, cc, d, ba, bb, bc, bd;
-        encode4(v.x, a, ba);
-        encode4(v.y, b, bb);
-        encode4(v.z, cc, bc);
-        encode4(v.w, d, bd);
+        // unconditional stores (chunks past the span go to the sink slot): a guarded store
+        // would let the compiler sink the load into the guard and wait for it there
+        const uint32_t cs = c < nch ? c : wc + 1;
         if (NTH) {
+            uint32_t a, b, cc, d, ba, bb, bc, bd;
+            encode4(v.x, a, ba);
+            encode4(v.y, b, bb);
+            encode4(v.z, cc, bc);
+            encode4(v.w, d, bd);
             ba = ntbad4(v.x);
             bb = ntbad4(v.y);
             bc = ntbad4(v.z);
             bd = ntbad4(v.w);
-        }
-        if (c < nch) {
-            s_codes[c] = a | (b << 8) | (cc << 16) | (d << 24);
-            s_bad[c] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
+            s_codes[cs] = a | (b << 8) | (cc << 16) | (d << 24);
+            s_bad[c < nch ? c : wc] = (uint16_t)(ba | (bb << 4) | (bc << 8) | (bd << 12));
+        } else {
+            // quant mode: 2-bit codes ((byte >> 1) & 3) packed by one dot product per word,
+            // and one "any byte that is not uppercase A/C/G/T" bit per chunk (XOR with the
+            // letter each code stands for), gathered per 64 chunks by a wave ballot
+            const uint32_t ta = (v.x >> 1) & 0x03030303u, tb = (v.y >> 1) & 0x03030303u;
+            const uint32_t tc = (v.z >> 1) & 0x03030303u, td = (v.w >> 1) & 0x03030303u;
+            constexpr uint32_t W4 = 0x40100401u;  // byte weights 1, 4, 16, 64
+            const uint32_t code = __builtin_amdgcn_udot4(ta, W4, 0u, false) |
+                                  (__builtin_amdgcn_udot4(tb, W4, 0u, false) << 8) |
+                                  (__builtin_amdgcn_udot4(tc, W4, 0u, false) << 16) |
+                                  (__builtin_amdgcn_udot4(td, W4, 0u, false) << 24);
+            constexpr uint32_t GTCA = 0x47544341u;  // 'A' 'C' 'T' 'G' by code
+            const uint32_t x = (__builtin_amdgcn_perm(0u, GTCA, ta) ^ v.x) | (__builtin_amdgcn_perm(0u, GTCA, tb) ^ v.y) |
+                               (__builtin_amdgcn_perm(0u, GTCA, tc) ^ v.z) | (__builtin_amdgcn_perm(0u, GTCA, td) ^ v.w);
+            s_codes[cs] = code;
+            const uint64_t wbits = __ballot(x != 0);  // lanes hold one 64-aligned group of chunks
+            if (lane == 0 && c < nch) s_badw[c >> 6] = wbits;
         }
         }
     }
-    if (tid == 0) s_codes[nch] = 0;
-    for (uint32_t e = tid; e < p.nk * 16 + 4; e += WG) {
-        const uint64_t v = p.rolltab[e];
-        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
-    }
-    __syncthreads();
+    if (lane == 0) s_codes[nch] = 0;
+    // wave-level hand-off: LDS operations of one wave complete in order; the fences keep the
+    // compiler from moving the reads below above the stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    if ((uint32_t)tid >= nr) return;
-    const uint64_t r = r0 + tid;
+    if (lane >= nr) return;
+    const uint64_t r = r0 + lane;
     uint64_t start, len;
     read_extent(p.offs, p.fixed_len, r, start, len);
     const uint64_t q0 = start + delta - c0 * 16;  // tile position of this read's first base
 
     bool slow = len > (uint64_t)LFAST || q0 + len > (uint64_t)nch * 16;
     uint8_t st = SKQ_READ_OK;
-    if (!slow) {
-        // is_valid_sequence (src/data_io.cpp:17-34): every byte uppercase A/C/G/T
+    if (!slow && !NTH) {
+        // is_valid_sequence (src/data_io.cpp:17-34): every byte uppercase A/C/G/T. A read whose
+        // chunks are all clean is valid; one touching a flagged chunk (the bad byte may belong
+        // to a neighbour) checks its own bytes. (ntHash mode: invalid bases only skip windows.)
         bool bad = false;
         if (len) {
-            const uint64_t last = q0 + len - 1;
-            for (uint64_t c = q0 >> 4; c <= (last >> 4); ++c) {
-                uint32_t m = s_bad[c];
-                const uint32_t lo = (c == (q0 >> 4)) ? (uint32_t)(q0 & 15) : 0u;
-                const uint32_t hi = (c == (last >> 4)) ? (uint32_t)(last & 15) : 15u;
-                m &= ((2u << hi) - 1u) & ~((1u << lo) - 1u);
+            const uint32_t ca = (uint32_t)(q0 >> 4), cz = (uint32_t)((q0 + len - 1) >> 4);
+            for (uint32_t wd = ca >> 6; wd <= (cz >> 6); ++wd) {
+                uint64_t m = s_badw[wd];
+                const uint32_t lo = wd == (ca >> 6) ? (ca & 63) : 0u, hi = wd == (cz >> 6) ? (cz & 63) : 63u;
+                m &= (hi == 63 ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
                 bad |= m != 0;
             }
+            if (bad) {
+                bad = false;
+                const uint8_t* rb = p.reads + start;
+                for (uint64_t q = 0; q < len; ++q) {
+                    const uint8_t ch = rb[q];
+                    bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+                }
+            }
         }
-        if (NTH) bad = false;  // ntHash mode: invalid bases only skip windows
         if (bad) st = SKQ_READ_INVALID;
-        else if (!NTH && len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
+        else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
     }
 
     if (!slow && st == SKQ_READ_OK) {
@@ -583,7 +624,10 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
 
 // the read's hash list at k slot i: (pointer, stride)
 __device__ __forceinline__ uint32_t hash_count(const ChainParams& p, uint64_t r, uint32_t i) {
-    return p.hash_offs ? p.hash_cnt[r * p.nk + i] : p.hash_cnt[(uint64_t)i * p.n + r];
+    // one load from a selected index (a load in each arm of the branch would be waited for at
+    // the join, before the loads that follow could issue)
+    const uint64_t at = p.hash_offs ? r * p.nk + i : (uint64_t)i * p.n + r;
+    return p.hash_cnt[at];
 }
 
 __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint64_t r, uint32_t i,
@@ -1047,14 +1091,21 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
     constexpr int W = NK == 1 ? 1 : 2;  // LDS words per slot
     // one round trip for everything the read needs first: offsets past the read's count are
     // read and ignored (the lofs array spans lcap >= 16 slots per k)
+    // all per-read loads issue before the first branch: the empty asm consumes them, so the
+    // compiler can neither sink a load into the branch that uses it nor split the wait
     uint32_t cnts[NK];
-    const uint8_t st = p.status ? p.status[r] : (uint8_t)SKQ_READ_OK;
-    const uint8_t pf = p.pflag[r];
+    uint32_t st = p.status[r];  // (never null for this kernel)
+    uint32_t pf = p.pflag[r];
 #pragma unroll
     for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, r, i);
     uint32_t lv0[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) lv0[u] = p.lofs[(uint64_t)u * p.n + r];
+    asm volatile("" : "+v"(st), "+v"(pf));
+#pragma unroll
+    for (int i = 0; i < NK; ++i) asm volatile("" : "+v"(cnts[i]));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(lv0[u]));
     if ((st & SKQ_STATUS_MASK) != SKQ_READ_OK) {
         p.cand_cnt[r] = 0;
         return 0;
@@ -1633,7 +1684,7 @@ bool count_bins(const ChainParams& p) { return use_count3(p) && p.nk <= (uint32_
 int launch_sketch(const SketchParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    const size_t lds = sketch_lds_bytes(p.nk, p.tile_chunks, p.hcap);
+    const size_t lds = sketch_lds_bytes(p.nk, p.tile_chunks, p.hcap, p.nthash != 0);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (lds > 160 * 1024) return -1;
     auto go = [&](auto kern) {
