@@ -66,10 +66,16 @@ int skq_index_free(skq_index* idx);
 /* device bytes held, total postings, longest postings list */
 int skq_index_stats(const skq_index* idx, uint64_t* device_bytes, uint64_t* npostings,
                     uint32_t* max_list);
-/* Probe mode of an index: 1 = direct tables (the sketch kernel probes each retained hash with one
- * 4-B gather, DESIGN.md "Index"), 0 = bucket table only (k_probe). Direct tables are built when
- * their total size (4 B x (largest key + 1) per k) fits SKQ_DIRECT_MB (environment, MiB, default
- * 8192; 0 disables) and half the free device memory. Results are identical in both modes. */
+/* Probe structure of an index (DESIGN.md "Index"); results are identical in every mode:
+ *   3 = wide direct tables: a 32-B entry per possible key holding the key's postings list (up to
+ *       7 transcripts inline); the sketch does not probe, the count kernel gathers one entry per
+ *       retained hash. 32 B x (largest key + 1) per k; only for indexes of <= 2^22 transcripts.
+ *   1 = direct tables: a 4-B list offset per possible key, gathered by the sketch kernel.
+ *   2 = rank tables (SKQ_PROBE=rank): 16-B blocks of 32 keys, gathered by the sketch kernel.
+ *   0 = the bucket table only (k_probe).
+ * The first that fits SKQ_DIRECT_MB (environment, MiB, default 49152; 0 disables all but the
+ * bucket table) and half the free device memory is built; SKQ_PROBE = wide | dir | rank forces
+ * one kind. */
 int skq_index_direct(const skq_index* ix);
 
 /* A session owns the device workspace for batches of up to max_reads reads of at most

@@ -67,8 +67,12 @@ struct skq_index {
     uint32_t* d_rovf_t[SKQ_MAX_K] = {};
     const uint32_t* rank[SKQ_MAX_K] = {};
     const uint32_t* rovf[SKQ_MAX_K] = {};
+    uint32_t* d_wdir_t[SKQ_MAX_K] = {};
+    const uint32_t* wdir[SKQ_MAX_K] = {};
+    uint32_t* d_wovf_t[SKQ_MAX_K] = {};
+    const uint32_t* wovf[SKQ_MAX_K] = {};
     uint64_t dir_bytes = 0;
-    int mode = 0;         // 1 = dir tables, 2 = rank tables (the sketch probes)
+    int mode = 0;  // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 4 = block tables
     bool direct = false;  // every slot with a table has a direct table: the sketch probes
 };
 
@@ -220,13 +224,127 @@ int build_rank(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     return 0;
 }
 
+// Wide direct tables: for each distinct k, an 8-word entry per possible key holding the key's
+// whole postings list when it has at most 7 transcripts (the first 7 and the list offset when
+// longer), so a retained hash costs the chain one 64-B line and the sketch no probe at all.
+// 32 B per key up to the largest: 6.9 GB per k at (double)0.05f. Only for k_count3's id range.
+int build_wide(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, const std::vector<uint32_t>* dkeys,
+               const std::vector<uint32_t>* dvals, const uint64_t* len) {
+    hipStream_t st = nullptr;
+    uint64_t need = 0;
+    uint32_t *dk = nullptr, *dv = nullptr;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const uint64_t m = dkeys[t].size();
+        if (m && dvals[t].back() >= 0x80000000u) return fail(-1, "index too large for wide tables");
+        if (dev_alloc(&ix->d_wdir_t[t], len[t] * 8) || dev_alloc(&dk, m) || dev_alloc(&dv, m)) {
+            dev_free(dk);
+            dev_free(dv);
+            return fail(-3, "wide table allocation failed");
+        }
+        if (hipMemsetAsync(ix->d_wdir_t[t], 0, len[t] * 32, st) != hipSuccess ||
+            hipMemcpy(dk, dkeys[t].data(), m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dv, dvals[t].data(), m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            skq::launch_wdir_scatter(ix->d_wdir_t[t], dk, dv, ix->d_lists, m, st) ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            dev_free(dk);
+            dev_free(dv);
+            return fail(-3, "wide table build failed");
+        }
+        dev_free(dk);
+        dev_free(dv);
+        need += len[t] * 32;
+    }
+    ix->dir_bytes = need;
+    for (uint32_t i = 0; i < ix->nk; ++i)
+        for (uint32_t t = 0; t < ntables; ++t)
+            if (tables[t].k == ix->ks[i]) {
+                ix->wdir[i] = ix->d_wdir_t[t];
+                ix->dir_len[i] = len[t];
+            }
+    ix->direct = true;
+    ix->mode = 3;
+    return 0;
+}
+
+// Block tables: for each distinct k, one 64-B block per 32 possible keys (2 B per key: 429 MB per
+// k at (double)0.05f): [bitmap, overflow base, entry A, entry B]. The first two keys of a block
+// carry their list inline ([n, t0..t5], or [0x80000000 | list offset, t0..t5] when longer), so a
+// retained hash costs the chain one 64-B line and no key compare (the bitmap tells a miss); the
+// 3rd+ key of a block (~1 % of keys at 5 %) keeps its list offset in the overflow array.
+int build_block(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, const std::vector<uint32_t>* dkeys,
+                const std::vector<uint32_t>* dvals, const std::vector<uint32_t>& lists) {
+    hipStream_t st = nullptr;
+    uint64_t need = 0;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const uint64_t m = dkeys[t].size();
+        if (m == 0) continue;
+        const uint64_t nb = ((uint64_t)dkeys[t].back() >> 5) + 1;
+        std::vector<uint32_t> bidx, content, ovf;
+        for (uint64_t j = 0; j < m; ++j) {
+            const uint32_t key = dkeys[t][j], off = dvals[t][j];
+            if (bidx.empty() || bidx.back() != key >> 5) {
+                bidx.push_back(key >> 5);
+                content.resize(content.size() + 16, 0);
+                content[content.size() - 15] = (uint32_t)ovf.size();
+            }
+            uint32_t* c = content.data() + content.size() - 16;
+            const uint32_t rank = __builtin_popcount(c[0]);
+            c[0] |= 1u << (key & 31);
+            if (rank >= 2) {
+                ovf.push_back(off);
+                continue;
+            }
+            uint32_t* e = c + 2 + 7 * rank;
+            const uint32_t n = lists[off];
+            if (off >= 0x80000000u) return fail(-1, "index too large for block tables");
+            e[0] = n <= 6 ? n : (0x80000000u | off);
+            for (uint32_t q = 0; q < 6 && q < n; ++q) e[1 + q] = lists[off + 1 + q];
+        }
+        ovf.push_back(0);
+        uint32_t *db = nullptr, *dc = nullptr;
+        const uint64_t nz = bidx.size();
+        if (dev_alloc(&ix->d_wdir_t[t], nb * 16) || dev_alloc(&ix->d_wovf_t[t], ovf.size()) ||
+            dev_alloc(&db, nz) || dev_alloc(&dc, nz * 16)) {
+            dev_free(db);
+            dev_free(dc);
+            return fail(-3, "block table allocation failed");
+        }
+        if (hipMemsetAsync(ix->d_wdir_t[t], 0, nb * 64, st) != hipSuccess ||
+            hipMemcpy(ix->d_wovf_t[t], ovf.data(), ovf.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(db, bidx.data(), nz * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dc, content.data(), nz * 64, hipMemcpyHostToDevice) != hipSuccess ||
+            skq::launch_blk_scatter(ix->d_wdir_t[t], db, dc, nz, st) || hipStreamSynchronize(st) != hipSuccess) {
+            dev_free(db);
+            dev_free(dc);
+            return fail(-3, "block table build failed");
+        }
+        dev_free(db);
+        dev_free(dc);
+        need += nb * 64 + ovf.size() * 4;
+        for (uint32_t i = 0; i < ix->nk; ++i)
+            if (tables[t].k == ix->ks[i]) {
+                ix->wdir[i] = ix->d_wdir_t[t];
+                ix->wovf[i] = ix->d_wovf_t[t];
+                ix->dir_len[i] = nb;
+            }
+    }
+    ix->dir_bytes = need;
+    ix->direct = true;
+    ix->mode = 4;
+    return 0;
+}
+
+// Probe structure: wide tables when they fit SKQ_DIRECT_MB (default 49152 MiB) and half the free
+// device memory and the ids fit k_count3, else 4-B direct tables, else the bucket table alone.
+// SKQ_PROBE = wide | dir | rank forces one kind (development A/B and tests).
 int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
-                 const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals) {
-    uint64_t budget = 8192ull << 20;
+                 const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals,
+                 const std::vector<uint32_t>& lists) {
+    uint64_t budget = 49152ull << 20;
     if (const char* e = std::getenv("SKQ_DIRECT_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     if (budget == 0) return 0;
-    if (const char* e = std::getenv("SKQ_PROBE"))
-        if (!std::strcmp(e, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
+    const char* force = std::getenv("SKQ_PROBE");
+    if (force && !std::strcmp(force, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
     uint64_t need = 0, len[SKQ_MAX_K] = {};
     for (uint32_t t = 0; t < ntables; ++t) {
         len[t] = dkeys[t].empty() ? 0 : (uint64_t)dkeys[t].back() + 1;  // keys ascending
@@ -234,7 +352,17 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     }
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
-    if (need == 0 || need > budget || need > fr / 2) return 0;
+    if (need == 0) return 0;
+    const bool ids_ok = ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull;
+    if (force && !std::strcmp(force, "block")) {
+        if (!ids_ok || need / 2 > budget || need / 2 > fr / 2) return 0;
+        return build_block(ix, ntables, tables, dkeys, dvals, lists);
+    }
+    const bool wide_ok = ix->ntx <= (1u << 22) && need * 8 <= budget && need * 8 <= fr / 2 &&
+                         ix->nlist_words < 0x80000000ull;
+    if (wide_ok && !(force && !std::strcmp(force, "dir"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
+    if (force && !std::strcmp(force, "wide")) return 0;  // forced but does not fit: bucket table
+    if (need > budget || need > fr / 2) return 0;
     hipStream_t st = nullptr;
     uint32_t *dk = nullptr, *dv = nullptr;
     for (uint32_t t = 0; t < ntables; ++t) {
@@ -414,7 +542,7 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
         skq_index_free(ix);
         return fail(-3, "index upload failed");
     }
-    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals)) {
+    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals, lists)) {
         skq_index_free(ix);
         return rc2;
     }
@@ -426,6 +554,8 @@ int skq_index_free(skq_index* ix) {
     if (!ix) return 0;
     DeviceGuard g(ix->device);
     for (auto& d : ix->d_dir_t) dev_free(d);
+    for (auto& d : ix->d_wdir_t) dev_free(d);
+    for (auto& d : ix->d_wovf_t) dev_free(d);
     for (auto& d : ix->d_rank_t) dev_free(d);
     for (auto& d : ix->d_rovf_t) dev_free(d);
     dev_free(ix->d_buckets);
@@ -453,7 +583,7 @@ int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chai
     return 0;
 }
 
-int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? 1 : 0; }
+int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? ix->mode : 0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
     if (!ix || !out) return fail(-1, "null argument");
@@ -536,8 +666,10 @@ int skq_session_free(skq_session* s) {
     return 0;
 }
 
+// prep: fill *prep and the session's batch state without launching (the fused map launches)
 static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
-                       uint64_t n_reads, uint32_t max_len, uint32_t threshold, int nthash, void* stream) {
+                       uint64_t n_reads, uint32_t max_len, uint32_t threshold, int nthash, void* stream,
+                       skq::SketchParams* prep = nullptr) {
     if (!s) return fail(-1, "null session");
     if (n_reads > s->max_reads) return fail(-1, "batch larger than the session's max_reads");
     if (n_reads && !d_reads) return fail(-1, "null reads");
@@ -579,12 +711,16 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     p.pflag = s->pflag;
     p.variant = s->variant;
     p.nthash = nthash;
-    HIP_TRY(hipMemsetAsync(s->ctrl, 0, 8 * 4, st));
-    hipEvent_t t0{};
-    record(s, 0, &t0, st);
-    if (skq::launch_sketch(p, stream)) return fail(-3, "sketch launch failed");
-    record_stop(s, 0, t0, st);
-    if (skq::launch_sketch_slow(p, stream)) return fail(-3, "sketch slow-path launch failed");
+    if (prep) {
+        *prep = p;
+    } else {
+        HIP_TRY(hipMemsetAsync(s->ctrl, 0, 8 * 4, st));
+        hipEvent_t t0{};
+        record(s, 0, &t0, st);
+        if (skq::launch_sketch(p, stream)) return fail(-3, "sketch launch failed");
+        record_stop(s, 0, t0, st);
+        if (skq::launch_sketch_slow(p, stream)) return fail(-3, "sketch slow-path launch failed");
+    }
     s->hcap = hcap;
     s->n_reads = n_reads;
     s->have_sketch = true;
@@ -607,7 +743,8 @@ int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_off
 
 static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const uint32_t* hash_cnt,
                       const uint32_t* hashes, const uint64_t* hash_offs, const uint8_t* present,
-                      uint32_t hcap, double fraction, int accumulate, bool probed, void* stream) {
+                      uint32_t hcap, double fraction, int accumulate, bool probed, void* stream,
+                      skq::ChainParams* prep = nullptr) {
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const skq_index* ix = s->idx;
@@ -643,6 +780,17 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.pflag = s->pflag;
     // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
     p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
+    // wide tables: the count kernel reads the sketch's hashes and gathers the entries itself
+    p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 4 ? 2 : 0;
+    if (p.wide) {
+        if (s->variant == 4) return fail(-1, "variant 4 (k_count) does not read wide tables");
+        p.lofs = const_cast<uint32_t*>(hashes);
+        for (uint32_t i = 0; i < ix->nk; ++i) {
+            p.wdir[i] = ix->wdir[i];
+            p.wdir_len[i] = ix->dir_len[i];
+            p.wovf[i] = ix->wovf[i];
+        }
+    }
     p.variant = s->variant;
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
@@ -650,6 +798,10 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.bin_hdr = s->bin_hdr;
     p.bin_region = s->bin_region;
     p.slow_totals = accumulate && skq::count_bins(p);
+    if (prep) {
+        *prep = p;
+        return 0;
+    }
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
     if (!probed) {
@@ -680,9 +832,53 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
                       fraction, accumulate, s->probed, stream);
 }
 
+// Fused map (k_map1): wide tables, one k slot, a raw capacity of 16 or 32 (variant 6 and the
+// sketch-side timing variants take the two-kernel path)
+static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,
+                        uint32_t threshold) {
+    const skq_index* ix = s->idx;
+    if (ix->mode != 3 || ix->nk != 1) return false;
+    if (s->variant == 1 || s->variant == 2 || s->variant == 4 || s->variant == 6) return false;
+    if (!d_offs) max_len = fixed_len;
+    const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
+    const uint32_t hcap = pick_hcap(Lc, ix->mink, threshold);
+    return hcap == 16 || hcap == 32;
+}
+
+static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
+                     uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction, int accumulate,
+                     void* stream) {
+    skq::SketchParams sp{};
+    skq::ChainParams cp{};
+    if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
+    if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
+                            accumulate, true, stream, &cp))
+        return rc;
+    DeviceGuard g(s->idx->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
+    hipEvent_t t0{};
+    record(s, 0, &t0, st);
+    if (int rc = skq::launch_map1(sp, cp, stream)) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
+    record_stop(s, 0, t0, st);
+    if (skq::launch_sketch_slow(sp, stream)) return fail(-3, "sketch slow-path launch failed");
+    if (skq::launch_chain_slow(cp, stream)) return fail(-3, "chain slow-path launch failed");
+    if (accumulate) {
+        record(s, 3, &t0, st);
+        if (skq::launch_bin(cp, cp.slow_totals, stream)) return fail(-3, "totals launch failed");
+        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, stream))
+            return fail(-3, "totals fold launch failed");
+        record_stop(s, 3, t0, st);
+    }
+    s->have_chain = true;
+    return 0;
+}
+
 int skq_map(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
             uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction, int accumulate,
             void* stream) {
+    if (s && n_reads && map_fusable(s, d_offs, fixed_len, max_len, threshold))
+        return map_fused(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, fraction, accumulate, stream);
     if (int rc = skq_sketch(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, stream)) return rc;
     return skq_chain(s, fraction, accumulate, stream);
 }

@@ -82,7 +82,8 @@ struct SketchParams {
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
     // the slow chain path. Slots without a table (dir[i] null) are skipped by the chain.
-    int fuse;                        // 1 = dir tables, 2 = rank tables
+    // (3 = wide direct tables: the sketch does not probe; k_count3 gathers the entries)
+    int fuse;                        // 1 = dir tables, 2 = rank tables, 3 = wide tables
     const uint32_t* dir[SKQ_MAX_K];
     uint64_t dir_len[SKQ_MAX_K];     // dir: entries; rank: blocks
     const uint32_t* rank[SKQ_MAX_K]; // rank table, 16-B blocks {bitmap of 32 keys, overflow base, v0, v1}
@@ -136,6 +137,19 @@ struct ChainParams {
     uint32_t* bin_region;
     int slow_totals;
     int variant;               // development A/B switch (0 = default)
+    // wide direct tables (DESIGN.md "Index"): entry h of k slot i is 8 words at wdir[i] + 8h,
+    // [n, t0..t6] for lists of n <= 7 transcripts, [0x80000000 | list offset, t0..t6] for longer
+    // ones (the rest at lists[offset + 8..]), n = 0 for no key; h >= wdir_len[i] is a miss.
+    // wide = 1: lofs holds the sketch's hashes themselves (k_count3 only)
+    // Block tables (wide = 2): block h >> 5 of k slot i is 16 words at wdir[i] + 16 * (h >> 5):
+    // [bitmap of its 32 keys, overflow base, entry A (7 words), entry B (7 words)]; the first two
+    // keys of a block (by key order) have entries [n, t0..t5] (n <= 6) or [0x80000000 | list
+    // offset, t0..t5]; the 3rd+ key's list offset is wovf[i][overflow base + rank - 2].
+    // wdir_len = blocks.
+    int wide;
+    const uint32_t* wdir[SKQ_MAX_K];
+    uint64_t wdir_len[SKQ_MAX_K];
+    const uint32_t* wovf[SKQ_MAX_K];
 };
 
 // records the message returned by skq_last_error(); returns code (skq_capi.hip)
@@ -144,6 +158,8 @@ int set_error(int code, const char* msg);
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream);
+// fused sketch + chain (k_map1: quant mode, one k slot, wide tables, hcap 16 or 32; -4 otherwise)
+int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream);
@@ -154,6 +170,11 @@ int launch_bin(const ChainParams& p, int binned, void* stream);
 // whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)
 bool count_bins(const ChainParams& p);
 int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n, void* stream);
+// block tables: blk[bidx[j]] = content[j] (16 words each)
+int launch_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* content, uint64_t n, void* stream);
+// fills wide entries wdir[keys[j]] from the postings lists at lists[vals[j]]
+int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
+                        uint64_t n, void* stream);
 
 #ifdef __HIPCC__
 #define SKQ_HD __host__ __device__

@@ -20,6 +20,8 @@
 //                  work lists with a fixed grid, so no host round trip is needed.
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include <algorithm>
 
 #include "skq_internal.h"
@@ -29,6 +31,16 @@ namespace skq {
 
 // ---------------------------------------------------------------------------------------------
 // small helpers
+
+// f(std::integral_constant<int, 0>{}) ... f(std::integral_constant<int, N - 1>{})
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 template <typename T>
 __device__ __forceinline__ void cswap(T& a, T& b) {
@@ -1083,84 +1095,351 @@ __global__ __launch_bounds__(WG) void k_route_slow(ChainParams p) {
 constexpr int TS = 16;    // distinct transcripts per read on the fast path (slot TS: sink)
 constexpr int PEND = 8;   // parked collisions per read (slot PEND: sink)
 
+// swap with the other lane of the pair (quad_perm(1,0,3,2))
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) { return quad_dpp<0xB1>(v); }
+__device__ __forceinline__ uint4 pair_swap(uint4 v) {
+    return make_uint4(pair_swap(v.x), pair_swap(v.y), pair_swap(v.z), pair_swap(v.w));
+}
+
+// Per-read transcript counter of the fast chain path (src/sparse_chaining.cpp:55-110): a
+// lane-private open-addressing table of TS slots in LDS, slot s at tab[s * WG] (slot TS: a sink
+// for writes not taken), W words per slot (NK == 1: tid << 8 | count; else tid, then 4 packed
+// 8-bit per-k counts), and up to PEND parked items at pend[e * PS] (slot PEND: sink).
+template <int NK, int PS>
+struct Counter {
+    static constexpr int W = NK == 1 ? 1 : 2;
+    uint32_t* tab;   // this lane's slot 0
+    uint32_t* pend;  // this lane's parked item 0
+    bool one;        // development A/B (variant 5): single-slot insert
+    uint32_t occ = 0;  // bit s: slot s holds a transcript
+    uint32_t np = 0;   // parked items
+
+    __device__ Counter(uint32_t* t, uint32_t* pe, bool single) : tab(t), pend(pe), one(single) {}
+    __device__ static uint32_t slot_of(uint32_t x) { return (x * 0x9E3779B1u) >> 28; }
+    __device__ uint32_t slot2_of(uint32_t x) const { return one ? slot_of(x) : (x * 0x85EBCA77u) >> 28; }
+    __device__ uint32_t& at(uint32_t w) { return tab[w * WG]; }
+
+    // transcript x gains rl at k slot i. Two candidate slots, checked in order (slots are never
+    // freed, so a transcript found in neither is in neither); both taken by other transcripts:
+    // parked for the linear-probing pass that runs after every direct insert
+    __device__ __forceinline__ void insert(uint32_t x, uint32_t rl, int i, bool valid) {
+        const uint32_t s1 = slot_of(x), s2 = slot2_of(x);
+        const bool u1 = (occ >> s1) & 1u, u2 = (occ >> s2) & 1u;
+        if (W == 1) {
+            const uint32_t e1 = at(s1), e2 = at(s2);
+            const bool h1 = u1 && (e1 >> 8) == x, h2 = u2 && (e2 >> 8) == x;
+            const bool c1 = !u1 || h1, c2 = !u2 || h2;
+            const uint32_t sl = c1 ? s1 : s2, e = c1 ? e1 : e2;
+            const bool hit = c1 ? h1 : h2;
+            const bool take = valid && (c1 || c2);
+            at(take ? sl : (uint32_t)TS) = hit ? e + rl : (x << 8) | rl;
+            occ |= take ? (1u << sl) : 0u;
+            const bool park = valid && !take;
+            pend[min(np, (uint32_t)PEND) * PS] = x | (rl << 22) | ((uint32_t)i << 29);
+            np += park ? 1u : 0u;
+        } else {
+            const uint32_t t1 = at(2 * s1), t2 = at(2 * s2);
+            const bool h1 = u1 && t1 == x, h2 = u2 && t2 == x;
+            const bool c1 = !u1 || h1, c2 = !u2 || h2;
+            const uint32_t sl = c1 ? s1 : s2;
+            const bool hit = c1 ? h1 : h2;
+            const uint32_t cx = at(2 * sl + 1);
+            const bool take = valid && (c1 || c2);
+            const uint32_t ws = take ? sl : (uint32_t)TS;
+            at(2 * ws) = x;
+            at(2 * ws + 1) = (hit ? cx : 0u) + (rl << (8 * i));
+            occ |= take ? (1u << sl) : 0u;
+            const bool park = valid && !take;
+            pend[min(np, (uint32_t)PEND) * PS] = x | (rl << 22) | ((uint32_t)i << 29);
+            np += park ? 1u : 0u;
+        }
+    }
+
+    // parked items: full linear probing. false: more than PEND parked or more than TS distinct
+    // transcripts (the read takes the slow chain path)
+    __device__ __forceinline__ bool drain() {
+        if (np > (uint32_t)PEND) return false;
+        for (uint32_t e = 0; e < np; ++e) {
+            const uint32_t it = pend[e * PS];
+            const uint32_t x = it & 0x3FFFFFu, rl = (it >> 22) & 0x7Fu;
+            const int i = (int)(it >> 29);
+            uint32_t q = slot_of(x);
+            bool done = false;
+            for (int z = 0; z < TS && !done; ++z) {
+                const bool used = (occ >> q) & 1u;
+                if (W == 1) {
+                    const uint32_t ev = at(q);
+                    if (!used || (ev >> 8) == x) {
+                        at(q) = used ? ev + rl : (x << 8) | rl;
+                        occ |= 1u << q;
+                        done = true;
+                    }
+                } else {
+                    const uint32_t tx = at(2 * q);
+                    if (!used || tx == x) {
+                        at(2 * q) = x;
+                        at(2 * q + 1) = (used ? at(2 * q + 1) : 0u) + (rl << (8 * i));
+                        occ |= 1u << q;
+                        done = true;
+                    }
+                }
+                q = (q + 1) & (TS - 1);
+            }
+            if (!done) return false;
+        }
+        return true;
+    }
+
+    // filter and order (src/sparse_chaining.cpp:76-110), write the read's candidates and return
+    // their number; key[] holds them first, in output order
+    __device__ __forceinline__ uint32_t finish(const ChainParams& p, uint64_t r, uint32_t (&key)[TS]) {
+        // two passes over the table (the slots are re-read rather than held in registers):
+        // per-k maximum (src/sparse_chaining.cpp:76-82), then the filter
+        // (double)c >= fraction * max  <=>  c >= ceil(fraction * max)  (:84-87, :93), as in k_count
+        auto slot_counts = [&](int sl) -> uint32_t {
+            const uint32_t c = W == 1 ? at(sl) & 0xFFu : at(2 * sl + 1);
+            return ((occ >> sl) & 1u) ? c : 0u;
+        };
+        uint32_t need[NK];
+        {
+            uint32_t m[NK] = {};
+#pragma unroll
+            for (int sl = 0; sl < TS; ++sl) {
+                const uint32_t c = slot_counts(sl);
+#pragma unroll
+                for (int i = 0; i < NK; ++i) m[i] = max(m[i], (c >> (8 * i)) & 0xFFu);
+            }
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const double thr = p.fraction * (double)m[i];
+                uint32_t ti = 0;
+                if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+                need[i] = ti;
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < TS; ++sl) {
+            const uint32_t c = slot_counts(sl);
+            const uint32_t tid = W == 1 ? at(sl) >> 8 : at(2 * sl);
+            bool ok = (occ >> sl) & 1u;
+            uint32_t score = 0;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const uint32_t ci = (c >> (8 * i)) & 0xFFu;
+                ok &= ci >= need[i];
+                score += ci;
+            }
+            // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
+            key[sl] = ok ? ((1023u - score) << 22) | tid : ~0u;
+        }
+        bitonic_sort<TS>(key);
+        uint32_t nc = 0;
+        uint32_t* ct = p.cand_tid + r;
+        uint32_t* cs = p.cand_score + r;
+#pragma unroll
+        for (int d = 0; d < TS; ++d) {
+            if (key[d] != ~0u) {
+                const uint32_t tid = key[d] & 0x3FFFFFu;
+                const uint32_t score = 1023u - (key[d] >> 22);
+                ct[(uint64_t)d * p.n] = tid;
+                cs[(uint64_t)d * p.n] = score;
+                ++nc;
+            }
+        }
+        p.cand_cnt[r] = nc;
+        return nc;
+    }
+};
+
+// Up to 8 retained hashes of k slot i against a wide table: dl[u] = h << 3 (the entry's word
+// offset) or ~0u. Entries are gathered by lane pairs (each lane loads one 16-B half of both
+// lanes' entries, so a pair fetches whole 32-B entries; then the two swap the half that
+// belongs to the other), 4 per lane in flight; both lanes of every pair must run this.
+template <int NK, int PS, int B = 4>
+__device__ __forceinline__ void wide_chunk(Counter<NK, PS>& c, const ChainParams& p, const uint32_t* wd,
+                                           const uint32_t (&dl)[8], bool odd, int i) {
+    static_assert(B == 4 || B == 8, "batch of 4 or 8 entries per lane");
+#pragma unroll
+    for (int u0 = 0; u0 < 8; u0 += B) {
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < B; ++u) any |= dl[u0 + u] != ~0u;
+        if (!__any(any)) continue;
+        uint4 la[B], lb[B], head[B], more[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const uint32_t mine = dl[u0 + u], theirs = pair_swap(mine);
+            const uint32_t ea = odd ? theirs : mine, eb = odd ? mine : theirs;
+            const uint32_t part = odd ? 4u : 0u;
+            la[u] = *reinterpret_cast<const uint4*>(wd + (ea != ~0u ? (uint64_t)ea : 0ull) + part);
+            lb[u] = *reinterpret_cast<const uint4*>(wd + (eb != ~0u ? (uint64_t)eb : 0ull) + part);
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const uint4 rcv = pair_swap(odd ? la[u] : lb[u]);
+            const uint4 h = odd ? rcv : la[u], m = odd ? lb[u] : rcv;
+            head[u] = dl[u0 + u] != ~0u ? h : make_uint4(0, 0, 0, 0);
+            more[u] = m;
+        }
+        bool lng = false;
+#pragma unroll
+        for (int u = 0; u < B; ++u) lng |= head[u].x > 3;
+        const bool any_long = __any(lng);
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const uint32_t n = head[u].x;  // [0x80000000 | offset] for lists longer than 7
+            c.insert(head[u].y, 1, i, n > 0);
+            c.insert(head[u].z, 1, i, n > 1);
+            c.insert(head[u].w, 1, i, n > 2);
+            if (any_long) {
+                c.insert(more[u].x, 1, i, n > 3);
+                c.insert(more[u].y, 1, i, n > 4);
+                c.insert(more[u].z, 1, i, n > 5);
+                c.insert(more[u].w, 1, i, n > 6);
+            }
+        }
+        // lists longer than 7 (rare): the rest from the postings list, one at a time
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (__any(head[u].x > 7) && head[u].x > 7) {
+                const uint32_t lo = head[u].x & 0x7FFFFFFFu;
+                const uint32_t len = p.lists[lo];
+                for (uint32_t q = 7; q < len; ++q) c.insert(p.lists[lo + 1 + q], 1, i, true);
+            }
+    }
+}
+
 // one read of k_count3: writes its candidates (and cand_cnt) and returns their number, the
-// first nc of key[] holding them in output order
-template <int NK>
+// first nc of key[] holding them in output order. MODE: 0 = lofs hold list offsets (k_probe or
+// the fused dir/rank probe), 1 = wide tables, 2 = block tables (lofs hold the hashes).
+// Wide tables are gathered by lane pairs (wide_chunk), so in MODE 1 every lane of the wave runs
+// the gather loops, reads past n and inactive reads with no hashes.
+template <int NK, int MODE>
 __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r, uint32_t t, uint32_t (*s_tab)[WG],
                                                uint32_t (*s_pend)[WG], uint32_t (&key)[TS]) {
-    constexpr int W = NK == 1 ? 1 : 2;  // LDS words per slot
+    constexpr bool COOP = MODE == 1;
+    const bool inb = r < p.n;
+    const uint64_t rr = inb ? r : p.n - 1;  // (p.n > 0)
     // one round trip for everything the read needs first: offsets past the read's count are
     // read and ignored (the lofs array spans lcap >= 16 slots per k)
     // all per-read loads issue before the first branch: the empty asm consumes them, so the
     // compiler can neither sink a load into the branch that uses it nor split the wait
     uint32_t cnts[NK];
-    uint32_t st = p.status[r];  // (never null for this kernel)
-    uint32_t pf = p.pflag[r];
+    uint32_t st = p.status[rr];  // (never null for this kernel)
+    uint32_t pf = p.pflag[rr];
 #pragma unroll
-    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, r, i);
+    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, rr, i);
     uint32_t lv0[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) lv0[u] = p.lofs[(uint64_t)u * p.n + r];
+    for (int u = 0; u < 8; ++u) lv0[u] = p.lofs[(uint64_t)u * p.n + rr];
     asm volatile("" : "+v"(st), "+v"(pf));
 #pragma unroll
     for (int i = 0; i < NK; ++i) asm volatile("" : "+v"(cnts[i]));
 #pragma unroll
     for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(lv0[u]));
-    if ((st & SKQ_STATUS_MASK) != SKQ_READ_OK) {
-        p.cand_cnt[r] = 0;
-        return 0;
-    }
-    if (p.variant == 1 || p.variant == 2) {  // sketch-side timing variants: lofs hold no offsets
-        p.cand_cnt[r] = 0;
-        return 0;
-    }
-    if (pf) {
-        list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
-        p.cand_cnt[r] = 0;
-        return 0;
-    }
-    uint32_t occ = 0;  // bit s: slot s holds a transcript
-    uint32_t np = 0;   // parked items
-    auto slot_of = [](uint32_t x) -> uint32_t { return (x * 0x9E3779B1u) >> 28; };
-    // item: transcript x gains rl at k slot i
-    auto insert = [&](uint32_t x, uint32_t rl, int i, bool valid) {
-        const uint32_t sl = slot_of(x);
-        const bool used = (occ >> sl) & 1u;
-        bool hit;
-        if (W == 1) {
-            const uint32_t e = s_tab[sl][t];
-            hit = used && (e >> 8) == x;
-            const bool take = valid && (!used || hit);
-            s_tab[take ? sl : (uint32_t)TS][t] = hit ? e + rl : (x << 8) | rl;
-            occ |= take ? (1u << sl) : 0u;
-            const bool park = valid && !take;
-            s_pend[min(np, (uint32_t)PEND)][t] = x | (rl << 22) | ((uint32_t)i << 29);
-            np += park ? 1u : 0u;
-        } else {
-            const uint32_t tx = s_tab[2 * sl][t], cx = s_tab[2 * sl + 1][t];
-            hit = used && tx == x;
-            const bool take = valid && (!used || hit);
-            const uint32_t ws = take ? sl : (uint32_t)TS;
-            s_tab[2 * ws][t] = x;
-            s_tab[2 * ws + 1][t] = (hit ? cx : 0u) + (rl << (8 * i));
-            occ |= take ? (1u << sl) : 0u;
-            const bool park = valid && !take;
-            s_pend[min(np, (uint32_t)PEND)][t] = x | (rl << 22) | ((uint32_t)i << 29);
-            np += park ? 1u : 0u;
-        }
-    };
+    // (sketch-side timing variants 1 and 2: lofs hold no offsets)
+    const bool ok = inb && (st & SKQ_STATUS_MASK) == SKQ_READ_OK && p.variant != 1 && p.variant != 2;
+    if (ok && pf) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+    const bool act = ok && !pf;
+    if (inb && !act) p.cand_cnt[r] = 0;
+    if (!COOP && !act) return 0;
+    Counter<NK, WG> c(&s_tab[0][t], &s_pend[0][t], p.variant == 5);
+    // k slots expanded at compile time (an unrolled loop this size exceeds the unroller's limit,
+    // and a rolled one would put cnts/lv0 in scratch)
+    static_for<NK>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if (!p.tabs[i].present) return;  // uniform
+        const bool pres = !(p.present && !p.present[rr * NK + i]);
+        if (!COOP && !pres) return;
+        const uint32_t cnt = act && pres ? cnts[i] : 0u;
+        const uint32_t cmax = COOP ? max(cnt, pair_swap(cnt)) : cnt;  // the pair's trip count
+        const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + rr;
+        constexpr bool blocks = MODE == 2;
+        const uint32_t* wd = p.wdir[i];
+        const uint64_t wlen = p.wdir_len[i];
+        for (uint32_t j0 = 0; j0 < cmax; j0 += 8) {
+            // this chunk's 8 lofs: the prologue's for the first chunk of k slot 0, else loaded
+            // (the asm keeps the compiler from merging the two arms into one load through a
+            // selected pointer, which would put lv0 in scratch)
+            uint32_t xs[8];
+            if (i == 0 && j0 == 0) {  // uniform
 #pragma unroll
-    for (int i = 0; i < NK; ++i) {
-        if (!p.tabs[i].present || (p.present && !p.present[r * NK + i])) continue;
-        const uint32_t cnt = cnts[i];
-        const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + r;
-        for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
+                for (int u = 0; u < 8; ++u) xs[u] = lv0[u];
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    uint32_t g = lo_i[(uint64_t)min(j0 + u, p.lcap - 1) * p.n];
+                    asm volatile("" : "+v"(g));
+                    xs[u] = g;
+                }
+            }
+            uint32_t dl[8];
+            if (COOP) {
+                // lofs holds the read's distinct retained hashes, front-packed: each is one
+                // entry; a hash past the table is a miss
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dl[u] = (j0 + u < cnt && xs[u] < wlen) ? xs[u] << 3 : ~0u;
+                wide_chunk(c, p, wd, dl, t & 1u, i);
+                continue;
+            }
+            if (blocks) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dl[u] = (j0 + u < cnt && (xs[u] >> 5) < wlen) ? xs[u] : ~0u;
+#pragma unroll
+                for (int u0 = 0; u0 < 8; u0 += 4) {
+                    if (u0 && !__any(j0 + u0 < cmax)) break;
+                    // one 64-B block per hash, all four in flight; the bitmap says whether the
+                    // key exists and its rank in the block
+                    uint4 b[4][4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool v = dl[u0 + u] != ~0u;
+                        const uint4* e = reinterpret_cast<const uint4*>(wd + (v ? (uint64_t)(dl[u0 + u] >> 5) * 16 : 0ull));
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) b[u][q] = e[q];
+                    }
+                    uint32_t tail_lo[4], tail_q0[4];
+                    bool tail[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t x = dl[u0 + u];
+                        const uint32_t bm = b[u][0].x, bit = x & 31u;
+                        const bool hit = x != ~0u && ((bm >> bit) & 1u);
+                        const uint32_t rank = __builtin_popcount(bm & ((1u << bit) - 1u));
+                        const bool a = rank == 0;
+                        const uint32_t meta = a ? b[u][0].z : b[u][2].y;
+                        const uint32_t w1 = a ? b[u][0].w : b[u][2].z, w2 = a ? b[u][1].x : b[u][2].w;
+                        const uint32_t w3 = a ? b[u][1].y : b[u][3].x, w4 = a ? b[u][1].z : b[u][3].y;
+                        const uint32_t w5 = a ? b[u][1].w : b[u][3].z, w6 = a ? b[u][2].x : b[u][3].w;
+                        const bool inl = hit && rank < 2;
+                        const uint32_t n = inl ? ((meta & 0x80000000u) ? 7u : meta) : 0u;
+                        c.insert(w1, 1, i, n > 0);
+                        c.insert(w2, 1, i, n > 1);
+                        c.insert(w3, 1, i, n > 2);
+                        c.insert(w4, 1, i, n > 3);
+                        c.insert(w5, 1, i, n > 4);
+                        c.insert(w6, 1, i, n > 5);
+                        tail[u] = hit && (rank >= 2 || (meta & 0x80000000u));
+                        tail_lo[u] = rank >= 2 ? b[u][0].y + rank - 2 : (meta & 0x7FFFFFFFu);
+                        tail_q0[u] = rank >= 2 ? 0u : 6u;
+                    }
+                    // 3rd+ keys of a block (their list from the overflow array) and lists longer
+                    // than 6 (the rest of the list): rare, one at a time
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (__any(tail[u]) && tail[u]) {
+                            const uint32_t lo = tail_q0[u] == 0 ? p.wovf[i][tail_lo[u]] : tail_lo[u];
+                            const uint32_t len = p.lists[lo];
+                            for (uint32_t q = tail_q0[u]; q < len; ++q) c.insert(p.lists[lo + 1 + q], 1, i, true);
+                        }
+                }
+                continue;
+            }
+            // list offsets: sort, so repeats of one list (different keys, same postings) are
+            // counted once with their run length
             uint32_t lv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t x = (i == 0 && j0 == 0) ? lv0[u] : lo_i[(uint64_t)min(j0 + u, p.lcap - 1) * p.n];
-                lv[u] = j0 + u < cnt ? x : ~0u;
-            }
+            for (int u = 0; u < 8; ++u) lv[u] = j0 + u < cnt ? xs[u] : ~0u;
             bitonic_sort<8>(lv);  // misses (~0u) sort last
             uint32_t rl[8];
             rl[7] = 1;
@@ -1168,7 +1447,6 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
             for (int u = 6; u >= 0; --u) rl[u] = lv[u] == lv[u + 1] ? rl[u + 1] + 1 : 1;
             // compact the distinct lists to the front: (offset << 3 | run - 1) for run starts
             // (offsets < 2^29 words, runs <= 8), everything else sorts last
-            uint32_t dl[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const bool start = lv[u] != ~0u && (u == 0 || lv[u] != lv[u - 1]);
@@ -1203,14 +1481,14 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
                 for (int u = 0; u < 4; ++u) {
                     const uint32_t n = head[u].x;  // 0 past the distinct lists
                     const uint32_t run = (dl[u0 + u] & 7u) + 1;
-                    insert(head[u].y, run, i, n > 0);
-                    insert(head[u].z, run, i, n > 1);
-                    insert(head[u].w, run, i, n > 2);
+                    c.insert(head[u].y, run, i, n > 0);
+                    c.insert(head[u].z, run, i, n > 1);
+                    c.insert(head[u].w, run, i, n > 2);
                     if (any_long) {
-                        insert(more[u].x, run, i, n > 3);
-                        insert(more[u].y, run, i, n > 4);
-                        insert(more[u].z, run, i, n > 5);
-                        insert(more[u].w, run, i, n > 6);
+                        c.insert(more[u].x, run, i, n > 3);
+                        c.insert(more[u].y, run, i, n > 4);
+                        c.insert(more[u].z, run, i, n > 5);
+                        c.insert(more[u].w, run, i, n > 6);
                     }
                 }
                 // lists longer than 7 (rare): one at a time
@@ -1218,126 +1496,25 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
                 for (int u = 0; u < 4; ++u)
                     if (__any(head[u].x > 7))
                         for (uint32_t q = 7; q < head[u].x; ++q)
-                            insert(p.lists[(dl[u0 + u] >> 3) + 1 + q], (dl[u0 + u] & 7u) + 1, i, true);
+                            c.insert(p.lists[(dl[u0 + u] >> 3) + 1 + q], (dl[u0 + u] & 7u) + 1, i, true);
             }
         }
-    }
-    // parked items: full linear probing
-    bool slow = np > (uint32_t)PEND;
-    for (uint32_t e = 0; e < np && !slow; ++e) {
-        const uint32_t it = s_pend[e][t];
-        const uint32_t x = it & 0x3FFFFFu, rl = (it >> 22) & 0x7Fu;
-        const int i = (int)(it >> 29);
-        uint32_t q = slot_of(x);
-        bool done = false;
-        for (int z = 0; z < TS && !done; ++z) {
-            const bool used = (occ >> q) & 1u;
-            if (W == 1) {
-                const uint32_t ev = s_tab[q][t];
-                if (!used || (ev >> 8) == x) {
-                    s_tab[q][t] = used ? ev + rl : (x << 8) | rl;
-                    occ |= 1u << q;
-                    done = true;
-                }
-            } else {
-                const uint32_t tx = s_tab[2 * q][t];
-                if (!used || tx == x) {
-                    s_tab[2 * q][t] = x;
-                    s_tab[2 * q + 1][t] = (used ? s_tab[2 * q + 1][t] : 0u) + (rl << (8 * i));
-                    occ |= 1u << q;
-                    done = true;
-                }
-            }
-            q = (q + 1) & (TS - 1);
-        }
-        slow = !done;  // more than TS distinct transcripts
-    }
-    if (slow) {
+    });
+    if (COOP && !act) return 0;
+    if (!c.drain()) {
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
         return 0;
     }
-    // two passes over the table (the slots are re-read rather than held in registers):
-    // per-k maximum (src/sparse_chaining.cpp:76-82), then the filter
-    // (double)c >= fraction * max  <=>  c >= ceil(fraction * max)  (:84-87, :93), as in k_count
-    auto slot_counts = [&](int sl) -> uint32_t {
-        const uint32_t c = W == 1 ? s_tab[sl][t] & 0xFFu : s_tab[2 * sl + 1][t];
-        return ((occ >> sl) & 1u) ? c : 0u;
-    };
-    uint32_t need[NK];
-    {
-        uint32_t m[NK] = {};
-#pragma unroll
-        for (int sl = 0; sl < TS; ++sl) {
-            const uint32_t c = slot_counts(sl);
-#pragma unroll
-            for (int i = 0; i < NK; ++i) m[i] = max(m[i], (c >> (8 * i)) & 0xFFu);
-        }
-#pragma unroll
-        for (int i = 0; i < NK; ++i) {
-            const double thr = p.fraction * (double)m[i];
-            uint32_t ti = 0;
-            if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
-            need[i] = ti;
-        }
-    }
-#pragma unroll
-    for (int sl = 0; sl < TS; ++sl) {
-        const uint32_t c = slot_counts(sl);
-        const uint32_t tid = W == 1 ? s_tab[sl][t] >> 8 : s_tab[2 * sl][t];
-        bool ok = (occ >> sl) & 1u;
-        uint32_t score = 0;
-#pragma unroll
-        for (int i = 0; i < NK; ++i) {
-            const uint32_t ci = (c >> (8 * i)) & 0xFFu;
-            ok &= ci >= need[i];
-            score += ci;
-        }
-        // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
-        key[sl] = ok ? ((1023u - score) << 22) | tid : ~0u;
-    }
-    bitonic_sort<TS>(key);
-    uint32_t nc = 0;
-    uint32_t* ct = p.cand_tid + r;
-    uint32_t* cs = p.cand_score + r;
-#pragma unroll
-    for (int d = 0; d < TS; ++d) {
-        if (key[d] != ~0u) {
-            const uint32_t tid = key[d] & 0x3FFFFFu;
-            const uint32_t score = 1023u - (key[d] >> 22);
-            ct[(uint64_t)d * p.n] = tid;
-            cs[(uint64_t)d * p.n] = score;
-            ++nc;
-        }
-    }
-    p.cand_cnt[r] = nc;
-    return nc;
+    return c.finish(p, r, key);
 }
 
-// The count kernel: count_read per lane, then (totals requested) the workgroup's candidates are
-// binned for k_bin_sum as k_bin does, straight from registers: counts per transcript bucket in
-// LDS, one wave scans them (hdr), entries are placed in LDS (reusing the dead count tables) and
-// the region leaves in coalesced 16-B stores.
-template <int NK>
-__global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
-    constexpr int W = NK == 1 ? 1 : 2;
-    constexpr int WORDS = ((TS + 1) * W + PEND + 1) * WG;
-    static_assert(WORDS >= WG * CCAP, "the region staging reuses the count tables");
-    __shared__ __attribute__((aligned(16))) uint32_t s_mem[WORDS];
-    __shared__ uint32_t s_bc[WG + 1];
-    auto s_tab = reinterpret_cast<uint32_t(*)[WG]>(s_mem);
-    auto s_pend = reinterpret_cast<uint32_t(*)[WG]>(s_mem + (TS + 1) * W * WG);
-    const uint32_t t = threadIdx.x, w = blockIdx.x;
-    const uint64_t r = (uint64_t)w * WG + t;
-    const bool bin = p.accumulate && p.bin_nb;  // uniform
-    if (bin) {
-        s_bc[t] = 0;
-        __syncthreads();
-    }
-    uint32_t key[TS];
-    uint32_t nc = 0;
-    if (r < p.n) nc = count_read<NK>(p, r, t, s_tab, s_pend, key);
-    if (!bin) return;
+// Binning epilogue (totals requested): the workgroup's candidates are binned for k_bin_sum as
+// k_bin does, straight from registers: counts per transcript bucket in LDS (s_bc, zeroed before),
+// one wave scans them (hdr), entries are placed in LDS (s_mem: >= WG * CCAP words no longer in
+// use) and the region leaves in coalesced 16-B stores. Every thread of the workgroup calls it.
+__device__ __forceinline__ void bin_candidates(const ChainParams& p, uint32_t t, uint32_t w, uint32_t nc,
+                                               const uint32_t (&key)[TS], uint32_t* s_bc, uint32_t* s_mem) {
     const uint32_t bits = p.bin_bits, nb = p.bin_nb, nW = gridDim.x;
 #pragma unroll
     for (int d = 0; d < TS; ++d)
@@ -1377,6 +1554,359 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
     uint4* reg = reinterpret_cast<uint4*>(p.bin_region + (uint64_t)w * (WG * CCAP));
     const uint4* sr = reinterpret_cast<const uint4*>(s_mem);
     for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
+}
+
+// The count kernel: count_read per lane, then (totals requested) bin_candidates.
+template <int NK, int MODE>
+__global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
+    constexpr int W = NK == 1 ? 1 : 2;
+    constexpr int WORDS = ((TS + 1) * W + PEND + 1) * WG;
+    static_assert(WORDS >= WG * CCAP, "the region staging reuses the count tables");
+    __shared__ __attribute__((aligned(16))) uint32_t s_mem[WORDS];
+    __shared__ uint32_t s_bc[WG + 1];
+    auto s_tab = reinterpret_cast<uint32_t(*)[WG]>(s_mem);
+    auto s_pend = reinterpret_cast<uint32_t(*)[WG]>(s_mem + (TS + 1) * W * WG);
+    const uint32_t t = threadIdx.x, w = blockIdx.x;
+    const uint64_t r = (uint64_t)w * WG + t;
+    const bool bin = p.accumulate && p.bin_nb;  // uniform
+    if (bin) {
+        s_bc[t] = 0;
+        __syncthreads();
+    }
+    uint32_t key[TS];
+    uint32_t nc = 0;
+    if (MODE == 1 || r < p.n) nc = count_read<NK, MODE>(p, r, t, s_tab, s_pend, key);
+    if (bin) bin_candidates(p, t, w, nc, key, s_bc, s_mem);
+}
+
+// k_map1 LDS: per wave max(staged codes + bad bits, one pass of the entry list: MAP_P hashes and
+// their owning lanes)
+constexpr uint32_t MAP_P = 384;
+__host__ __device__ inline size_t map1_wave_bytes(uint32_t wc) {
+    const size_t a = sketch_codes_bytes(wc) + sketch_bad_bytes(wc, false);
+    const size_t b = (size_t)MAP_P * 5;
+    return (a > b ? a : b + 15) & ~(size_t)15;
+}
+
+size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
+    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks) + ((size_t)hcap + 1) * WG * 4 +
+           (size_t)(WG + 1) * 4;
+}
+
+// Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
+// the retained hashes go straight from registers to the pair-cooperative wide-table count
+// (wide_chunk), the filter and the candidates, then the binning epilogue. The count tables
+// overlay LDS the hashing no longer needs: the transcript table the raw slots ([slot][WG], this
+// lane's own), the parked list the wave's staged codes (all of the wave's lanes have left the
+// hashing loop before any counts). Reads k_sketch would hand to the slow path are listed for
+// both slow paths (k_sketch_slow, then k_chain_slow). No early exits: pairs gather together and
+// the epilogue has workgroup barriers.
+template <int HCAP, int MB>
+__global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    const uint32_t wc = p.tile_chunks;  // chunks per wave
+    const size_t wave_bytes = map1_wave_bytes(wc);
+    uint2* s_tab = reinterpret_cast<uint2*>(smem);
+    const uint2* s_seed = s_tab + 16;
+    unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
+    uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
+    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_wave + sketch_codes_bytes(wc));
+    uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * wave_bytes);
+    uint32_t* s_bc = s_raw + (HCAP + 1) * WG;
+    const bool bin = cp.accumulate && cp.bin_nb;  // uniform
+    for (uint32_t e = tid; e < 16 + 4; e += WG) {
+        const uint64_t v = p.rolltab[e];
+        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
+    }
+    if (bin) s_bc[tid] = 0;
+    __syncthreads();
+
+    const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
+    const uint32_t nr = r0 < p.n ? (uint32_t)min((uint64_t)64, p.n - r0) : 0u;  // wave-uniform
+    const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
+    const uintptr_t abase = base & ~(uintptr_t)15;
+    const uint64_t delta = base - abase;
+    uint64_t c0 = 0;
+    uint32_t nch = 0;
+    if (nr) {
+        uint64_t s0, l0, sl, ll;
+        read_extent(p.offs, p.fixed_len, r0, s0, l0);
+        read_extent(p.offs, p.fixed_len, r0 + nr - 1, sl, ll);
+        c0 = (s0 + delta) >> 4;
+        const uint64_t c1 = (sl + ll + delta + 15) >> 4;
+        nch = (uint32_t)min((uint64_t)wc, c1 - c0);
+        const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
+        constexpr uint32_t SU = 10;
+        for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
+            uint4 vv[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * 64, nch - 1)];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; ++u) {
+                const uint32_t c = cb + u * 64;
+                const uint4 v = vv[u];
+                const uint32_t cs = c < nch ? c : wc + 1;
+                const uint32_t ta = (v.x >> 1) & 0x03030303u, tb = (v.y >> 1) & 0x03030303u;
+                const uint32_t tc = (v.z >> 1) & 0x03030303u, td = (v.w >> 1) & 0x03030303u;
+                constexpr uint32_t W4 = 0x40100401u;
+                const uint32_t code = __builtin_amdgcn_udot4(ta, W4, 0u, false) |
+                                      (__builtin_amdgcn_udot4(tb, W4, 0u, false) << 8) |
+                                      (__builtin_amdgcn_udot4(tc, W4, 0u, false) << 16) |
+                                      (__builtin_amdgcn_udot4(td, W4, 0u, false) << 24);
+                constexpr uint32_t GTCA = 0x47544341u;
+                const uint32_t x = (__builtin_amdgcn_perm(0u, GTCA, ta) ^ v.x) | (__builtin_amdgcn_perm(0u, GTCA, tb) ^ v.y) |
+                                   (__builtin_amdgcn_perm(0u, GTCA, tc) ^ v.z) | (__builtin_amdgcn_perm(0u, GTCA, td) ^ v.w);
+                s_codes[cs] = code;
+                const uint64_t wbits = __ballot(x != 0);
+                if (lane == 0 && c < nch) s_badw[c >> 6] = wbits;
+            }
+        }
+        if (lane == 0) s_codes[nch] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    const bool live = lane < nr;
+    const uint64_t r = live ? r0 + lane : 0;
+    uint64_t start = 0, len = 0;
+    if (live) read_extent(p.offs, p.fixed_len, r, start, len);
+    const uint64_t q0 = start + delta - c0 * 16;
+    bool slow = live && (len > (uint64_t)LFAST || q0 + len > (uint64_t)nch * 16);
+    uint8_t st = SKQ_READ_OK;
+    if (live && !slow) {
+        // is_valid_sequence (src/data_io.cpp:17-34), as in k_sketch
+        bool bad = false;
+        if (len) {
+            const uint32_t ca = (uint32_t)(q0 >> 4), cz = (uint32_t)((q0 + len - 1) >> 4);
+            for (uint32_t wd = ca >> 6; wd <= (cz >> 6); ++wd) {
+                uint64_t m = s_badw[wd];
+                const uint32_t lo = wd == (ca >> 6) ? (ca & 63) : 0u, hi = wd == (cz >> 6) ? (cz & 63) : 63u;
+                m &= (hi == 63 ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+                bad |= m != 0;
+            }
+            if (bad) {
+                bad = false;
+                const uint8_t* rb = p.reads + start;
+                for (uint64_t q = 0; q < len; ++q) {
+                    const uint8_t ch = rb[q];
+                    bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+                }
+            }
+        }
+        if (bad) st = SKQ_READ_INVALID;
+        else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
+    }
+
+    uint32_t v[HCAP];
+#pragma unroll
+    for (int j = 0; j < HCAP; ++j) v[j] = 0xFFFFFFFFu;
+    uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
+    const bool hashing = live && !slow && st == SKQ_READ_OK;
+    if (hashing) {
+        const uint32_t T = p.threshold;
+        const uint32_t L = (uint32_t)len;
+        const uint32_t k = p.ks[0];
+        auto codes16 = [&](uint32_t q) -> uint32_t {
+            const uint32_t d = q >> 4;
+            return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
+        };
+        uint32_t hlo = 0, hhi = 0;
+        for (uint32_t b = 0; b < k; b += 16) {
+            const uint32_t w = codes16((uint32_t)q0 + b);
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (b + j < k) roll33b(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
+        }
+        uint32_t* raw = s_raw + tid;
+        raw[0] = hlo;
+        uint32_t nraw = hlo <= T ? 1u : 0u;  // src/sketch.cpp:33-35
+        const uint32_t nw = L - k + 1;
+        const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
+        for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
+            const uint32_t win = codes16(qin + w0 - 1);
+            const uint32_t wout = codes16(qout + w0 - 1);
+            const uint32_t jn = nw - w0;
+            uint2 e[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) e[j] = s_tab[((win >> (2 * j)) & 3u) * 4 + ((wout >> (2 * j)) & 3u)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                roll33b(hlo, hhi, e[j]);
+                const bool rec = hlo <= T && (uint32_t)j < jn;
+                raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
+                nraw += rec ? 1u : 0u;
+            }
+        }
+        if (nraw > HCAP) {
+            slow = true;
+        } else {
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
+            bitonic_sort<HCAP>(v);
+            uint32_t* out = p.hashes + r;
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) {
+                const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
+                if (keep) {
+                    out[(uint64_t)(m++) * p.n] = v[j];
+                    keepm |= 1ull << j;
+                }
+            }
+            p.hash_cnt[r] = m;
+        }
+    }
+    if (live) {
+        if (slow) {
+            st = ST_SLOW1;
+            list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
+            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+        } else if (st != SKQ_READ_OK) {
+            p.hash_cnt[r] = 0;
+        }
+        p.status[r] = st;
+        p.pflag[r] = slow ? 1 : 0;  // (a later skq_chain on these results reads it)
+    }
+    // every lane of the wave has left the hashing loop: the staged codes become the parked lists
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- count, entry-parallel: the wave's retained hashes are listed in LDS (hash, owning
+    // lane), in passes of MAP_P; lane pairs take them round-robin (each pair gathers one 32-B
+    // wide entry, the even lane inserts its head tids t0..t2, the odd lane t3..t6) into the
+    // owning read's transcript table with LDS atomics, so the work follows the tids the wave
+    // really has rather than its longest read. Table of read (lane) o: column o of this wave in
+    // the raw region, slot s at s * WG, (tid << 8 | count) or EMPTY; slot TS: overflow flag.
+    const bool act = hashing && !slow;
+    const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
+    const uint32_t incl = wave_incl_scan(m, lane);
+    const uint32_t off = incl - m;
+    const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes
+    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+#pragma unroll
+    for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
+    s_raw[TS * WG + tid] = 0;
+    uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
+    uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
+    uint32_t* colbase = s_raw + wv * 64;
+    const uint32_t* wd = cp.wdir[0];
+    const uint64_t wlen = cp.wdir_len[0];
+    const bool odd = lane & 1u;
+    auto ains = [&](uint32_t x, uint32_t o, bool valid) {
+        if (!valid) return;
+        uint32_t* col = colbase + o;
+        uint32_t sl = Counter<1, WG>::slot_of(x);
+        for (int z = 0; z < TS; ++z) {
+            const uint32_t old = atomicCAS(col + sl * WG, EMPTY, (x << 8) | 1u);
+            if (old == EMPTY) return;
+            if ((old >> 8) == x) {
+                atomicAdd(col + sl * WG, 1u);
+                return;
+            }
+            sl = (sl + 1) & (TS - 1);
+        }
+        atomicOr(col + TS * WG, 1u);  // more than TS distinct transcripts
+    };
+    for (uint32_t pb = 0; pb < M; pb += MAP_P) {  // wave-uniform
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t rank = 0;
+#pragma unroll
+        for (int j = 0; j < HCAP; ++j) {
+            const bool kj = (keepm >> j) & 1ull;
+            const uint32_t e = off + rank;
+            if (kj && e >= pb && e < pb + MAP_P) {
+                s_h[e - pb] = v[j];
+                s_own[e - pb] = (uint8_t)lane;
+            }
+            rank += kj ? 1u : 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t ne = min(M - pb, (uint32_t)MAP_P);
+        constexpr int R = 4;  // rounds of 32 entries in flight together
+        for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
+            uint4 w[R];
+            uint32_t own[R];
+            bool ok[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const uint32_t e = e0 + 32 * u + (lane >> 1);
+                const bool in = e < ne;
+                const uint32_t h = s_h[in ? e : 0];
+                own[u] = s_own[in ? e : 0];
+                ok[u] = in && h < wlen;
+                w[u] = *reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const uint32_t sw = pair_swap(w[u].x);
+                const uint32_t n = ok[u] ? (odd ? sw : w[u].x) : 0u;  // [0x80000000 | offset] when long
+                const uint32_t qb = odd ? 3u : 0u;
+                ains(odd ? w[u].x : w[u].y, own[u], n > qb);
+                ains(odd ? w[u].y : w[u].z, own[u], n > qb + 1);
+                ains(odd ? w[u].z : w[u].w, own[u], n > qb + 2);
+                ains(w[u].w, own[u], odd && n > 6);
+                // lists longer than 7 (rare): the even lane inserts the rest of the list
+                if (__any(!odd && n > 7) && !odd && n > 7) {
+                    const uint32_t lo = n & 0x7FFFFFFFu;
+                    const uint32_t len = cp.lists[lo];
+                    for (uint32_t q = 7; q < len; ++q) ains(cp.lists[lo + 1 + q], own[u], true);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t key[TS];
+    uint32_t nc = 0;
+    if (act) {
+        if (s_raw[TS * WG + tid] == 0) {
+            // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
+            uint32_t ev[TS];
+            uint32_t mx = 0;
+#pragma unroll
+            for (int sl = 0; sl < TS; ++sl) {
+                ev[sl] = s_raw[sl * WG + tid];
+                mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
+            }
+            const double thr = cp.fraction * (double)mx;
+            uint32_t need = 0;
+            if (thr > 0.0) need = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+#pragma unroll
+            for (int sl = 0; sl < TS; ++sl) {
+                const uint32_t cnt = ev[sl] & 0xFFu;
+                key[sl] = (ev[sl] != EMPTY && cnt >= need) ? ((1023u - cnt) << 22) | (ev[sl] >> 8) : ~0u;
+            }
+            bitonic_sort<TS>(key);
+            uint32_t* ct = cp.cand_tid + r;
+            uint32_t* cs = cp.cand_score + r;
+#pragma unroll
+            for (int d = 0; d < TS; ++d) {
+                if (key[d] != ~0u) {
+                    ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
+                    cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                    ++nc;
+                }
+            }
+            cp.cand_cnt[r] = nc;
+        } else {
+            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+            cp.cand_cnt[r] = 0;
+        }
+    } else if (live) {
+        cp.cand_cnt[r] = 0;
+    }
+    // (bin_candidates places entries only after its barriers, when every wave's count tables
+    // are dead)
+    if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
 }
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
@@ -1724,13 +2254,20 @@ int launch_count(const ChainParams& p, void* stream) {
     // k_count3 (32-bit sort keys) unless transcript ids need more than 22 bits; variant 4 forces
     // the wide kernel for A/B timing
     if (use_count3(p)) {
-        switch (p.nk) {
-        case 1: hipLaunchKernelGGL(k_count3<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-        case 2: hipLaunchKernelGGL(k_count3<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-        case 3: hipLaunchKernelGGL(k_count3<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-        case 4: hipLaunchKernelGGL(k_count3<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-        default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-        }
+        const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        auto go = [&](auto mode) {
+            constexpr int M = decltype(mode)::value;
+            switch (p.nk) {
+            case 1: hipLaunchKernelGGL((k_count3<1, M>), grid, dim3(WG), 0, st, p); break;
+            case 2: hipLaunchKernelGGL((k_count3<2, M>), grid, dim3(WG), 0, st, p); break;
+            case 3: hipLaunchKernelGGL((k_count3<3, M>), grid, dim3(WG), 0, st, p); break;
+            case 4: hipLaunchKernelGGL((k_count3<4, M>), grid, dim3(WG), 0, st, p); break;
+            default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, st, p); break;
+            }
+        };
+        if (p.wide == 1) go(std::integral_constant<int, 1>{});
+        else if (p.wide == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 0>{});
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     switch (p.nk) {
@@ -1749,6 +2286,31 @@ int launch_chain_slow(const ChainParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+__global__ void k_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* content, uint64_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint4* c = reinterpret_cast<const uint4*>(content) + j * 4;
+    uint4* d = reinterpret_cast<uint4*>(blk) + (uint64_t)bidx[j] * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = c[q];
+}
+
+// wide entry for key keys[j]: [n, t0..t6] (n <= 7) or [0x80000000 | list offset, t0..t6]
+__global__ void k_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
+                               uint64_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t off = vals[j];
+    const uint32_t len = lists[off];
+    uint32_t e[8];
+    e[0] = len <= 7 ? len : (0x80000000u | off);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) e[q + 1] = (uint32_t)q < len ? lists[off + 1 + q] : 0u;
+    uint4* d = reinterpret_cast<uint4*>(wdir + (uint64_t)keys[j] * 8);
+    d[0] = make_uint4(e[0], e[1], e[2], e[3]);
+    d[1] = make_uint4(e[4], e[5], e[6], e[7]);
+}
+
 __global__ void k_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n) {
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
         dir[keys[j]] = vals[j];
@@ -1758,6 +2320,38 @@ int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals
     if (n == 0) return 0;
     const unsigned grid = (unsigned)std::min<uint64_t>((n + WG - 1) / WG, 4096);
     hipLaunchKernelGGL(k_dir_scatter, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), dir, keys, vals, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* content, uint64_t n, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_blk_scatter, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0,
+                       reinterpret_cast<hipStream_t>(stream), blk, bidx, content, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
+    if (p.n == 0) return 0;
+    const dim3 grid((unsigned)((p.n + WG - 1) / WG));
+    const size_t lds = map1_lds_bytes(p.tile_chunks, p.hcap);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (p.hcap) {
+    case 16:
+        if (cp.variant == 7) hipLaunchKernelGGL((k_map1<16, 4>), grid, dim3(WG), lds, st, p, cp);
+        else hipLaunchKernelGGL((k_map1<16, 8>), grid, dim3(WG), lds, st, p, cp);
+        break;
+    case 32: hipLaunchKernelGGL((k_map1<32, 8>), grid, dim3(WG), lds, st, p, cp); break;
+    default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
+                        uint64_t n, void* stream) {
+    if (n == 0) return 0;
+    const unsigned grid = (unsigned)((n + WG - 1) / WG);
+    hipLaunchKernelGGL(k_wdir_scatter, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), wdir, keys,
+                       vals, lists, n);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -183,7 +183,8 @@ class Index:
         b, n, m = C.c_uint64(), C.c_uint64(), C.c_uint32()
         _check(lib().skq_index_stats(self.h, C.byref(b), C.byref(n), C.byref(m)))
         return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
-                    direct=bool(lib().skq_index_direct(self.h)))
+                    direct=bool(lib().skq_index_direct(self.h)),
+                    probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 4: "block"}[lib().skq_index_direct(self.h)])
 
     def free(self):
         if self.h:

@@ -15,11 +15,20 @@ from skq import synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["direct", "bucket"])
+@pytest.fixture(autouse=True, params=["block", "wide", "wide-split", "dir", "bucket"])
 def probe_mode(request, monkeypatch):
-    """Every test runs with both index probe modes: direct tables probed inside the sketch
-    kernel, and the bucket table probed by k_probe (SKQ_DIRECT_MB=0)."""
-    monkeypatch.setenv("SKQ_DIRECT_MB", "8192" if request.param == "direct" else "0")
+    """Every test runs with each index probe structure: block tables and wide direct tables
+    gathered by the count kernel, 4-B direct tables probed inside the sketch kernel, and the bucket table probed by
+    k_probe (SKQ_DIRECT_MB=0)."""
+    if request.param == "bucket":
+        monkeypatch.setenv("SKQ_DIRECT_MB", "0")
+    elif request.param == "wide-split":  # wide tables through k_sketch + k_count3 (no fused map)
+        monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
+        monkeypatch.setenv("SKQ_PROBE", "wide")
+        monkeypatch.setenv("SKQ_VARIANT", "6")
+    else:
+        monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
+        monkeypatch.setenv("SKQ_PROBE", request.param)
     return request.param
 
 
@@ -91,7 +100,7 @@ def totals_from(ref, n, ntx):
 def test_probe_mode_is_selected(tx300, probe_mode):
     gi, _ = build([21, 31], tx=tx300)
     st = gi.stats()
-    assert st["direct"] == (probe_mode == "direct")
+    assert st["probe"] == probe_mode.split("-")[0]
     assert st["device_bytes"] > 0
 
 
@@ -101,7 +110,7 @@ def tx300():
 
 
 @pytest.mark.parametrize("ks", [[31], [21, 25, 31], [31, 31], [19], [17, 19, 21, 25, 31]])
-@pytest.mark.parametrize("read_len", [100, 150])
+@pytest.mark.parametrize("read_len", [100, 150, 250])
 def test_random_reads_match_oracle(tx300, ks, read_len):
     gi, oi = build(ks, tx=tx300)
     bases, _, _ = synth.reads(tx300, 3000, read_len, seed=read_len + len(ks), err=0.002)
@@ -243,6 +252,60 @@ def test_wide_postings_take_slow_chain_path():
         ref = oi.map_batch(reads, fraction=fraction)
         compare(out, ref, len(reads), 1)
         assert ref["cand_cnt"].max() > 16 or fraction != 0.0
+
+
+def test_list_lengths_around_the_inline_limit():
+    # hand-built index whose lists hold 1..12 transcripts: wide entries keep 7 inline and read
+    # the rest from the postings list; each read stays within 16 distinct transcripts (the
+    # extras of one source transcript come from its own group of 11)
+    rng = np.random.default_rng(5)
+    src = synth.transcriptome(20, seed=15)
+    seqs = [src.seq(t) for t in range(src.ntx)]
+    ntx = 20 + 20 * 11
+    h, t = [], []
+    for tid, s in enumerate(seqs):
+        group = 20 + 11 * tid + np.arange(11)
+        for x in orc.sketch(s, 31):
+            h.append(x)
+            t.append(tid)
+            for extra in rng.choice(group, int(rng.integers(0, 12)), replace=False):
+                h.append(x)
+                t.append(int(extra))
+    pairs = [(np.array(h, np.uint32), np.array(t, np.uint32))]
+    gi, oi = build([31], pairs=pairs, ntx=ntx)
+    assert gi.stats()["max_list"] >= 10
+    bases, _, _ = synth.reads(src, 600, 150, seed=16)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(600)]
+    for fraction in (0.9, 0.0):
+        out = run_gpu(gi, reads, fraction=fraction)
+        ref = oi.map_batch(reads, fraction=fraction)
+        compare(out, ref, len(reads), 1)
+
+
+def test_crowded_blocks():
+    # hand-built index: below each real key, up to 3 extra keys in its 32-key block (ranks 2+ of
+    # a block table take the overflow array), with lists of 1..9 transcripts
+    rng = np.random.default_rng(6)
+    src = synth.transcriptome(30, seed=18)
+    seqs = [src.seq(t) for t in range(src.ntx)]
+    ntx = 60
+    h, t = [], []
+    for tid, s in enumerate(seqs):
+        for x in orc.sketch(s, 31):
+            h.append(x)
+            t.append(tid)
+            low = x & 31
+            for j in rng.choice(low, min(low, int(rng.integers(0, 4))), replace=False) if low else []:
+                for extra in rng.choice(ntx, int(rng.integers(1, 10)), replace=False):
+                    h.append((x & ~31) | int(j))
+                    t.append(int(extra))
+    pairs = [(np.array(h, np.uint32), np.array(t, np.uint32))]
+    gi, oi = build([31], pairs=pairs, ntx=ntx)
+    bases, _, _ = synth.reads(src, 500, 150, seed=19, err=0.01)
+    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(500)]
+    out = run_gpu(gi, reads)
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), 1)
 
 
 def test_index_without_some_k():

@@ -22,6 +22,7 @@ ap.add_argument("--len", type=int, default=150)
 ap.add_argument("--ks", default="31")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--variants", default="0", help="chain kernel variants to A/B (0 = default)")
+ap.add_argument("--pipeline", type=int, default=0, help="also time N batches on two alternating streams")
 a = ap.parse_args()
 ks = [int(x) for x in a.ks.split(",")]
 t0 = time.time()
@@ -69,3 +70,27 @@ for name, v in res.items():
     med = np.median(v, axis=0)
     print("%-10s wall %.3f ms  k_sketch %.3f  k_probe %.3f  k_count %.3f  totals %.3f  -> %.2f G reads/s" % (
         name, med[0], med[1], med[2], med[3], med[4], a.reads / med[0] / 1e6))
+
+if a.pipeline:
+    # two sessions on two streams, alternating batches: batch b's chain overlaps batch b+1's
+    # sketch (steady-state time per batch of a streamed run)
+    s2 = skq.Session(index, a.reads, a.len)
+    st = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    ses = [s, s2]
+    for acc in (True, False):
+        for sx in ses:
+            sx.set_variant(0)
+        best = 1e9
+        for rnd in range(a.rounds + 1):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for b in range(a.pipeline):
+                sx, stx = ses[b % 2], st[b % 2]
+                sx.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len,
+                       stream=C.c_void_p(stx.cuda_stream), accumulate=acc)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t) * 1e3 / a.pipeline
+            if rnd:
+                best = min(best, wall)
+        print("pipelined x%d%s: %.3f ms per batch -> %.2f G reads/s" % (
+            a.pipeline, " +acc" if acc else "", best, a.reads / best / 1e6))
