@@ -148,8 +148,12 @@ def main():
     # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"); an index lookup is priced at
     # the 8 B (key, list offset) it needs, a posting at its 4 B tid
     fused = kt[1][1] == 0  # no k_probe launches: the sketch kernel probed (direct/rank table)
+    # wide tables, one k: skq_map runs ONE kernel (k_map1: sketch + entry gathers + count), timed
+    # as kind 0 with no separate count launches
+    map1 = kt[2][1] == 0 and kt[0][1] > 0
     # the count kernel: k_count3 (32-bit keys, bins the totals) unless ids need > 22 bits
     count_name = "k_count3" if tx.ntx <= (1 << 22) and os.environ.get("SKQ_VARIANT") != "4" else "k_count"
+    b_chain = 4 * P + 4 + 8 * Cn + 4 * Cn  # postings in, candidates + count + binned totals out
     b_kern = {
         # read bases in; retained hashes, per-k counts, status out (+ when fused: one lookup per
         # hash, list offsets and the slow flag out)
@@ -162,8 +166,11 @@ def main():
         # binned candidates in (4 B each), per-transcript sums out (amortised: 16 B x ntx / n)
         "totals": 4 * Cn + 16.0 * tx.ntx / n,
     }
+    if map1:  # the fused kernel: read in, one lookup per hash, postings, hashes + candidates out
+        b_kern = {"k_map1": L + 1 + 4 * nk + 4 * h + 8 * h + b_chain, "totals": b_kern["totals"]}
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
-    avg = {name: ms / cnt for name, (ms, cnt) in zip(("k_sketch", "k_probe", count_name, "totals"), kt) if cnt}
+    names = ("k_map1" if map1 else "k_sketch", "k_probe", count_name, "totals")
+    avg = {name: ms / cnt for name, (ms, cnt) in zip(names, kt) if cnt}
     kname = max(avg, key=avg.get)                       # dominant kernel
     achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
     traffic = None
@@ -206,7 +213,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname]},
-            "path": {"bytes_per_read": b_path, "probe": "fused in k_sketch" if fused else "k_probe",
+            "path": {"bytes_per_read": b_path, "probe": ("k_map1 (sketch + wide-entry gathers + count fused)" if map1 else
+                                                "fused in k_sketch" if fused else "k_probe"),
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
                      "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn},
