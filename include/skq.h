@@ -157,6 +157,29 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
 int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, int to_device,
                        void* stream);
 
+/* ---- FASTQ ingest on the GPU (process_fastq_single_pass's reader, src/main.cpp:113-148) ------
+ * The FASTQ text itself goes to the device: a reader thread pulls the file into pinned staging
+ * buffers (io_threads parallel preads) and copies chunks of about chunk_bytes (0 = 256 MiB) to HBM
+ * on its own stream, two chunks ahead; the GPU splits them into records with the reader's rules
+ * (a line starting with '@' opens a record whose id is the rest of that line; the next three
+ * lines are sequence, '+' and quality, whatever they hold; other lines between records are
+ * skipped) and the batch goes through skq_map. Records are numbered in file order from 0. */
+typedef struct skq_ingest skq_ingest;
+int skq_ingest_open(skq_session* s, const char* path, uint64_t chunk_bytes, int io_threads, skq_ingest** out);
+/* The next batch (at most the session's max_reads records): parse if needed, sketch + chain on
+ * `stream`. Results are the session's, as after skq_map; *n = records in the batch (0 at the end
+ * of the file), numbered from *first. Every record is in the batch: status marks the reads the
+ * reference drops (invalid / shorter than the largest k). */
+int skq_ingest_map(skq_ingest* g, uint32_t threshold, double fraction, int accumulate, void* stream,
+                   uint64_t* n, uint64_t* first);
+uint64_t skq_ingest_records(const skq_ingest* g);
+/* After the last batch: kept[r] = 1 for the record that the reference keeps for its id, the last
+ * one with status SKQ_READ_OK (src/main.cpp:147); kept holds skq_ingest_records() bytes. */
+int skq_ingest_finish(skq_ingest* g, uint8_t* kept);
+/* id of a record (the header line after '@'), pointing into the mapped file */
+int skq_ingest_id(const skq_ingest* g, uint64_t ordinal, const char** id, uint64_t* len);
+int skq_ingest_close(skq_ingest* g);
+
 /* Device memory helpers (for hosts without their own allocator). */
 int skq_malloc(int device, size_t bytes, void** out);
 int skq_free(void* p);

@@ -124,6 +124,9 @@ struct skq_session {
     int variant = 0;
 };
 
+int skq::session_device(const skq_session* s) { return s->idx->device; }
+uint64_t skq::session_max_reads(const skq_session* s) { return s->max_reads; }
+
 namespace {
 
 template <typename T>

@@ -154,6 +154,9 @@ struct ChainParams {
 
 // records the message returned by skq_last_error(); returns code (skq_capi.hip)
 int set_error(int code, const char* msg);
+// session facts for skq_ingest (skq_capi.hip)
+int session_device(const skq_session* s);
+uint64_t session_max_reads(const skq_session* s);
 
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);

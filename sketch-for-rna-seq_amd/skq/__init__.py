@@ -89,6 +89,12 @@ def lib():
             "skq_fastq_records": (u64, [vp]),
             "skq_fastq_id": (i32, [vp, u64, C.POINTER(vp), C.POINTER(u64)]),
             "skq_fastq_close": (i32, [vp]),
+            "skq_ingest_open": (i32, [vp, C.c_char_p, u64, i32, C.POINTER(vp)]),
+            "skq_ingest_map": (i32, [vp, u32, dbl, i32, vp, C.POINTER(u64), C.POINTER(u64)]),
+            "skq_ingest_records": (u64, [vp]),
+            "skq_ingest_finish": (i32, [vp, vp]),
+            "skq_ingest_id": (i32, [vp, u64, C.POINTER(vp), C.POINTER(u64)]),
+            "skq_ingest_close": (i32, [vp]),
             "skq_legacy_index_write": (i32, [C.c_char_p, u32, vp, vp, vp]),
             "skq_legacy_index_read": (i32, [C.c_char_p, C.POINTER(vp)]),
             "skq_legacy_index_view": (i32, [vp, C.POINTER(u32), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]),
@@ -391,6 +397,43 @@ class FastqReader:
     def close(self):
         if self.h:
             lib().skq_fastq_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+
+class Ingest:
+    """FASTQ parsed on the GPU (skq_ingest_*): batches of records mapped through `session`."""
+
+    def __init__(self, session, path, chunk_bytes=0, io_threads=4):
+        self.session = session  # keeps the session alive
+        self.h = C.c_void_p()
+        _check(lib().skq_ingest_open(session.h, str(path).encode(), chunk_bytes, io_threads, C.byref(self.h)))
+
+    def map(self, thr=None, fraction=0.9, accumulate=True, stream=None):
+        """(first ordinal, n) of the next batch, now in the session's results; n == 0 at the end."""
+        n, first = C.c_uint64(), C.c_uint64()
+        _check(lib().skq_ingest_map(self.h, threshold() if thr is None else thr, fraction, int(accumulate),
+                                    stream, C.byref(n), C.byref(first)))
+        return first.value, n.value
+
+    def records(self):
+        return lib().skq_ingest_records(self.h)
+
+    def finish(self):
+        kept = np.zeros(self.records(), np.uint8)
+        _check(lib().skq_ingest_finish(self.h, _p(kept)))
+        return kept
+
+    def id(self, ordinal):
+        p, n = C.c_void_p(), C.c_uint64()
+        _check(lib().skq_ingest_id(self.h, ordinal, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value)
+
+    def close(self):
+        if self.h:
+            lib().skq_ingest_close(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):
