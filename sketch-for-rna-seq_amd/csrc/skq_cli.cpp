@@ -3,9 +3,9 @@
 //   -o index <reference.fasta> <index_output>
 //   -o quant <index_file> <reads.fastq> <output.csv>     (the default mode)
 // index: FASTA -> per-transcript FracMinHash sketches -> inverted index -> the legacy file.
-// quant: legacy file -> device index; FASTQ streamed in batches through skq_map (sketch +
-//        sparse chain on the GPU); the last valid record of every read id kept; EM (20 rounds,
-//        0.01) -> assignment -> CSV. As in the reference, quant uses the index's k list.
+// quant: legacy file -> device index; FASTQ streamed to the GPU, parsed there and mapped in
+//        batches (skq_ingest: sketch + sparse chain); the last valid record of every read id
+//        kept; EM (20 rounds, 0.01) -> assignment -> CSV. As in the reference, quant uses the index's k list.
 #include <getopt.h>
 
 #include <algorithm>
@@ -40,7 +40,8 @@ void print_help(const std::string& prog) {
               << "  " << prog << " -o index <reference_genome.fasta> <index_output>\n\n"
               << "Quant mode usage:\n"
               << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
-              << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_BATCH (reads per batch).\n";
+              << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_BATCH (reads per batch),\n"
+              << "             SKQ_CHUNK_MB (FASTQ bytes per device chunk, default 256).\n";
 }
 
 const float kSketchSize = 0.05f;  // src/main.cpp:43
@@ -69,24 +70,6 @@ void build_and_save_index(const std::string& fasta, const std::string& out, cons
     skq_seqs_free(tx);
 }
 
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~DevBuf() {
-        if (p) skq_free(p);
-    }
-    void put(const void* src, size_t n) {
-        if (n > cap) {
-            if (p) skq_free(p);
-            p = nullptr;
-            cap = 0;
-            check(skq_malloc(device(), std::max<size_t>(n, 16), &p), "device allocation");
-            cap = std::max<size_t>(n, 16);
-        }
-        if (n) check(skq_memcpy_h2d(p, src, n, nullptr), "upload");
-    }
-};
-
 void quantification(const std::string& index_path, const std::string& reads_path, const std::string& out_path) {
     skq_legacy_index* lx = nullptr;
     check(skq_legacy_index_read(index_path.c_str(), &lx), "load_index");
@@ -106,28 +89,21 @@ void quantification(const std::string& index_path, const std::string& reads_path
     if (const char* e = std::getenv("SKQ_BATCH")) batch = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     skq_session* s = nullptr;
     check(skq_session_create(ix, batch, 256, &s), "session");
-    skq_fastq* q = nullptr;
-    check(skq_fastq_open(reads_path.c_str(), &q), "FASTQ");
+    // FASTQ parsed on the GPU: the reader thread streams the file to HBM (skq_ingest)
+    skq_ingest* q = nullptr;
+    uint64_t chunk = 0;
+    if (const char* e = std::getenv("SKQ_CHUNK_MB")) chunk = std::strtoull(e, nullptr, 10) << 20;
+    check(skq_ingest_open(s, reads_path.c_str(), chunk, 8, &q), "FASTQ");
 
     // per record: status and candidates, kept until duplicates are resolved
     std::vector<uint8_t> status;
     std::vector<uint64_t> rec_offs{0};
     std::vector<uint32_t> ctid, cscore;
-    DevBuf d_bytes, d_offs;
     const uint32_t thr = skq_threshold((double)kSketchSize);
     for (;;) {
         uint64_t n = 0, first = 0;
-        const uint8_t* bytes = nullptr;
-        const uint64_t* offs = nullptr;
-        check(skq_fastq_next(q, batch, &n, &bytes, &offs, &first), "FASTQ read");
+        check(skq_ingest_map(q, thr, 0.9, 0, nullptr, &n, &first), "sketch + sparse chain");
         if (n == 0) break;
-        uint64_t maxlen = 0;
-        for (uint64_t r = 0; r < n; ++r) maxlen = std::max(maxlen, offs[r + 1] - offs[r]);
-        d_bytes.put(bytes, offs[n]);
-        d_offs.put(offs, (n + 1) * 8);
-        check(skq_map(s, static_cast<const uint8_t*>(d_bytes.p), static_cast<const uint64_t*>(d_offs.p), 0, n,
-                      (uint32_t)std::min<uint64_t>(maxlen, 0xFFFFFFFFu), thr, 0.9, 0, nullptr),
-              "sketch + sparse chain");
         uint64_t nh = 0, nc = 0;
         check(skq_session_export(s, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &nh, &nc), "export");
         const size_t s0 = status.size(), c0 = ctid.size();
@@ -139,8 +115,9 @@ void quantification(const std::string& index_path, const std::string& reads_path
                                  cscore.data() + c0, &nh, &nc),
               "export");
         for (uint64_t r = 0; r < n; ++r) rec_offs.push_back(c0 + co[r + 1]);
-        check(skq_fastq_mark(q, first, n, status.data() + s0), "FASTQ mark");
     }
+    std::vector<uint8_t> kept(status.size());
+    check(skq_ingest_finish(q, kept.data()), "duplicate reads");
     std::cout << "Loading read completed" << std::endl;
     std::cout << "Sparse chaining completed" << std::endl;
 
@@ -149,7 +126,7 @@ void quantification(const std::string& index_path, const std::string& reads_path
     std::vector<uint32_t> t2, s2;
     const uint64_t nrec = status.size();
     for (uint64_t r = 0; r < nrec; ++r) {
-        if ((status[r] & SKQ_STATUS_MASK) != SKQ_READ_OK || !skq_fastq_kept(q, r)) continue;
+        if (!kept[r]) continue;  // status OK and the last such record of its id
         t2.insert(t2.end(), ctid.begin() + (ptrdiff_t)rec_offs[r], ctid.begin() + (ptrdiff_t)rec_offs[r + 1]);
         s2.insert(s2.end(), cscore.begin() + (ptrdiff_t)rec_offs[r], cscore.begin() + (ptrdiff_t)rec_offs[r + 1]);
         offs.push_back(t2.size());
@@ -164,7 +141,7 @@ void quantification(const std::string& index_path, const std::string& reads_path
     std::cout << "Read assignment completed" << std::endl;
     check(skq_csv_write(out_path.c_str(), tx, counts.data(), assigned.data(), pi.data()), "output_to_csv");
     std::cout << "Output written to " << out_path << std::endl;
-    skq_fastq_close(q);
+    skq_ingest_close(q);
     skq_session_free(s);
     skq_index_free(ix);
     skq_legacy_index_free(lx);

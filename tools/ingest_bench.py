@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""End-to-end FASTQ throughput of the GPU ingest (skq_ingest_*): file in the page cache ->
+records parsed on the device -> sketch + chain -> (optionally) per-read candidates on the host.
+
+usage: tools/ingest_bench.py [--reads N] [--chunk MiB] [--io-threads T] [--export]
+
+Writes a synthetic FASTQ (cfg3 shape: 150 bp reads of the 200k-transcript synthetic
+transcriptome, headers like '@read000000001 tx=...') to --path, reads it once to warm the page
+cache, then times skq_ingest_map over the whole file. Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sketch-for-rna-seq_amd"))
+import torch  # noqa: E402,F401  (one HIP runtime per process, as in bench.py)
+import skq  # noqa: E402
+from skq import synth  # noqa: E402
+
+
+def write_fastq(path, bases, n, L, block=1_000_000):
+    """Fixed-layout records: '@read%09d tx=synthetic\\n' + seq + '\\n+\\n' + qual + '\\n'."""
+    head = len(b"@read%09d tx=synthetic\n" % 0)
+    rec = head + L + 1 + 2 + L + 1
+    with open(path, "wb") as f:
+        for a in range(0, n, block):
+            m = min(block, n - a)
+            buf = np.empty((m, rec), np.uint8)
+            ids = np.char.encode(np.char.mod("@read%09d tx=synthetic\n", np.arange(a, a + m)), "ascii")
+            buf[:, :head] = np.frombuffer(b"".join(ids), np.uint8).reshape(m, head)
+            buf[:, head:head + L] = bases[a * L:(a + m) * L].reshape(m, L)
+            buf[:, head + L:head + L + 3] = np.frombuffer(b"\n+\n", np.uint8)
+            buf[:, head + L + 3:head + 2 * L + 3] = ord("I")
+            buf[:, -1] = ord("\n")
+            f.write(buf.tobytes())
+    return n * rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--ntx", type=int, default=200_000)
+    ap.add_argument("--chunk", type=int, default=256, help="MiB per chunk")
+    ap.add_argument("--io-threads", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=4_000_000, help="session max_reads")
+    ap.add_argument("--export", action="store_true", help="copy every batch's candidates to the host")
+    ap.add_argument("--path", default="/tmp/skq_ingest_bench.fq")
+    args = ap.parse_args()
+
+    t0 = time.time()
+    tx = synth.transcriptome(args.ntx, seed=1)
+    tables = skq.build_tables(tx.seqs, tx.offs, [31], nthreads=16)
+    index = skq.Index([31], tx.ntx, tables, device=0)
+    bases, _, _ = synth.reads(tx, args.reads, 150, seed=1000, err=0.001)
+    size = write_fastq(args.path, bases, args.reads, 150)
+    with open(args.path, "rb") as f:  # page cache
+        while f.read(1 << 28):
+            pass
+    sess = skq.Session(index, args.batch, 256)
+    print("[ingest] setup %.1fs, %.2f GB FASTQ" % (time.time() - t0, size / 1e9), file=sys.stderr, flush=True)
+
+    def run():
+        g = skq.Ingest(sess, args.path, chunk_bytes=args.chunk << 20, io_threads=args.io_threads)
+        tot = 0
+        ncand = 0
+        while True:
+            _, n = g.map(accumulate=True)
+            if n == 0:
+                break
+            tot += n
+            if args.export:
+                ncand += len(sess.export()["cand_tid"])
+        sess.check()
+        kept = g.finish()
+        g.close()
+        return tot, int(kept.sum()), ncand
+
+    run()  # warm-up (allocations, code objects)
+    sess.reset_totals()
+    ts = time.perf_counter()
+    n, kept, ncand = run()
+    dt = time.perf_counter() - ts
+    res = {"what": "GPU FASTQ ingest end to end (page cache -> parsed on device -> sketch + chain%s)"
+                   % (" -> candidates on host" if args.export else ""),
+           "reads": n, "kept": kept, "seconds": dt, "reads_per_s": n / dt, "fastq_GB_per_s": size / dt / 1e9,
+           "chunk_MiB": args.chunk, "io_threads": args.io_threads, "batch": args.batch,
+           "candidates_exported": ncand if args.export else None}
+    print(json.dumps(res), flush=True)
+    os.unlink(args.path)
+
+
+if __name__ == "__main__":
+    main()
