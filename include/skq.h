@@ -195,6 +195,9 @@ int skq_stream_sync(void* stream);
 int skq_session_enable_timing(skq_session* s, int enable);
 /* Development A/B switch for the chain kernel (0 = default). Not needed by users. */
 int skq_session_set_variant(skq_session* s, int variant);
+/* Development: device buffer of 8 uint64 per wave of the fused map kernel that receives the
+ * wave's phase clocks (s_memtime); NULL turns it off. Not needed by users. */
+int skq_session_set_stamps(skq_session* s, void* d_stamps);
 int skq_session_kernel_time(skq_session* s, int kind, double* total_ms, uint64_t* launches);
 /* Reads of the last batch that took the slow sketch / slow chain path (synchronous). */
 int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chain_slow);

@@ -122,6 +122,7 @@ struct skq_session {
     bool timing = false;
     std::vector<TimedLaunch> timed;
     int variant = 0;
+    uint64_t* stamps = nullptr;  // development: k_map1 phase clocks (skq_session_set_stamps)
 };
 
 int skq::session_device(const skq_session* s) { return s->idx->device; }
@@ -795,6 +796,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
         }
     }
     p.variant = s->variant;
+    p.stamps = s->stamps;
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
     p.bin_nb = s->bin_nb;
@@ -840,7 +842,7 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
 static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,
                         uint32_t threshold) {
     const skq_index* ix = s->idx;
-    if (ix->mode != 3 || ix->nk != 1) return false;
+    if ((ix->mode != 3 && ix->mode != 4) || ix->nk != 1) return false;
     if (s->variant == 1 || s->variant == 2 || s->variant == 4 || s->variant == 6) return false;
     if (!d_offs) max_len = fixed_len;
     const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
@@ -859,6 +861,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         return rc;
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (s->variant == 12) cp.slow_totals = 0;  // development A/B: totals binned by k_bin afterwards
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
     hipEvent_t t0{};
     record(s, 0, &t0, st);
@@ -1078,6 +1081,14 @@ int skq_stream_sync(void* stream) {
 int skq_session_set_variant(skq_session* s, int variant) {
     if (!s) return fail(-1, "null session");
     s->variant = variant;
+    return 0;
+}
+
+// Development hook (tools/kbench.py --stamps): a device buffer of 8 u64 per wave of k_map1 that
+// receives the wave's phase clocks (s_memtime); null turns it off.
+int skq_session_set_stamps(skq_session* s, void* d_stamps) {
+    if (!s) return fail(-1, "null session");
+    s->stamps = static_cast<uint64_t*>(d_stamps);
     return 0;
 }
 

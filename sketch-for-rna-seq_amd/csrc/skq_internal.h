@@ -137,6 +137,7 @@ struct ChainParams {
     uint32_t* bin_region;
     int slow_totals;
     int variant;               // development A/B switch (0 = default)
+    uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
     // wide direct tables (DESIGN.md "Index"): entry h of k slot i is 8 words at wdir[i] + 8h,
     // [n, t0..t6] for lists of n <= 7 transcripts, [0x80000000 | list offset, t0..t6] for longer
     // ones (the rest at lists[offset + 8..]), n = 0 for no key; h >= wdir_len[i] is a miss.

@@ -1513,9 +1513,16 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
 // k_bin does, straight from registers: counts per transcript bucket in LDS (s_bc, zeroed before),
 // one wave scans them (hdr), entries are placed in LDS (s_mem: >= WG * CCAP words no longer in
 // use) and the region leaves in coalesced 16-B stores. Every thread of the workgroup calls it.
+// (ZERO: s_bc overlays LDS the waves may still be using, so it is zeroed here, between barriers)
+template <bool ZERO = false>
 __device__ __forceinline__ void bin_candidates(const ChainParams& p, uint32_t t, uint32_t w, uint32_t nc,
                                                const uint32_t (&key)[TS], uint32_t* s_bc, uint32_t* s_mem) {
     const uint32_t bits = p.bin_bits, nb = p.bin_nb, nW = gridDim.x;
+    if (ZERO) {
+        __syncthreads();
+        if (t <= (uint32_t)WG) s_bc[t] = 0;
+        __syncthreads();
+    }
 #pragma unroll
     for (int d = 0; d < TS; ++d)
         if ((uint32_t)d < nc) atomicAdd(&s_bc[(key[d] & 0x3FFFFFu) >> bits], 1u);
@@ -1581,16 +1588,20 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
 
 // k_map1 LDS: per wave max(staged codes + bad bits, one pass of the entry list: MAP_P hashes and
 // their owning lanes)
+// (the per-chunk bad bits sit in row 0 of the wave's raw columns, dead until hashing starts; the
+// binning counts in wave 0's region, dead once every wave has counted; HCAP + 1 raw rows, the
+// last one the sink of windows past the capacity)
 constexpr uint32_t MAP_P = 384;
 __host__ __device__ inline size_t map1_wave_bytes(uint32_t wc) {
-    const size_t a = sketch_codes_bytes(wc) + sketch_bad_bytes(wc, false);
-    const size_t b = (size_t)MAP_P * 5;
-    return (a > b ? a : b + 15) & ~(size_t)15;
+    const size_t a = sketch_codes_bytes(wc);
+    const size_t b = (size_t)MAP_P * 5 + 64 * 4;  // the list, then the per-read overflow flags
+    const size_t c = (size_t)(WG + 1) * 4;
+    const size_t m = a > b ? a : b;
+    return ((m > c ? m : c) + 15) & ~(size_t)15;
 }
 
 size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
-    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks) + ((size_t)hcap + 1) * WG * 4 +
-           (size_t)(WG + 1) * 4;
+    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks) + ((size_t)hcap + 1) * WG * 4;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -1601,26 +1612,34 @@ size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
 // hashing loop before any counts). Reads k_sketch would hand to the slow path are listed for
 // both slow paths (k_sketch_slow, then k_chain_slow). No early exits: pairs gather together and
 // the epilogue has workgroup barriers.
-template <int HCAP, int MB>
+// development phase clocks (ChainParams::stamps): 8 u64 per wave, written by lane 0
+#define MAP1_STAMP(i)                                                                           \
+    do {                                                                                        \
+        if (cp.stamps && lane == 0)                                                             \
+            cp.stamps[((uint64_t)blockIdx.x * (WG / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
+template <int HCAP, int MB, bool BLK>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
+    static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const uint32_t lane = tid & 63, wv = tid >> 6;
+    MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
     const size_t wave_bytes = map1_wave_bytes(wc);
     uint2* s_tab = reinterpret_cast<uint2*>(smem);
     const uint2* s_seed = s_tab + 16;
     unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
-    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_wave + sketch_codes_bytes(wc));
     uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * wave_bytes);
-    uint32_t* s_bc = s_raw + (HCAP + 1) * WG;
-    const bool bin = cp.accumulate && cp.bin_nb;  // uniform
+    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + wv * 64);  // (row 0 of the wave's columns)
+    uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1));
+    const bool bin = cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
     for (uint32_t e = tid; e < 16 + 4; e += WG) {
         const uint64_t v = p.rolltab[e];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
     }
-    if (bin) s_bc[tid] = 0;
     __syncthreads();
 
     const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
@@ -1668,6 +1687,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    MAP1_STAMP(1);
 
     const bool live = lane < nr;
     const uint64_t r = live ? r0 + lane : 0;
@@ -1704,7 +1724,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
     for (int j = 0; j < HCAP; ++j) v[j] = 0xFFFFFFFFu;
     uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
-    const bool hashing = live && !slow && st == SKQ_READ_OK;
+    // development timing variants (tools/kbench.py; results not valid): 8 skips the count
+    // phase, 9 gathers the entries without inserting them, 10 skips the hashing
+    const int var = cp.variant;
+    const bool hashing = live && !slow && st == SKQ_READ_OK && var != 10;
     if (hashing) {
         const uint32_t T = p.threshold;
         const uint32_t L = (uint32_t)len;
@@ -1770,6 +1793,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         p.status[r] = st;
         p.pflag[r] = slow ? 1 : 0;  // (a later skq_chain on these results reads it)
     }
+    MAP1_STAMP(2);
     // every lane of the wave has left the hashing loop: the staged codes become the parked lists
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1785,52 +1809,142 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
     const uint32_t incl = wave_incl_scan(m, lane);
     const uint32_t off = incl - m;
-    const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes
+    const uint32_t M = var == 8 ? 0u : __shfl(incl, 63, 64);  // the wave's retained hashes
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
-    s_raw[TS * WG + tid] = 0;
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 5);  // per read: > TS transcripts
+    s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
     uint32_t* colbase = s_raw + wv * 64;
     const uint32_t* wd = cp.wdir[0];
     const uint64_t wlen = cp.wdir_len[0];
     const bool odd = lane & 1u;
-    auto ains = [&](uint32_t x, uint32_t o, bool valid) {
-        if (!valid) return;
-        uint32_t* col = colbase + o;
+    // slot sl of read (lane) o sits in column (o + sl) & 63 of row sl: the slots of one read
+    // fall in distinct LDS banks (the lane pairs of one round mostly insert into the same read)
+    // an insert whose home slot holds another tid probes on from the next slot (rare: not unrolled)
+    auto ains_probe = [&](uint32_t x, uint32_t o) {
         uint32_t sl = Counter<1, WG>::slot_of(x);
-        for (int z = 0; z < TS; ++z) {
-            const uint32_t old = atomicCAS(col + sl * WG, EMPTY, (x << 8) | 1u);
+#pragma unroll 1
+        for (int z = 1; z < TS; ++z) {
+            sl = (sl + 1) & (TS - 1);
+            uint32_t* a = colbase + sl * WG + ((o + sl) & 63u);
+            const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | 1u);
             if (old == EMPTY) return;
             if ((old >> 8) == x) {
-                atomicAdd(col + sl * WG, 1u);
+                atomicAdd(a, 1u);
                 return;
             }
-            sl = (sl + 1) & (TS - 1);
         }
-        atomicOr(col + TS * WG, 1u);  // more than TS distinct transcripts
+        atomicOr(s_flag + o, 1u);  // more than TS distinct transcripts
     };
-    for (uint32_t pb = 0; pb < M; pb += MAP_P) {  // wave-uniform
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto ains = [&](uint32_t x, uint32_t o) {
+        const uint32_t sl = Counter<1, WG>::slot_of(x);
+        uint32_t* a = colbase + sl * WG + ((o + sl) & 63u);
+        const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | 1u);
+        if (old == EMPTY) return;
+        if ((old >> 8) == x) atomicAdd(a, 1u);
+        else ains_probe(x, o);
+    };
+    // the first pass's list, straight from the sorted registers (v dies here)
+    {
         uint32_t rank = 0;
 #pragma unroll
         for (int j = 0; j < HCAP; ++j) {
             const bool kj = (keepm >> j) & 1ull;
             const uint32_t e = off + rank;
-            if (kj && e >= pb && e < pb + MAP_P) {
-                s_h[e - pb] = v[j];
-                s_own[e - pb] = (uint8_t)lane;
+            if (kj && e < MAP_P) {
+                s_h[e] = v[j];
+                s_own[e] = (uint8_t)lane;
             }
             rank += kj ? 1u : 0u;
+        }
+    }
+    for (uint32_t pb = 0; pb < M; pb += MAP_P) {  // wave-uniform
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (pb) {  // (rare: more than MAP_P hashes in the wave) this lane's hashes, as written above
+#pragma unroll 1
+            for (uint32_t d = 0; d < m; ++d) {
+                const uint32_t e = off + d;
+                if (e >= pb && e < pb + MAP_P) {
+                    s_h[e - pb] = p.hashes[(uint64_t)d * p.n + r];
+                    s_own[e - pb] = (uint8_t)lane;
+                }
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t ne = min(M - pb, (uint32_t)MAP_P);
-        constexpr int R = 4;  // rounds of 32 entries in flight together
+        constexpr int R = MB;  // rounds of 32 entries in flight together
+        if constexpr (BLK) {
+            // block tables (DESIGN.md "Index"): one 64-B block per hash, the even lane loading
+            // words 0-7 (bitmap, overflow base, entry A's meta and t0..t4), the odd lane words
+            // 8-15 (A's t5, entry B); four swaps give each lane what its half of the inserts
+            // needs (even: t0..t2 of the key's entry, odd: t3..t5)
+            for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
+                uint4 b0[R], b1[R];
+                uint32_t own[R], hh[R];
+                bool ok[R];
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    const uint32_t e = e0 + 32 * u + (lane >> 1);
+                    const bool in = e < ne;
+                    hh[u] = s_h[in ? e : 0];
+                    own[u] = s_own[in ? e : 0];
+                    ok[u] = in && (hh[u] >> 5) < wlen;
+                    const uint4* bp =
+                        reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)(hh[u] >> 5) * 16 : 0ull) + (odd ? 8u : 0u));
+                    b0[u] = bp[0];
+                    b1[u] = bp[1];
+                }
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    const uint32_t r1 = pair_swap(odd ? b0[u].y : b0[u].x);  // even: B.meta, odd: bitmap
+                    const uint32_t r2 = pair_swap(odd ? b0[u].z : b0[u].z);  // even: B.t0, odd: A.meta
+                    const uint32_t r3 = pair_swap(odd ? b0[u].w : b1[u].z);  // even: B.t1, odd: A.t3
+                    const uint32_t r4 = pair_swap(odd ? b1[u].x : b1[u].w);  // even: B.t2, odd: A.t4
+                    const uint32_t bm = odd ? r1 : b0[u].x, bit = hh[u] & 31u;
+                    const bool hit = ok[u] && ((bm >> bit) & 1u);
+                    const uint32_t rank = __builtin_popcount(bm & ((1u << bit) - 1u));
+                    const bool a = rank == 0;
+                    const uint32_t meta = a ? (odd ? r2 : b0[u].z) : (odd ? b0[u].y : r1);
+                    const uint32_t x0 = a ? (odd ? r3 : b0[u].w) : (odd ? b1[u].y : r2);
+                    const uint32_t x1 = a ? (odd ? r4 : b1[u].x) : (odd ? b1[u].z : r3);
+                    const uint32_t x2 = a ? (odd ? b0[u].x : b1[u].y) : (odd ? b1[u].w : r4);
+                    const bool inl = hit && rank < 2;
+                    const uint32_t n = inl ? ((meta & 0x80000000u) ? 6u : meta) : 0u;
+                    const uint32_t qb = odd ? 3u : 0u;
+                    const uint32_t xs[3] = {x0, x1, x2};
+                    uint32_t olds[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+                        olds[q] = n > qb + q ? atomicCAS(colbase + sl * WG + ((own[u] + sl) & 63u), EMPTY, (xs[q] << 8) | 1u)
+                                             : EMPTY;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const uint32_t x = xs[q], sl = Counter<1, WG>::slot_of(x), o = olds[q];
+                        if (o == EMPTY) continue;
+                        if ((o >> 8) == x) atomicAdd(colbase + sl * WG + ((own[u] + sl) & 63u), 1u);
+                        else ains_probe(x, own[u]);
+                    }
+                    // 3rd+ keys of a block (list from the overflow array) and lists longer than
+                    // 6 (the rest of the list): rare, the even lane, one at a time
+                    const bool tail = !odd && hit && (rank >= 2 || (meta & 0x80000000u));
+                    if (__any(tail) && tail) {
+                        const uint32_t lo = rank >= 2 ? cp.wovf[0][b0[u].y + rank - 2] : (meta & 0x7FFFFFFFu);
+                        const uint32_t len = cp.lists[lo];
+                        for (uint32_t q = rank >= 2 ? 0u : 6u; q < len; ++q) ains(cp.lists[lo + 1 + q], own[u]);
+                    }
+                }
+            }
+            continue;
+        }
         for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
             uint4 w[R];
             uint32_t own[R];
@@ -1844,20 +1958,50 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 ok[u] = in && h < wlen;
                 w[u] = *reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
             }
+            if (var == 9) {
+                uint32_t dz = 0;
+#pragma unroll
+                for (int u = 0; u < R; ++u) dz ^= ok[u] ? (w[u].x ^ w[u].y ^ w[u].z ^ w[u].w) + own[u] : 0u;
+                if (dz == 0x9E3779B9u) atomicOr(s_flag + lane, 1u);
+                continue;
+            }
+            // the inserts of each entry: the four first attempts (a CAS at each tid's home slot)
+            // are issued before any result is looked at, one LDS round trip; a tid already there
+            // gets a non-returning add, and only a slot held by another tid sends the insert on
+            // to the probing loop
 #pragma unroll
             for (int u = 0; u < R; ++u) {
                 const uint32_t sw = pair_swap(w[u].x);
                 const uint32_t n = ok[u] ? (odd ? sw : w[u].x) : 0u;  // [0x80000000 | offset] when long
                 const uint32_t qb = odd ? 3u : 0u;
-                ains(odd ? w[u].x : w[u].y, own[u], n > qb);
-                ains(odd ? w[u].y : w[u].z, own[u], n > qb + 1);
-                ains(odd ? w[u].z : w[u].w, own[u], n > qb + 2);
-                ains(w[u].w, own[u], odd && n > 6);
+                uint32_t xs[4], olds[4];
+                bool vs[4];
+                xs[0] = odd ? w[u].x : w[u].y;
+                xs[1] = odd ? w[u].y : w[u].z;
+                xs[2] = odd ? w[u].z : w[u].w;
+                xs[3] = w[u].w;
+                vs[0] = n > qb;
+                vs[1] = n > qb + 1;
+                vs[2] = n > qb + 2;
+                vs[3] = odd && n > 6;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+                    olds[q] = vs[q] ? atomicCAS(colbase + sl * WG + ((own[u] + sl) & 63u), EMPTY, (xs[q] << 8) | 1u)
+                                    : EMPTY;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t x = xs[q], sl = Counter<1, WG>::slot_of(x), o = olds[q];
+                    if (o == EMPTY) continue;
+                    if ((o >> 8) == x) atomicAdd(colbase + sl * WG + ((own[u] + sl) & 63u), 1u);
+                    else ains_probe(x, own[u]);
+                }
                 // lists longer than 7 (rare): the even lane inserts the rest of the list
                 if (__any(!odd && n > 7) && !odd && n > 7) {
                     const uint32_t lo = n & 0x7FFFFFFFu;
                     const uint32_t len = cp.lists[lo];
-                    for (uint32_t q = 7; q < len; ++q) ains(cp.lists[lo + 1 + q], own[u], true);
+                    for (uint32_t q = 7; q < len; ++q) ains(cp.lists[lo + 1 + q], own[u]);
                 }
             }
         }
@@ -1865,16 +2009,17 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    MAP1_STAMP(3);
     uint32_t key[TS];
     uint32_t nc = 0;
     if (act) {
-        if (s_raw[TS * WG + tid] == 0) {
+        if (s_flag[lane] == 0) {
             // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
             uint32_t ev[TS];
             uint32_t mx = 0;
 #pragma unroll
             for (int sl = 0; sl < TS; ++sl) {
-                ev[sl] = s_raw[sl * WG + tid];
+                ev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
                 mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
             }
             const double thr = cp.fraction * (double)mx;
@@ -1904,9 +2049,11 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     } else if (live) {
         cp.cand_cnt[r] = 0;
     }
+    MAP1_STAMP(4);
     // (bin_candidates places entries only after its barriers, when every wave's count tables
     // are dead)
-    if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
+    if (bin) bin_candidates<true>(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
+    MAP1_STAMP(5);
 }
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
@@ -2337,10 +2484,15 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (p.hcap) {
     case 16:
-        if (cp.variant == 7) hipLaunchKernelGGL((k_map1<16, 4>), grid, dim3(WG), lds, st, p, cp);
-        else hipLaunchKernelGGL((k_map1<16, 8>), grid, dim3(WG), lds, st, p, cp);
+        // (MB: gather rounds in flight; variant 11 = 8, a development A/B)
+        if (cp.wide == 2) hipLaunchKernelGGL((k_map1<16, 4, true>), grid, dim3(WG), lds, st, p, cp);
+        else if (cp.variant == 11) hipLaunchKernelGGL((k_map1<16, 8, false>), grid, dim3(WG), lds, st, p, cp);
+        else hipLaunchKernelGGL((k_map1<16, 4, false>), grid, dim3(WG), lds, st, p, cp);
         break;
-    case 32: hipLaunchKernelGGL((k_map1<32, 8>), grid, dim3(WG), lds, st, p, cp); break;
+    case 32:
+        if (cp.wide == 2) hipLaunchKernelGGL((k_map1<32, 4, true>), grid, dim3(WG), lds, st, p, cp);
+        else hipLaunchKernelGGL((k_map1<32, 4, false>), grid, dim3(WG), lds, st, p, cp);
+        break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -23,6 +23,8 @@ ap.add_argument("--ks", default="31")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--variants", default="0", help="chain kernel variants to A/B (0 = default)")
 ap.add_argument("--pipeline", type=int, default=0, help="also time N batches on two alternating streams")
+ap.add_argument("--stamps", action="store_true", help="k_map1 per-wave phase clocks of one launch")
+ap.add_argument("--pipe-variant", type=int, default=0, help="variant the pipelined batches use")
 a = ap.parse_args()
 ks = [int(x) for x in a.ks.split(",")]
 t0 = time.time()
@@ -79,7 +81,7 @@ if a.pipeline:
     ses = [s, s2]
     for acc in (True, False):
         for sx in ses:
-            sx.set_variant(0)
+            sx.set_variant(a.pipe_variant)
         best = 1e9
         for rnd in range(a.rounds + 1):
             torch.cuda.synchronize()
@@ -94,3 +96,27 @@ if a.pipeline:
                 best = min(best, wall)
         print("pipelined x%d%s: %.3f ms per batch -> %.2f G reads/s" % (
             a.pipeline, " +acc" if acc else "", best, a.reads / best / 1e6))
+
+if a.stamps:
+    nw = (a.reads + 255) // 256 * 4
+    for v in [int(x) for x in a.variants.split(",")]:
+        buf = torch.zeros(nw * 8, dtype=torch.int64, device=dev)
+        s.set_variant(v)
+        s.set_stamps(buf.data_ptr())
+        for acc in (True, False):
+            s.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=acc)
+            torch.cuda.synchronize()
+            st = buf.view(nw, 8).cpu().numpy().astype(np.int64)
+            t0 = st[:, 0].min()
+            span = st[:, 5 if acc else 4].max() - t0
+            print("stamps v%d acc=%d: span %d ticks; per-wave phase ticks (median / mean / p90):" % (v, acc, span))
+            names = ["stage", "hash+sort", "gather+insert", "filter+emit", "bin"]
+            for i in range(4 + acc):
+                dd = st[:, i + 1] - st[:, i]
+                print("   %-14s %8.0f %8.0f %8.0f" % (names[i], np.median(dd), dd.mean(), np.percentile(dd, 90)))
+            life = st[:, 5 if acc else 4] - st[:, 0]
+            print("   %-14s %8.0f %8.0f %8.0f" % ("lifetime", np.median(life), life.mean(), np.percentile(life, 90)))
+            # concurrency: waves alive at the median time, and start-time histogram deciles
+            starts = st[:, 0] - t0
+            print("   start deciles:", [int(x) for x in np.percentile(starts, np.arange(0, 101, 10))])
+        s.set_stamps(0)
