@@ -180,6 +180,47 @@ int skq_ingest_finish(skq_ingest* g, uint8_t* kept);
 int skq_ingest_id(const skq_ingest* g, uint64_t ordinal, const char** id, uint64_t* len);
 int skq_ingest_close(skq_ingest* g);
 
+/* ---- EM and assignment on the GPU (estimate_isoform_abundance_em / assign_reads_to_isoforms,
+ * src/isoform_assignment.cpp:9-97) ----------------------------------------------------------
+ * An skq_em_set holds one device's share of the reads' candidate lists. Reads are appended in order
+ * (from a session's device results, or from host CSR arrays); skq_em_select optionally keeps only
+ * some of them (the reads the reference's EM sees). Every kept read counts in R, with or without
+ * candidates (homologous_segments.size(), :55).
+ * One device: skq_em_run + skq_em_assign_host. Several devices (one process each, read-sharded):
+ * every rank runs skq_em_estep on its share, the caller sums post[ntx] over ranks (all-reduce),
+ * and every rank runs skq_em_mstep with the global R; the rounds are then identical on all ranks.
+ * Posterior sums are formed in a fixed order (bitwise reproducible run to run); the reference's
+ * own order is unordered_map iteration order, so parity is to a relative tolerance. */
+typedef struct skq_em_set skq_em_set;
+int skq_em_create(int device, uint32_t ntx, skq_em_set** out);
+int skq_em_free(skq_em_set* em);
+/* append nreads reads: read r's candidates are cand_tid/cand_score[cand_offs[r] .. cand_offs[r+1]) */
+int skq_em_add(skq_em_set* em, uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+               const uint32_t* cand_score);
+/* append every read of the session's last batch, in batch order (device to device; synchronous) */
+int skq_em_add_session(skq_em_set* em, skq_session* s, void* stream);
+/* reads appended so far */
+uint64_t skq_em_size(const skq_em_set* em);
+/* keep[r] != 0 selects appended read r (skq_em_size() bytes, host); once, after the last add */
+int skq_em_select(skq_em_set* em, const uint8_t* keep);
+/* R: the selected reads (all appended reads without skq_em_select) */
+uint64_t skq_em_reads(const skq_em_set* em);
+/* device arrays of ntx doubles: pi = 1/ntx (:17-20) */
+int skq_em_init(skq_em_set* em, double* d_pi, void* stream);
+/* post[t] = sum over this share's reads with den = sum(pi * score) > 1e-10 of pi[t] * score / den */
+int skq_em_estep(skq_em_set* em, const double* d_pi, double* d_post, void* stream);
+/* pi[t] = (post[t] + (double)(0.01f / (float)total_reads)) + (double)0.01f; *change (host, may be
+ * NULL) = sum of |new - old| — synchronous when change is requested */
+int skq_em_mstep(skq_em_set* em, double* d_pi, const double* d_post, uint64_t total_reads, double* change,
+                 void* stream);
+/* one device: the whole loop (stops after the round whose change < convergence); pi (host, ntx) */
+int skq_em_run(skq_em_set* em, int max_iterations, double convergence, double* pi, int* iterations);
+/* assign_reads_to_isoforms: counts[t] = sum of pi[t] * score / total over this share's reads with
+ * total > 0; assigned[t] = 1 where such a read lists t (device arrays) */
+int skq_em_assign(skq_em_set* em, const double* d_pi, double* d_counts, uint8_t* d_assigned, void* stream);
+/* the same with host arrays; pi NULL = the pi skq_em_run left on the device */
+int skq_em_assign_host(skq_em_set* em, const double* pi, double* counts, uint8_t* assigned);
+
 /* Device memory helpers (for hosts without their own allocator). */
 int skq_malloc(int device, size_t bytes, void** out);
 int skq_free(void* p);

@@ -100,6 +100,14 @@ int skq_legacy_index_free(skq_legacy_index* ix);
 int skq_em(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
            const uint32_t* cand_score, uint32_t ntx, int max_iterations, double convergence,
            int nthreads, double* pi, int* iterations);
+/* The EM round split for read-sharded drivers (skq/dist.py; the GPU forms are skq_em_estep /
+ * skq_em_mstep in skq.h): post[ntx] = posterior sums of these reads under pi; then, with post
+ * summed over all shards, pi = (post + (double)(0.01f / R)) + (double)0.01f, *change = sum |d pi|. */
+int skq_em_estep_host(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+                      const uint32_t* cand_score, uint32_t ntx, const double* pi, int nthreads,
+                      double* post);
+int skq_em_mstep_host(uint32_t ntx, double* pi, const double* post, uint64_t total_reads,
+                      double* change);
 /* counts[ntx]: expected reads per transcript; assigned[ntx] = 1 where a read contributed. */
 int skq_assign(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
                const uint32_t* cand_score, uint32_t ntx, const double* pi, double* counts,

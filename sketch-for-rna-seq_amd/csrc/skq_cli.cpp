@@ -5,7 +5,7 @@
 // index: FASTA -> per-transcript FracMinHash sketches -> inverted index -> the legacy file.
 // quant: legacy file -> device index; FASTQ streamed to the GPU, parsed there and mapped in
 //        batches (skq_ingest: sketch + sparse chain); the last valid record of every read id
-//        kept; EM (20 rounds, 0.01) -> assignment -> CSV. As in the reference, quant uses the index's k list.
+//        kept; EM (20 rounds, 0.01) and assignment on the GPU -> CSV. As in the reference, quant uses the index's k list.
 #include <getopt.h>
 
 #include <algorithm>
@@ -95,52 +95,33 @@ void quantification(const std::string& index_path, const std::string& reads_path
     if (const char* e = std::getenv("SKQ_CHUNK_MB")) chunk = std::strtoull(e, nullptr, 10) << 20;
     check(skq_ingest_open(s, reads_path.c_str(), chunk, 8, &q), "FASTQ");
 
-    // per record: status and candidates, kept until duplicates are resolved
-    std::vector<uint8_t> status;
-    std::vector<uint64_t> rec_offs{0};
-    std::vector<uint32_t> ctid, cscore;
+    // every record's candidates stay on the device, appended batch by batch to the EM set
+    skq_em_set* em = nullptr;
+    check(skq_em_create(device(), ntx, &em), "EM");
     const uint32_t thr = skq_threshold((double)kSketchSize);
     for (;;) {
         uint64_t n = 0, first = 0;
         check(skq_ingest_map(q, thr, 0.9, 0, nullptr, &n, &first), "sketch + sparse chain");
         if (n == 0) break;
-        uint64_t nh = 0, nc = 0;
-        check(skq_session_export(s, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &nh, &nc), "export");
-        const size_t s0 = status.size(), c0 = ctid.size();
-        status.resize(s0 + n);
-        ctid.resize(c0 + nc);
-        cscore.resize(c0 + nc);
-        std::vector<uint64_t> co(n + 1);
-        check(skq_session_export(s, status.data() + s0, nullptr, nullptr, co.data(), ctid.data() + c0,
-                                 cscore.data() + c0, &nh, &nc),
-              "export");
-        for (uint64_t r = 0; r < n; ++r) rec_offs.push_back(c0 + co[r + 1]);
+        check(skq_em_add_session(em, s, nullptr), "EM reads");
     }
-    std::vector<uint8_t> kept(status.size());
+    std::vector<uint8_t> kept(skq_ingest_records(q));
     check(skq_ingest_finish(q, kept.data()), "duplicate reads");
     std::cout << "Loading read completed" << std::endl;
     std::cout << "Sparse chaining completed" << std::endl;
 
-    // reads that reach sparse_chain: status OK, and the last such record of their id
-    std::vector<uint64_t> offs{0};
-    std::vector<uint32_t> t2, s2;
-    const uint64_t nrec = status.size();
-    for (uint64_t r = 0; r < nrec; ++r) {
-        if (!kept[r]) continue;  // status OK and the last such record of its id
-        t2.insert(t2.end(), ctid.begin() + (ptrdiff_t)rec_offs[r], ctid.begin() + (ptrdiff_t)rec_offs[r + 1]);
-        s2.insert(s2.end(), cscore.begin() + (ptrdiff_t)rec_offs[r], cscore.begin() + (ptrdiff_t)rec_offs[r + 1]);
-        offs.push_back(t2.size());
-    }
-    const uint64_t R = offs.size() - 1;
+    // the reads sparse_chain saw: status OK, and the last such record of their id
+    check(skq_em_select(em, kept.data()), "EM reads");
     std::vector<double> pi(ntx), counts(ntx);
     std::vector<uint8_t> assigned(ntx);
     int iters = 0;
-    check(skq_em(R, offs.data(), t2.data(), s2.data(), ntx, 20, 0.01, 0, pi.data(), &iters), "EM");
+    check(skq_em_run(em, 20, 0.01, pi.data(), &iters), "EM");
     std::cout << "EM estimation completed" << std::endl;
-    check(skq_assign(R, offs.data(), t2.data(), s2.data(), ntx, pi.data(), counts.data(), assigned.data()), "assign");
+    check(skq_em_assign_host(em, nullptr, counts.data(), assigned.data()), "assign");
     std::cout << "Read assignment completed" << std::endl;
     check(skq_csv_write(out_path.c_str(), tx, counts.data(), assigned.data(), pi.data()), "output_to_csv");
     std::cout << "Output written to " << out_path << std::endl;
+    skq_em_free(em);
     skq_ingest_close(q);
     skq_session_free(s);
     skq_index_free(ix);

@@ -425,7 +425,7 @@ int skq_em(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
     const double probability_epsilon = 1e-10;  // (:30)
     // the pseudocount is a float (:55-58): (posterior + 0.01f / R) + 0.01f
     const float pseudocount = 0.01f;
-    const float pc_per_read = nreads ? pseudocount / (float)nreads : 0.0f;
+    const float pc_per_read = pseudocount / (float)nreads;  // (R = 0: inf, as the reference)
     int it = 0;
     for (; it < max_iterations; ++it) {
         auto estep = [&](int w) {
@@ -460,6 +460,43 @@ int skq_em(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
         }
     }
     if (iterations) *iterations = it;
+    return 0;
+}
+
+// One E-step on the host (the reads' posterior sums, read order): the CPU side of the multi-rank
+// EM loop (skq/dist.py), used where there is no GPU (gloo tests).
+int skq_em_estep_host(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
+                      const uint32_t* cand_score, uint32_t ntx, const double* pi, int nthreads, double* post) {
+    (void)nthreads;
+    if (!pi || !post || (nreads && (!cand_offs || !cand_tid || !cand_score))) return fail(-1, "null argument");
+    std::fill(post, post + ntx, 0.0);
+    for (uint64_t r = 0; r < nreads; ++r) {
+        double den = 0.0;
+        for (uint64_t c = cand_offs[r]; c < cand_offs[r + 1]; ++c) {
+            if (cand_tid[c] >= ntx) return fail(-1, "candidate transcript id out of range");
+            den += pi[cand_tid[c]] * (double)cand_score[c];
+        }
+        if (den > 1e-10) {
+            const double inv = 1.0 / den;
+            for (uint64_t c = cand_offs[r]; c < cand_offs[r + 1]; ++c)
+                post[cand_tid[c]] += pi[cand_tid[c]] * (double)cand_score[c] * inv;
+        }
+    }
+    return 0;
+}
+
+// The M-step (src/isoform_assignment.cpp:53-60) on host arrays; returns sum |new - old| in *change.
+int skq_em_mstep_host(uint32_t ntx, double* pi, const double* post, uint64_t total_reads, double* change) {
+    if (!pi || !post || !change) return fail(-1, "null argument");
+    const float pc = 0.01f;
+    const double a = (double)(pc / (float)total_reads), b = (double)pc;  // (R = 0: inf, as the reference)
+    double ch = 0.0;
+    for (uint32_t t = 0; t < ntx; ++t) {
+        const double np = post[t] + a + b;
+        ch += std::fabs(np - pi[t]);
+        pi[t] = np;
+    }
+    *change = ch;
     return 0;
 }
 

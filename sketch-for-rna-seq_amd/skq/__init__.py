@@ -103,6 +103,21 @@ def lib():
             "skq_em": (i32, [u64, vp, vp, vp, u32, i32, dbl, i32, vp, C.POINTER(i32)]),
             "skq_assign": (i32, [u64, vp, vp, vp, u32, vp, vp, vp]),
             "skq_csv_write": (i32, [C.c_char_p, vp, vp, vp, vp]),
+            "skq_em_create": (i32, [i32, u32, C.POINTER(vp)]),
+            "skq_em_free": (i32, [vp]),
+            "skq_em_add": (i32, [vp, u64, vp, vp, vp]),
+            "skq_em_add_session": (i32, [vp, vp, vp]),
+            "skq_em_size": (u64, [vp]),
+            "skq_em_select": (i32, [vp, vp]),
+            "skq_em_reads": (u64, [vp]),
+            "skq_em_init": (i32, [vp, vp, vp]),
+            "skq_em_estep": (i32, [vp, vp, vp, vp]),
+            "skq_em_mstep": (i32, [vp, vp, vp, u64, C.POINTER(dbl), vp]),
+            "skq_em_run": (i32, [vp, i32, dbl, vp, C.POINTER(i32)]),
+            "skq_em_assign": (i32, [vp, vp, vp, vp, vp]),
+            "skq_em_assign_host": (i32, [vp, vp, vp, vp]),
+            "skq_em_estep_host": (i32, [u64, vp, vp, vp, u32, vp, i32, vp]),
+            "skq_em_mstep_host": (i32, [u32, vp, vp, u64, C.POINTER(dbl)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -448,6 +463,95 @@ class Ingest:
 def _csr(cand_offs, cand_tid, cand_score):
     return (np.ascontiguousarray(cand_offs, np.uint64), np.ascontiguousarray(cand_tid, np.uint32),
             np.ascontiguousarray(cand_score, np.uint32))
+
+
+class EMSet:
+    """One device's share of the reads' candidate lists for the GPU EM (skq_em_*; include/skq.h).
+
+    add(offs, tid, score) / add_session(session) append reads in order; select(keep) keeps a
+    subset; run() and assign() do the whole thing on one device. estep / mstep take device
+    pointers (e.g. torch tensors' data_ptr()) for the multi-GPU loop in skq/dist.py."""
+
+    def __init__(self, ntx, device=0):
+        self.ntx = int(ntx)
+        self.device = device
+        self.h = C.c_void_p()
+        _check(lib().skq_em_create(device, self.ntx, C.byref(self.h)))
+
+    def add(self, cand_offs, cand_tid, cand_score):
+        o, t, s = _csr(cand_offs, cand_tid, cand_score)
+        _check(lib().skq_em_add(self.h, len(o) - 1, _p(o), _p(t), _p(s)))
+
+    def add_session(self, session, stream=None):
+        _check(lib().skq_em_add_session(self.h, session.h, stream))
+
+    def size(self):
+        return lib().skq_em_size(self.h)
+
+    def select(self, keep):
+        k = np.ascontiguousarray(keep, np.uint8)
+        _check(lib().skq_em_select(self.h, _p(k)))
+
+    def reads(self):
+        return lib().skq_em_reads(self.h)
+
+    def init(self, d_pi, stream=None):
+        _check(lib().skq_em_init(self.h, d_pi, stream))
+
+    def estep(self, d_pi, d_post, stream=None):
+        _check(lib().skq_em_estep(self.h, d_pi, d_post, stream))
+
+    def mstep(self, d_pi, d_post, total_reads, stream=None):
+        ch = C.c_double()
+        _check(lib().skq_em_mstep(self.h, d_pi, d_post, int(total_reads), C.byref(ch), stream))
+        return ch.value
+
+    def run(self, max_iterations=20, convergence=0.01):
+        """(pi, iterations) on this device alone."""
+        pi = np.zeros(self.ntx, np.float64)
+        it = C.c_int()
+        _check(lib().skq_em_run(self.h, max_iterations, convergence, _p(pi), C.byref(it)))
+        return pi, it.value
+
+    def assign_device(self, d_pi, d_counts, d_assigned, stream=None):
+        _check(lib().skq_em_assign(self.h, d_pi, d_counts, d_assigned, stream))
+
+    def assign(self, pi=None):
+        """(counts, assigned) for pi (host; None = the pi run() left on the device)."""
+        counts = np.zeros(self.ntx, np.float64)
+        assigned = np.zeros(self.ntx, np.uint8)
+        p = None if pi is None else np.ascontiguousarray(pi, np.float64)
+        _check(lib().skq_em_assign_host(self.h, _p(p), _p(counts), _p(assigned)))
+        return counts, assigned.astype(bool)
+
+    def free(self):
+        if self.h:
+            lib().skq_em_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def em_estep_host(cand_offs, cand_tid, cand_score, ntx, pi):
+    """Posterior sums of these reads under pi (host E-step; the CPU side of skq/dist.py's EM)."""
+    o, t, s = _csr(cand_offs, cand_tid, cand_score)
+    pi = np.ascontiguousarray(pi, np.float64)
+    post = np.zeros(max(ntx, 1), np.float64)
+    _check(lib().skq_em_estep_host(len(o) - 1, _p(o), _p(t), _p(s), ntx, _p(pi), 1, _p(post)))
+    return post[:ntx]
+
+
+def em_mstep_host(pi, post, total_reads):
+    """M-step in place on pi (float64, contiguous); returns the change."""
+    assert pi.dtype == np.float64 and pi.flags.c_contiguous
+    post = np.ascontiguousarray(post, np.float64)
+    ch = C.c_double()
+    _check(lib().skq_em_mstep_host(len(pi), _p(pi), _p(post), int(total_reads), C.byref(ch)))
+    return ch.value
 
 
 def em(cand_offs, cand_tid, cand_score, ntx, max_iterations=20, convergence=0.01, nthreads=0):

@@ -81,3 +81,50 @@ def test_allreduced_shard_totals_equal_whole_batch():
     for rank, tot, slowest in got:
         np.testing.assert_array_equal(tot, whole)
         assert slowest == 1.5
+
+
+def _em_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o, t, s = _em_candidates()
+        start, count = sdist.shard(len(o) - 1, rank, world)
+        so = o[start:start + count + 1] - o[start]
+        st = t[o[start]:o[start + count]]
+        ss = s[o[start]:o[start + count]]
+        pi, it = sdist.em_host(so, st, ss, 700)
+        q.put((rank, pi, it))
+    finally:
+        dist.destroy_process_group()
+
+
+def _em_candidates():
+    rng = np.random.default_rng(77)
+    cnt = rng.choice([0, 1, 1, 2, 3, 5, 9], size=4001)
+    offs = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64)
+    tids = np.concatenate([rng.choice(700, size=c, replace=False) for c in cnt]).astype(np.uint32)
+    scores = rng.integers(1, 40, size=len(tids)).astype(np.uint32)
+    return offs, tids, scores
+
+
+def test_sharded_em_equals_whole_batch():
+    """The EM over read shards (skq/dist.py: per-rank E-step, all-reduced posterior sums, the
+    M-step on every rank) against the oracle EM over all reads, world size 2 on gloo."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_em_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=240) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    o, t, s = _em_candidates()
+    pi_ref, it_ref = orc.em(o, t, s, 700)
+    for _, pi, it in got:
+        assert it == it_ref
+        # shards add their posterior sums separately: only the order of additions differs
+        np.testing.assert_allclose(pi, pi_ref, rtol=1e-12, atol=0)
+    assert got[0][1].tobytes() == got[1][1].tobytes()  # every rank holds the same pi

@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--io-threads", type=int, default=8)
     ap.add_argument("--batch", type=int, default=4_000_000, help="session max_reads")
     ap.add_argument("--export", action="store_true", help="copy every batch's candidates to the host")
+    ap.add_argument("--em", action="store_true",
+                    help="quant end to end: candidates appended on the device, EM (20 rounds) + assignment")
     ap.add_argument("--path", default="/tmp/skq_ingest_bench.fq")
     args = ap.parse_args()
 
@@ -66,6 +68,7 @@ def main():
 
     def run():
         g = skq.Ingest(sess, args.path, chunk_bytes=args.chunk << 20, io_threads=args.io_threads)
+        em = skq.EMSet(tx.ntx) if args.em else None
         tot = 0
         ncand = 0
         while True:
@@ -75,11 +78,23 @@ def main():
             tot += n
             if args.export:
                 ncand += len(sess.export()["cand_tid"])
+            if em is not None:
+                em.add_session(sess)
         sess.check()
         kept = g.finish()
         g.close()
+        if em is not None:
+            t1 = time.perf_counter()
+            em.select(kept)
+            pi, it = em.run(20, 0.01)
+            counts, assigned = em.assign()
+            timing["em_s"] = time.perf_counter() - t1
+            timing["em_rounds"] = it
+            timing["assigned_tx"] = int(assigned.sum())
+            em.free()
         return tot, int(kept.sum()), ncand
 
+    timing = {}
     run()  # warm-up (allocations, code objects)
     sess.reset_totals()
     ts = time.perf_counter()
@@ -90,6 +105,9 @@ def main():
            "reads": n, "kept": kept, "seconds": dt, "reads_per_s": n / dt, "fastq_GB_per_s": size / dt / 1e9,
            "chunk_MiB": args.chunk, "io_threads": args.io_threads, "batch": args.batch,
            "candidates_exported": ncand if args.export else None}
+    if args.em:
+        res["what"] = "quant end to end on the GPU (page cache -> parse -> sketch + chain -> EM + assignment)"
+        res.update(timing)
     print(json.dumps(res), flush=True)
     os.unlink(args.path)
 
