@@ -29,6 +29,7 @@ from skq import synth  # noqa: E402
 
 METRIC = "reads/sec (quant, 150 bp, k=31) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GATHER_CEIL_GPS = 48.1  # random 32-B gathers per ns from an 8 GiB table (profiles/r1_gather_bench.log)
 
 CONFIGS = {
     "cfg2": dict(ntx=10_000, reads=1_000_000, read_len=100, ks=[31],
@@ -179,6 +180,15 @@ def main():
         tr = json.load(open(tf))
         if kname in tr.get("kernels", {}):
             traffic = tr["kernels"][kname]["hbm_bytes_per_read"] * n
+    # the bound that binds the lookups: random fabric requests, not bytes. k_map1
+    # issues one random 32-B entry gather per retained hash; tools/micro/gather_bench measures the
+    # chip's rate for exactly that access (pair-cooperative 32-B gathers, 8 GiB table).
+    requests = None
+    if map1:
+        rps = n * h / (avg[kname] * 1e-3) / 1e9
+        requests = {"random_per_read": h, "achieved": rps, "ceiling": GATHER_CEIL_GPS, "unit": "G/s",
+                    "frac": rps / GATHER_CEIL_GPS,
+                    "ceiling_source": "tools/micro/gather_bench: random pair-cooperative 32-B gathers, 8 GiB table"}
     total_reads = n * world * args.steps
     value = total_reads / elapsed
 
@@ -212,7 +222,8 @@ def main():
                        + (", 1 all-reduce of per-transcript totals per step" if world > 1 else "")},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname]},
+                         "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname],
+                         "requests": requests},
             "path": {"bytes_per_read": b_path, "probe": ("k_map1 (sketch + wide-entry gathers + count fused)" if map1 else
                                                 "fused in k_sketch" if fused else "k_probe"),
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
