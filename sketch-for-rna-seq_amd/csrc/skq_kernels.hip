@@ -2319,18 +2319,35 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
     for (uint32_t i = t; i < bs; i += WG) s_bins[i] = 0;
     __syncthreads();
     const uint32_t w0 = blockIdx.x * chunk, w1 = min(nW, w0 + chunk);
-    // one lane per region (the header loads of WG regions are coalesced), 4 entries in flight
-    for (uint32_t w = w0 + t; w < w1; w += WG) {
-        const uint32_t s0 = hdr[(uint64_t)b * nW + w], s1 = hdr[(uint64_t)(b + 1) * nW + w];
+    // one lane per region (the header loads of WG regions are coalesced); a segment holds ~32
+    // entries, so 16 loads are issued together and the next region's header is read ahead: the
+    // kernel is latency-bound (two workgroups per CU, 64 KiB of bins each)
+    constexpr int U = 16;
+    uint32_t w = w0 + t;
+    uint32_t s0 = 0, s1 = 0;
+    if (w < w1) {
+        s0 = hdr[(uint64_t)b * nW + w];
+        s1 = hdr[(uint64_t)(b + 1) * nW + w];
+    }
+    while (w < w1) {
         const uint32_t* reg = region + (uint64_t)w * (WG * CCAP);
-        for (uint32_t q = s0; q < s1; q += 4) {
-            uint32_t x[4];
+        const uint32_t wn = w + WG;
+        uint32_t n0 = 0, n1 = 0;
+        if (wn < w1) {
+            n0 = hdr[(uint64_t)b * nW + wn];
+            n1 = hdr[(uint64_t)(b + 1) * nW + wn];
+        }
+        for (uint32_t q = s0; q < s1; q += U) {
+            uint32_t x[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = reg[min(q + u, s1 - 1)];
+            for (int u = 0; u < U; ++u) x[u] = reg[min(q + u, s1 - 1)];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < U; ++u)
                 if (q + u < s1) atomicAdd(&s_bins[x[u] & (bs - 1u)], (1ull << 40) | (unsigned long long)(x[u] >> bits));
         }
+        w = wn;
+        s0 = n0;
+        s1 = n1;
     }
     __syncthreads();
     for (uint32_t i = t; i < bs; i += WG) {
