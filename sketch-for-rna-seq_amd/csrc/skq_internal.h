@@ -2,8 +2,11 @@
 // side (skq_capi.hip). Not part of the public ABI.
 #pragma once
 #include <cstdint>
+#include <vector>
 
 #include "skq.h"
+
+struct skq_tables;
 
 namespace skq {
 
@@ -158,6 +161,11 @@ int set_error(int code, const char* msg);
 // session facts for skq_ingest (skq_capi.hip)
 int session_device(const skq_session* s);
 uint64_t session_max_reads(const skq_session* s);
+
+// host: ascending sort with threads (skq_tables.cpp)
+void parallel_sort_u64(std::vector<uint64_t>& v, int threads);
+// host: tables from (key << 32 | tid) words per distinct k (consumed; duplicates removed)
+int tables_from_words(uint32_t ntables, const uint32_t* ks, std::vector<uint64_t>* words, skq_tables** out);
 
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);

@@ -350,31 +350,62 @@ int skq_legacy_index_read(const char* path, skq_legacy_index** out) {
         if (!r.ok) break;
         if (id.emplace(name, (uint32_t)skq_seqs_count(&ix->tx)).second) ix->tx.add(name, seq);
     }
+    // postings: one sequential walk records where each posting's name is (cheap: lengths only);
+    // the name -> id lookups then run on all cores (the map is only read), and the rare names
+    // that are not transcripts of the file get ids afterwards, in file order
     const uint64_t nmaps = r.u64();
     std::vector<uint32_t> tks;
-    std::vector<std::vector<uint32_t>> hs, ts;
+    std::vector<std::vector<uint64_t>> words;  // per map: (key << 32 | tid)
+    std::vector<std::vector<uint64_t>> at;     // per map: file offset of each posting's name
     for (uint64_t m = 0; r.ok && m < nmaps; ++m) {
         tks.push_back(r.u32());
-        hs.emplace_back();
-        ts.emplace_back();
+        words.emplace_back();
+        at.emplace_back();
         const uint64_t nkeys = r.u64();
         for (uint64_t j = 0; r.ok && j < nkeys; ++j) {
             const uint32_t key = r.u32();
             const uint64_t np = r.u64();
             for (uint64_t q = 0; r.ok && q < np; ++q) {
-                const std::string_view name = r.str();
-                if (!r.ok) break;
+                at.back().push_back(r.at);
+                (void)r.str();
+                words.back().push_back((uint64_t)key << 32);
+            }
+        }
+    }
+    if (r.ok) {
+        const int P = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        for (size_t m = 0; m < words.size(); ++m) {
+            std::vector<uint64_t>& wv = words[m];
+            const std::vector<uint64_t>& av = at[m];
+            const uint64_t n = wv.size();
+            auto resolve = [&](uint64_t lo, uint64_t hi) {
+                for (uint64_t i = lo; i < hi; ++i) {
+                    Reader q{f.p, f.n, (size_t)av[i]};
+                    auto it = id.find(q.str());
+                    wv[i] |= it == id.end() ? 0xFFFFFFFFull : (uint64_t)it->second;
+                }
+            };
+            if (n < (1u << 16) || P == 1) {
+                resolve(0, n);
+            } else {
+                std::vector<std::thread> pool;
+                for (int w = 0; w < P; ++w) pool.emplace_back(resolve, n * w / P, n * (w + 1) / P);
+                for (auto& t : pool) t.join();
+            }
+            for (uint64_t i = 0; i < n; ++i) {
+                if ((uint32_t)wv[i] != 0xFFFFFFFFu) continue;
+                Reader q{f.p, f.n, (size_t)av[i]};
+                const std::string_view name = q.str();
                 auto it = id.find(name);
                 uint32_t t;
                 if (it == id.end()) {  // keep unknown names addressable
                     t = (uint32_t)skq_seqs_count(&ix->tx);
                     ix->tx.add(name, std::string_view());
-                    id.emplace(std::string_view(ix->tx.names.data() + ix->tx.name_offs[t], name.size()), t);
+                    id.emplace(name, t);  // (a view into the mapping: stable while it lives)
                 } else {
                     t = it->second;
                 }
-                hs.back().push_back(key);
-                ts.back().push_back(t);
+                wv[i] = (wv[i] & ~0xFFFFFFFFull) | t;
             }
         }
     }
@@ -382,14 +413,8 @@ int skq_legacy_index_read(const char* path, skq_legacy_index** out) {
         delete ix;
         return fail(-5, std::string("truncated or malformed index: ") + path);
     }
-    std::vector<uint64_t> np(tks.size());
-    std::vector<const uint32_t*> hp(tks.size()), tp(tks.size());
-    for (size_t i = 0; i < tks.size(); ++i) {
-        np[i] = hs[i].size();
-        hp[i] = hs[i].data();
-        tp[i] = ts[i].data();
-    }
-    if (int rc = skq_tables_from_pairs((uint32_t)tks.size(), tks.data(), np.data(), hp.data(), tp.data(), &ix->tables)) {
+    at.clear();
+    if (int rc = skq::tables_from_words((uint32_t)tks.size(), tks.data(), words.data(), &ix->tables)) {
         delete ix;
         return rc;
     }

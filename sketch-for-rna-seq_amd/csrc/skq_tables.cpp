@@ -70,8 +70,42 @@ void sort_unique(std::vector<uint32_t>& v) {
     v.erase(std::unique(v.begin(), v.end()), v.end());
 }
 
+}  // namespace
+
+namespace skq {
+// Sorts ascending with up to `threads` threads: sorted chunks, then rounds of pairwise merges.
+// Input that is already sorted (the product's own index files) costs one pass.
+void parallel_sort_u64(std::vector<uint64_t>& v, int threads) {
+    if (std::is_sorted(v.begin(), v.end())) return;
+    if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+    const uint64_t n = v.size();
+    int P = 1;
+    while (P * 2 <= threads && n / (uint64_t)(P * 2) >= (1u << 16)) P *= 2;
+    std::vector<uint64_t> cut(P + 1);
+    for (int i = 0; i <= P; ++i) cut[i] = n * (uint64_t)i / (uint64_t)P;
+    {
+        std::vector<std::thread> pool;
+        for (int i = 0; i < P; ++i)
+            pool.emplace_back([&, i] { std::sort(v.begin() + (ptrdiff_t)cut[i], v.begin() + (ptrdiff_t)cut[i + 1]); });
+        for (auto& t : pool) t.join();
+    }
+    for (int w = 1; w < P; w *= 2) {
+        std::vector<std::thread> pool;
+        for (int i = 0; i + w < P; i += 2 * w) {
+            const uint64_t a = cut[i], m = cut[i + w], b = cut[std::min(i + 2 * w, P)];
+            pool.emplace_back([&v, a, m, b] {
+                std::inplace_merge(v.begin() + (ptrdiff_t)a, v.begin() + (ptrdiff_t)m, v.begin() + (ptrdiff_t)b);
+            });
+        }
+        for (auto& t : pool) t.join();
+    }
+}
+}  // namespace skq
+
+namespace {
+
 void finalize(skq_tables::T& T, std::vector<uint64_t>& words) {
-    std::sort(words.begin(), words.end());
+    skq::parallel_sort_u64(words, 0);
     words.erase(std::unique(words.begin(), words.end()), words.end());
     T.tids.resize(words.size());
     T.keys.clear();
@@ -175,6 +209,23 @@ int skq_tables_from_pairs(uint32_t ntables, const uint32_t* ks, const uint64_t* 
     *out = T;
     return 0;
 }
+
+}  // extern "C"
+
+int skq::tables_from_words(uint32_t ntables, const uint32_t* ks, std::vector<uint64_t>* words, skq_tables** out) {
+    if (!out) return hfail(-1, "out is null");
+    auto* T = new skq_tables();
+    T->t.resize(ntables);
+    for (uint32_t d = 0; d < ntables; ++d) {
+        T->t[d].k = ks[d];
+        finalize(T->t[d], words[d]);
+        std::vector<uint64_t>().swap(words[d]);
+    }
+    *out = T;
+    return 0;
+}
+
+extern "C" {
 
 uint32_t skq_tables_count(const skq_tables* t) { return t ? (uint32_t)t->t.size() : 0; }
 

@@ -71,18 +71,18 @@ def test_fastq_invalid_duplicate_does_not_replace_a_valid_one(tmp_path):
 
 def _legacy_bytes(ks, transcripts, maps):
     """The reference's save_index layout (src/data_io.cpp:175-216), written independently."""
-    b = struct.pack("<Q", len(ks)) + b"".join(struct.pack("<I", k) for k in ks)
-    b += struct.pack("<Q", len(transcripts))
+    b = [struct.pack("<Q", len(ks))] + [struct.pack("<I", k) for k in ks]
+    b.append(struct.pack("<Q", len(transcripts)))
     for name, seq in transcripts:
-        b += struct.pack("<Q", len(name)) + name + struct.pack("<Q", len(seq)) + seq + struct.pack("<i", 0)
-    b += struct.pack("<Q", len(maps))
+        b += [struct.pack("<Q", len(name)), name, struct.pack("<Q", len(seq)), seq, struct.pack("<i", 0)]
+    b.append(struct.pack("<Q", len(maps)))
     for k, mapping in maps:
-        b += struct.pack("<IQ", k, len(mapping))
+        b.append(struct.pack("<IQ", k, len(mapping)))
         for key, names in mapping:
-            b += struct.pack("<IQ", key, len(names))
+            b.append(struct.pack("<IQ", key, len(names)))
             for n in names:
-                b += struct.pack("<Q", len(n)) + n
-    return b
+                b += [struct.pack("<Q", len(n)), n]
+    return b"".join(b)
 
 
 def test_legacy_index_reads_the_reference_layout(tmp_path):
@@ -94,6 +94,32 @@ def test_legacy_index_reads_the_reference_layout(tmp_path):
     keys, offs, tids = tabs[31]
     assert list(keys) == [5, 17, 900] and list(offs) == [0, 2, 3, 5] and list(tids) == [0, 2, 0, 0, 1]
     assert [list(a) for a in tabs[21]] == [[3], [0, 1], [1]]
+
+
+def test_legacy_index_unknown_names_and_parallel_lookups(tmp_path):
+    """Postings naming transcripts absent from the file get ids past them, in file order; a big
+    map (name lookups on all cores, keys in unordered order, as the reference writes them)
+    reads back to the same CSR as a sort of its pairs."""
+    rng = random.Random(4)
+    names = [b"ENSTSYN%08d.1|gene|long-name-padding-padding-padding" % i for i in range(3000)]
+    mapping, pairs = [], set()
+    for key in rng.sample(range(1 << 28), 40_000):
+        ts = rng.sample(range(3000), rng.randint(1, 4))
+        mapping.append((key, [names[t] for t in ts]))
+        pairs.update((key, t) for t in ts)
+    extra = [(7, [b"ghost1", b"tA0"]), (8, [b"ghost2", b"ghost1"])]
+    p = tmp_path / "big.idx"
+    p.write_bytes(_legacy_bytes([31, 25], [(n, b"ACGT") for n in names] + [(b"tA0", b"")],
+                                [(31, mapping), (25, extra)]))
+    ks, got_names, _, tabs = skq.legacy_index_read(p)
+    assert ks == [31, 25]
+    assert got_names == names + [b"tA0", b"ghost1", b"ghost2"]
+    keys, offs, tids = tabs[31]
+    exp = sorted(pairs)
+    assert len(tids) == len(exp)
+    flat = [(int(keys[j]), int(t)) for j in range(len(keys)) for t in tids[offs[j]:offs[j + 1]]]
+    assert flat == exp
+    assert [list(a) for a in tabs[25]] == [[7, 8], [0, 2, 4], [3000, 3001, 3001, 3002]]
 
 
 def test_legacy_index_rejects_truncated_files(tmp_path):
