@@ -93,6 +93,14 @@ int skq_legacy_index_read(const char* path, skq_legacy_index** out);
 int skq_legacy_index_view(const skq_legacy_index* ix, uint32_t* nk, const uint32_t** ks,
                           const skq_seqs** tx, const skq_tables** tables);
 int skq_legacy_index_free(skq_legacy_index* ix);
+/* Compact sidecar `<legacy_path>.skq` (CSR tables + names, no sequences), stamped with the legacy
+ * file's size and mtime; written by the CLI's index mode after the legacy file. */
+int skq_sidecar_write(const char* legacy_path, uint32_t nk, const uint32_t* ks, const skq_seqs* tx,
+                      const skq_tables* tables);
+/* quant's loader: the sidecar when present and its stamp matches, else skq_legacy_index_read.
+ * From the sidecar the transcripts carry names only (empty sequences). *from_sidecar (may be
+ * NULL) tells which. */
+int skq_index_open(const char* path, skq_legacy_index** out, int* from_sidecar);
 
 /* ---- EM, assignment, CSV (src/isoform_assignment.cpp:9-97, src/data_io.cpp:133-152) ------- */
 /* Reads' candidates in CSR form (cand_offs[nreads+1]); every read counts in R, including reads

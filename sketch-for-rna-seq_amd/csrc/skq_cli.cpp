@@ -2,7 +2,8 @@
 //   skq [-h] [-k K1,K2,...] [-o index|quant] <args>
 //   -o index <reference.fasta> <index_output>
 //   -o quant <index_file> <reads.fastq> <output.csv>     (the default mode)
-// index: FASTA -> per-transcript FracMinHash sketches -> inverted index -> the legacy file.
+// index: FASTA -> per-transcript FracMinHash sketches -> inverted index -> the legacy file, plus
+//        its compact CSR sidecar <index>.skq (loaded by quant when its stamp matches).
 // quant: legacy file -> device index; FASTQ streamed to the GPU, parsed there and mapped in
 //        batches (skq_ingest: sketch + sparse chain); the last valid record of every read id
 //        kept; EM (20 rounds, 0.01) and assignment on the GPU -> CSV. As in the reference, quant uses the index's k list.
@@ -65,6 +66,8 @@ void build_and_save_index(const std::string& fasta, const std::string& out, cons
     const std::chrono::duration<double> dt = std::chrono::steady_clock::now() - t0;
     std::cout << "Index built in " << dt.count() << " seconds." << std::endl;
     check(skq_legacy_index_write(out.c_str(), (uint32_t)ks.size(), ks.data(), tx, tabs), "save_index");
+    // the compact CSR copy quant loads instead of parsing the legacy file (skq_index_open)
+    check(skq_sidecar_write(out.c_str(), (uint32_t)ks.size(), ks.data(), tx, tabs), "index sidecar");
     std::cout << "Index saved to " << out << std::endl;
     skq_tables_free(tabs);
     skq_seqs_free(tx);
@@ -72,7 +75,7 @@ void build_and_save_index(const std::string& fasta, const std::string& out, cons
 
 void quantification(const std::string& index_path, const std::string& reads_path, const std::string& out_path) {
     skq_legacy_index* lx = nullptr;
-    check(skq_legacy_index_read(index_path.c_str(), &lx), "load_index");
+    check(skq_index_open(index_path.c_str(), &lx, nullptr), "load_index");
     std::cout << "Index loaded from " << index_path << std::endl;
     std::cout << "Loading index completed" << std::endl;
     uint32_t nk = 0;

@@ -166,6 +166,9 @@ uint64_t session_max_reads(const skq_session* s);
 void parallel_sort_u64(std::vector<uint64_t>& v, int threads);
 // host: tables from (key << 32 | tid) words per distinct k (consumed; duplicates removed)
 int tables_from_words(uint32_t ntables, const uint32_t* ks, std::vector<uint64_t>* words, skq_tables** out);
+// host: tables taking over ready CSR arrays per distinct k (moved from)
+int tables_from_csr(uint32_t ntables, const uint32_t* ks, std::vector<uint32_t>* keys, std::vector<uint64_t>* offs,
+                    std::vector<uint32_t>* tids, skq_tables** out);
 
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);

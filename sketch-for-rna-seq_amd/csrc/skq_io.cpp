@@ -329,6 +329,70 @@ int skq_legacy_index_write(const char* path, uint32_t nk, const uint32_t* ks, co
     return ok ? 0 : fail(-4, std::string("write failed: ") + path);
 }
 
+// ---- compact sidecar -----------------------------------------------
+// `<legacy>.skq`, written by `index` next to the reference's file: the same content in CSR form
+// (k list, transcript names, per distinct k keys / offsets / dense ids; no sequences, which
+// quant does not use), stamped with the legacy file's size and mtime. skq_index_open loads it
+// with a few large copies instead of parsing 1.3 GB of length-prefixed strings, and falls back
+// to the legacy file whenever the stamp does not match.
+namespace {
+
+constexpr char kSidecarMagic[8] = {'S', 'K', 'Q', 'I', 'D', 'X', '0', '1'};
+
+std::string sidecar_path(const char* legacy) { return std::string(legacy) + ".skq"; }
+
+bool file_stamp(const char* path, uint64_t& size, int64_t& mtime_ns) {
+    struct stat st {};
+    if (stat(path, &st) != 0) return false;
+    size = (uint64_t)st.st_size;
+    mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int skq_sidecar_write(const char* legacy_path, uint32_t nk, const uint32_t* ks, const skq_seqs* tx,
+                      const skq_tables* tables) {
+    if (!legacy_path || !tx || !tables || (nk && !ks)) return fail(-1, "null argument");
+    uint64_t lsize = 0;
+    int64_t lmtime = 0;
+    if (!file_stamp(legacy_path, lsize, lmtime)) return fail(-4, std::string("no legacy index at ") + legacy_path);
+    const std::string out = sidecar_path(legacy_path);
+    const std::string tmp = out + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return fail(-4, std::string("could not open for writing: ") + tmp);
+    Writer w{f};
+    w.raw(kSidecarMagic, 8);
+    w.u64(lsize);
+    w.u64((uint64_t)lmtime);
+    w.u64(nk);
+    for (uint32_t i = 0; i < nk; ++i) w.u32(ks[i]);
+    const uint64_t ntx = skq_seqs_count(tx);
+    w.u64(ntx);
+    w.u64(tx->names.size());
+    w.raw(tx->names.data(), tx->names.size());
+    w.raw(tx->name_offs.data(), (ntx + 1) * 8);
+    const uint32_t nt = skq_tables_count(tables);
+    w.u64(nt);
+    for (uint32_t i = 0; i < nt; ++i) {
+        skq_kmer_table v{};
+        skq_tables_get(tables, i, &v);
+        w.u32(v.k);
+        w.u64(v.nkeys);
+        w.u64(v.offs[v.nkeys]);
+        w.raw(v.keys, v.nkeys * 4);
+        w.raw(v.offs, (v.nkeys + 1) * 8);
+        w.raw(v.tids, v.offs[v.nkeys] * 4);
+    }
+    const bool ok = w.ok && fclose(f) == 0 && rename(tmp.c_str(), out.c_str()) == 0;
+    if (!ok) std::remove(tmp.c_str());
+    return ok ? 0 : fail(-4, std::string("write failed: ") + out);
+}
+
+}  // extern "C"
+
 // Reads the format back: dense transcript ids follow the transcripts' order in the file; a
 // posting naming a transcript that is not in the file gets a new id past them (name kept).
 int skq_legacy_index_read(const char* path, skq_legacy_index** out) {
@@ -435,6 +499,76 @@ int skq_legacy_index_view(const skq_legacy_index* ix, uint32_t* nk, const uint32
 int skq_legacy_index_free(skq_legacy_index* ix) {
     delete ix;
     return 0;
+}
+
+// quant's loader: the sidecar when its stamp matches the legacy file, else the legacy file
+int skq_index_open(const char* path, skq_legacy_index** out, int* from_sidecar) {
+    if (!path || !out) return fail(-1, "null argument");
+    *out = nullptr;
+    if (from_sidecar) *from_sidecar = 0;
+    uint64_t lsize = 0;
+    int64_t lmtime = 0;
+    const std::string sp = sidecar_path(path);
+    if (file_stamp(path, lsize, lmtime) && access(sp.c_str(), R_OK) == 0) {
+        MappedFile f;
+        if (f.open(sp.c_str()) == 0) {
+            Reader r{f.p, f.n};
+            char magic[8] = {};
+            r.raw(magic, 8);
+            const uint64_t sz = r.u64(), mt = r.u64();
+            if (r.ok && !std::memcmp(magic, kSidecarMagic, 8) && sz == lsize && (int64_t)mt == lmtime) {
+                auto* ix = new skq_legacy_index();
+                const uint64_t nk = r.u64();
+                if (nk > SKQ_MAX_K * 64ull) r.ok = false;
+                for (uint64_t i = 0; r.ok && i < nk; ++i) ix->ks.push_back(r.u32());
+                const uint64_t ntx = r.u64(), nb = r.u64();
+                if (r.ok && nb <= f.n && ntx < f.n) {
+                    ix->tx.names.resize(nb);
+                    r.raw(ix->tx.names.data(), nb);
+                    ix->tx.name_offs.resize(ntx + 1);
+                    r.raw(ix->tx.name_offs.data(), (ntx + 1) * 8);
+                    ix->tx.offs.assign(ntx + 1, 0);  // no sequences
+                } else {
+                    r.ok = false;
+                }
+                const uint64_t nt = r.u64();
+                if (nt > SKQ_MAX_K * 64ull) r.ok = false;
+                std::vector<uint32_t> tks;
+                std::vector<std::vector<uint32_t>> K, T;
+                std::vector<std::vector<uint64_t>> O;
+                for (uint64_t i = 0; r.ok && i < nt; ++i) {
+                    tks.push_back(r.u32());
+                    const uint64_t nkeys = r.u64(), np = r.u64();
+                    if (!r.ok || nkeys > f.n || np > f.n) {
+                        r.ok = false;
+                        break;
+                    }
+                    std::vector<uint32_t> keys(nkeys), tids(np);
+                    std::vector<uint64_t> offs(nkeys + 1);
+                    r.raw(keys.data(), nkeys * 4);
+                    r.raw(offs.data(), (nkeys + 1) * 8);
+                    r.raw(tids.data(), np * 4);
+                    bool mono = r.ok && offs[0] == 0 && offs[nkeys] == np;
+                    for (uint64_t j = 0; mono && j < nkeys; ++j) mono = offs[j] <= offs[j + 1];
+                    if (!mono) {
+                        r.ok = false;
+                        break;
+                    }
+                    K.push_back(std::move(keys));
+                    O.push_back(std::move(offs));
+                    T.push_back(std::move(tids));
+                }
+                if (r.ok && skq::tables_from_csr((uint32_t)tks.size(), tks.data(), K.data(), O.data(), T.data(),
+                                                 &ix->tables) == 0) {
+                    *out = ix;
+                    if (from_sidecar) *from_sidecar = 1;
+                    return 0;
+                }
+                delete ix;
+            }
+        }
+    }
+    return skq_legacy_index_read(path, out);
 }
 
 // ---- EM, assignment (src/isoform_assignment.cpp:9-97), CSV (src/data_io.cpp:133-152) ---------

@@ -225,6 +225,21 @@ int skq::tables_from_words(uint32_t ntables, const uint32_t* ks, std::vector<uin
     return 0;
 }
 
+int skq::tables_from_csr(uint32_t ntables, const uint32_t* ks, std::vector<uint32_t>* keys,
+                         std::vector<uint64_t>* offs, std::vector<uint32_t>* tids, skq_tables** out) {
+    if (!out) return hfail(-1, "out is null");
+    auto* T = new skq_tables();
+    T->t.resize(ntables);
+    for (uint32_t d = 0; d < ntables; ++d) {
+        T->t[d].k = ks[d];
+        T->t[d].keys = std::move(keys[d]);
+        T->t[d].offs = std::move(offs[d]);
+        T->t[d].tids = std::move(tids[d]);
+    }
+    *out = T;
+    return 0;
+}
+
 extern "C" {
 
 uint32_t skq_tables_count(const skq_tables* t) { return t ? (uint32_t)t->t.size() : 0; }

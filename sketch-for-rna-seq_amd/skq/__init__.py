@@ -100,6 +100,8 @@ def lib():
             "skq_legacy_index_read": (i32, [C.c_char_p, C.POINTER(vp)]),
             "skq_legacy_index_view": (i32, [vp, C.POINTER(u32), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]),
             "skq_legacy_index_free": (i32, [vp]),
+            "skq_sidecar_write": (i32, [C.c_char_p, u32, vp, vp, vp]),
+            "skq_index_open": (i32, [C.c_char_p, C.POINTER(vp), C.POINTER(i32)]),
             "skq_em": (i32, [u64, vp, vp, vp, u32, i32, dbl, i32, vp, C.POINTER(i32)]),
             "skq_assign": (i32, [u64, vp, vp, vp, u32, vp, vp, vp]),
             "skq_csv_write": (i32, [C.c_char_p, vp, vp, vp, vp]),
@@ -383,6 +385,23 @@ def legacy_index_read(path):
         _check(lib().skq_legacy_index_view(h, C.byref(nk), C.byref(ks), C.byref(tx), C.byref(tabs)))
         names, seqs = _seqs(tx)
         return ([int(x) for x in _arr(ks, C.c_uint32, nk.value, np.uint32)], names, seqs, _tables_dict(tabs))
+    finally:
+        lib().skq_legacy_index_free(h)
+
+
+def index_open(path):
+    """quant's index loader (skq_index_open): the `<path>.skq` sidecar when its stamp matches the
+    legacy file, else the legacy file. (ks, names, sequences, tables, from_sidecar); sequences
+    are empty when read from the sidecar."""
+    h = C.c_void_p()
+    side = C.c_int()
+    _check(lib().skq_index_open(str(path).encode(), C.byref(h), C.byref(side)))
+    try:
+        nk, ks, tx, tabs = C.c_uint32(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(lib().skq_legacy_index_view(h, C.byref(nk), C.byref(ks), C.byref(tx), C.byref(tabs)))
+        names, seqs = _seqs(tx)
+        return ([int(x) for x in _arr(ks, C.c_uint32, nk.value, np.uint32)], names, seqs, _tables_dict(tabs),
+                bool(side.value))
     finally:
         lib().skq_legacy_index_free(h)
 

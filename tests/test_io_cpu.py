@@ -122,6 +122,32 @@ def test_legacy_index_unknown_names_and_parallel_lookups(tmp_path):
     assert [list(a) for a in tabs[25]] == [[7, 8], [0, 2, 4], [3000, 3001, 3001, 3002]]
 
 
+def test_sidecar_matches_the_legacy_file_and_is_stamped(tmp_path):
+    """index mode writes <index>.skq next to the legacy file; skq_index_open reads the same tables
+    and names from it, and falls back to the legacy file once the stamp no longer matches."""
+    out = tmp_path / "e.idx"
+    subprocess.run([CLI, "-k", "31,25", "-o", "index", os.path.join(EDGE, "e.fa"), str(out)], check=True,
+                   capture_output=True, timeout=120)
+    assert os.path.exists(str(out) + ".skq")
+    ks, names, seqs, tabs = skq.legacy_index_read(out)
+    ks2, names2, seqs2, tabs2, side = skq.index_open(out)
+    assert side and ks2 == ks and names2 == names and all(s == b"" for s in seqs2)
+    for k in ks:
+        for a, b in zip(tabs[k], tabs2[k]):
+            np.testing.assert_array_equal(a, b)
+    os.utime(out, ns=(1, 1))  # the legacy file changed: the sidecar is stale
+    ks3, names3, seqs3, _, side3 = skq.index_open(out)
+    assert not side3 and names3 == names and seqs3 == seqs
+    # a corrupt sidecar with a matching stamp is not trusted past its checks either
+    raw = bytearray(open(str(out) + ".skq", "rb").read())
+    st = os.stat(out)
+    import struct as _s
+    raw[8:24] = _s.pack("<QQ", st.st_size, st.st_mtime_ns)
+    open(str(out) + ".skq", "wb").write(bytes(raw[:-7]))
+    ks4, names4, _, tabs4, side4 = skq.index_open(out)
+    assert not side4 and names4 == names
+
+
 def test_legacy_index_rejects_truncated_files(tmp_path):
     p = tmp_path / "bad.idx"
     p.write_bytes(_legacy_bytes([31], [(b"t", b"ACGT")], [(31, [(1, [b"t"])])])[:-3])
