@@ -1586,6 +1586,257 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
     if (bin) bin_candidates(p, t, w, nc, key, s_bc, s_mem);
 }
 
+// Entry-parallel count over wide tables for 2..4 k slots (the multi-k quant path: k_sketch, then
+// this): k_map1's count phase with per-k counters. Per wave, the 64 reads' retained hashes of
+// every k slot are listed in LDS (hash, owning lane | k slot << 6), in passes of CW_P; lane pairs
+// take them round-robin, gather one 32-B wide entry each (the even lane inserts t0..t2, the odd
+// lane t3..t6) into the owning read's table: TS slots of two words (tid; 8-bit counts per k
+// slot), slot s of read o in column (o + s) & 63 of the wave (distinct LDS banks). Then the
+// filter of src/sparse_chaining.cpp:76-110 at every k, the candidates, and the binning epilogue.
+// Reads with more than TS distinct transcripts go to the slow chain path, as in k_count3.
+constexpr uint32_t CW_P = 512;
+template <int NK>
+__global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
+    static_assert(NK >= 2 && NK <= NK_FAST, "2..4 k slots (8-bit counts packed per k)");
+    static_assert(2 * TS >= CCAP, "the binned region reuses the count tables");
+    __shared__ __attribute__((aligned(16))) uint32_t s_tabs[2 * TS * WG];
+    __shared__ uint32_t s_hl[WG / 64][CW_P];
+    __shared__ uint8_t s_ow[WG / 64][CW_P];
+    __shared__ uint32_t s_flag[WG];
+    __shared__ uint32_t s_bc[WG + 1];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint64_t r = (uint64_t)blockIdx.x * WG + t;
+    const bool inb = r < p.n;
+    const uint64_t rr = inb ? r : p.n - 1;  // (p.n > 0)
+    const bool bin = p.accumulate && p.bin_nb;  // uniform
+    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+#pragma unroll
+    for (int sl = 0; sl < TS; ++sl) {
+        s_tabs[(2 * sl) * WG + t] = EMPTY;
+        s_tabs[(2 * sl + 1) * WG + t] = 0;
+    }
+    s_flag[t] = 0;
+    if (bin) s_bc[t] = 0;
+    // the read's status, slow flag and per-k counts (as count_read)
+    const uint32_t st = p.status[rr], pf = p.pflag[rr];
+    uint32_t cnts[NK];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, rr, i);
+    const bool ok = inb && (st & SKQ_STATUS_MASK) == SKQ_READ_OK;
+    if (ok && pf) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+    const bool act = ok && !pf;
+    if (inb && !act) p.cand_cnt[r] = 0;
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        cnts[i] = act && p.tabs[i].present ? min(cnts[i], p.lcap) : 0u;
+        m += cnts[i];
+    }
+    const uint32_t incl = wave_incl_scan(m, lane);
+    const uint32_t off = incl - m;
+    const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes, all k slots
+    uint32_t* colbase = s_tabs + wv * 64;
+    const bool odd = lane & 1u;
+    auto wd_of = [&](uint32_t i) -> const uint32_t* {
+        const uint32_t* w = p.wdir[0];
+#pragma unroll
+        for (int q = 1; q < NK; ++q) w = i == (uint32_t)q ? p.wdir[q] : w;
+        return w;
+    };
+    auto wlen_of = [&](uint32_t i) -> uint64_t {
+        uint64_t w = p.wdir_len[0];
+#pragma unroll
+        for (int q = 1; q < NK; ++q) w = i == (uint32_t)q ? p.wdir_len[q] : w;
+        return w;
+    };
+    // an insert whose home slot holds another transcript probes on (rare: not unrolled)
+    auto ins_probe = [&](uint32_t x, uint32_t o, uint32_t inc) {
+        uint32_t sl = Counter<1, WG>::slot_of(x);
+#pragma unroll 1
+        for (int z = 1; z < TS; ++z) {
+            sl = (sl + 1) & (TS - 1);
+            const uint32_t c = (o + sl) & 63u;
+            const uint32_t old = atomicCAS(colbase + (2 * sl) * WG + c, EMPTY, x);
+            if (old == EMPTY || old == x) {
+                atomicAdd(colbase + (2 * sl + 1) * WG + c, inc);
+                return;
+            }
+        }
+        atomicOr(&s_flag[wv * 64 + o], 1u);  // more than TS distinct transcripts
+    };
+    auto ins = [&](uint32_t x, uint32_t o, uint32_t inc) {
+        const uint32_t sl = Counter<1, WG>::slot_of(x), c = (o + sl) & 63u;
+        const uint32_t old = atomicCAS(colbase + (2 * sl) * WG + c, EMPTY, x);
+        if (old == EMPTY || old == x) atomicAdd(colbase + (2 * sl + 1) * WG + c, inc);
+        else ins_probe(x, o, inc);
+    };
+    uint32_t hx[NK][8];  // the first 8 hashes of every k slot (loaded once, listed in every pass)
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        const uint32_t* src = p.lofs + (uint64_t)i * p.lcap * p.n + rr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hx[i][u] = (uint32_t)u < cnts[i] ? src[(uint64_t)u * p.n] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t pb = 0; pb < M; pb += CW_P) {  // wave-uniform
+        // this lane's entries that fall in the pass, straight from the sketch's hash rows: the
+        // first 8 of every k slot in one round trip (all loads issued before any store), the
+        // rest (reads with more than 8 at a k) 8 at a time
+        {
+            uint32_t e = off;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t ee = e + u;
+                    if ((uint32_t)u < cnts[i] && ee >= pb && ee < pb + CW_P) {
+                        s_hl[wv][ee - pb] = hx[i][u];
+                        s_ow[wv][ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
+                    }
+                }
+                e += cnts[i];
+            }
+        }
+        {
+            uint32_t e = off;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const uint32_t c = cnts[i];
+                const uint32_t* src = p.lofs + (uint64_t)i * p.lcap * p.n + rr;
+#pragma unroll 1
+                for (uint32_t j0 = 8; j0 < c; j0 += 8) {
+                    uint32_t x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = j0 + u < c ? src[(uint64_t)(j0 + u) * p.n] : 0u;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t ee = e + j0 + u;
+                        if (j0 + u < c && ee >= pb && ee < pb + CW_P) {
+                            s_hl[wv][ee - pb] = x[u];
+                            s_ow[wv][ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
+                        }
+                    }
+                }
+                e += c;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t ne = min(M - pb, CW_P);
+        constexpr int R = 4;  // rounds of 32 entries in flight together
+        for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
+            uint4 w[R];
+            uint32_t own[R];
+            bool okk[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const uint32_t ee = e0 + 32 * u + (lane >> 1);
+                const bool in = ee < ne;
+                const uint32_t h = s_hl[wv][in ? ee : 0];
+                own[u] = s_ow[wv][in ? ee : 0];
+                const uint32_t i = own[u] >> 6;
+                okk[u] = in && h < wlen_of(i);
+                w[u] = *reinterpret_cast<const uint4*>(wd_of(i) + (okk[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const uint32_t sw = pair_swap(w[u].x);
+                const uint32_t n = okk[u] ? (odd ? sw : w[u].x) : 0u;  // [0x80000000 | offset] when long
+                const uint32_t qb = odd ? 3u : 0u;
+                const uint32_t o = own[u] & 63u, inc = 1u << (8 * (own[u] >> 6));
+                // the first attempts (a CAS at each tid's home slot) issue before any result is
+                // looked at; a tid found there gets a non-returning add of its k slot's count
+                uint32_t xs[4], olds[4];
+                bool vs[4];
+                xs[0] = odd ? w[u].x : w[u].y;
+                xs[1] = odd ? w[u].y : w[u].z;
+                xs[2] = odd ? w[u].z : w[u].w;
+                xs[3] = w[u].w;
+                vs[0] = n > qb;
+                vs[1] = n > qb + 1;
+                vs[2] = n > qb + 2;
+                vs[3] = odd && n > 6;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+                    olds[q] = vs[q] ? atomicCAS(colbase + (2 * sl) * WG + ((o + sl) & 63u), EMPTY, xs[q]) : 0u;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (!vs[q]) continue;
+                    const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+                    if (olds[q] == EMPTY || olds[q] == xs[q]) atomicAdd(colbase + (2 * sl + 1) * WG + ((o + sl) & 63u), inc);
+                    else ins_probe(xs[q], o, inc);
+                }
+                // lists longer than 7 (rare): the even lane inserts the rest of the list
+                if (__any(!odd && n > 7) && !odd && n > 7) {
+                    const uint32_t lo = n & 0x7FFFFFFFu;
+                    const uint32_t len = p.lists[lo];
+                    for (uint32_t q = 7; q < len; ++q) ins(p.lists[lo + 1 + q], o, inc);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    uint32_t key[TS];
+    uint32_t nc = 0;
+    if (act) {
+        if (s_flag[t] == 0) {
+            // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
+            uint32_t tx[TS], cx[TS], mx[NK] = {};
+#pragma unroll
+            for (int sl = 0; sl < TS; ++sl) {
+                const uint32_t c = (lane + sl) & 63u;
+                tx[sl] = colbase[(2 * sl) * WG + c];
+                cx[sl] = tx[sl] != EMPTY ? colbase[(2 * sl + 1) * WG + c] : 0u;
+#pragma unroll
+                for (int i = 0; i < NK; ++i) mx[i] = max(mx[i], (cx[sl] >> (8 * i)) & 0xFFu);
+            }
+            uint32_t need[NK];
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const double thr = p.fraction * (double)mx[i];
+                uint32_t ti = 0;
+                if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+                need[i] = ti;
+            }
+#pragma unroll
+            for (int sl = 0; sl < TS; ++sl) {
+                bool keep = tx[sl] != EMPTY;
+                uint32_t score = 0;
+#pragma unroll
+                for (int i = 0; i < NK; ++i) {
+                    const uint32_t ci = (cx[sl] >> (8 * i)) & 0xFFu;
+                    keep &= ci >= need[i];
+                    score += ci;
+                }
+                // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
+                key[sl] = keep ? ((1023u - score) << 22) | tx[sl] : ~0u;
+            }
+            bitonic_sort<TS>(key);
+            uint32_t* ct = p.cand_tid + r;
+            uint32_t* cs = p.cand_score + r;
+#pragma unroll
+            for (int d = 0; d < TS; ++d) {
+                if (key[d] != ~0u) {
+                    ct[(uint64_t)d * p.n] = key[d] & 0x3FFFFFu;
+                    cs[(uint64_t)d * p.n] = 1023u - (key[d] >> 22);
+                    ++nc;
+                }
+            }
+            p.cand_cnt[r] = nc;
+        } else {
+            list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+            p.cand_cnt[r] = 0;
+        }
+    }
+    // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
+    if (bin) bin_candidates(p, t, blockIdx.x, nc, key, s_bc, s_tabs);
+}
+
 // k_map1 LDS: per wave max(staged codes + bad bits, one pass of the entry list: MAP_P hashes and
 // their owning lanes)
 // (the per-chunk bad bits sit in row 0 of the wave's raw columns, dead until hashing starts; the
@@ -2429,6 +2680,16 @@ int launch_count(const ChainParams& p, void* stream) {
             default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, st, p); break;
             }
         };
+        // wide tables, 2..4 k slots: the entry-parallel count (variant 13: k_count3, A/B)
+        if (p.wide == 1 && p.nk >= 2 && p.nk <= (uint32_t)NK_FAST && p.status && !p.present && !p.hash_offs &&
+            p.variant != 13) {
+            switch (p.nk) {
+            case 2: hipLaunchKernelGGL((k_countw<2>), grid, dim3(WG), 0, st, p); break;
+            case 3: hipLaunchKernelGGL((k_countw<3>), grid, dim3(WG), 0, st, p); break;
+            default: hipLaunchKernelGGL((k_countw<4>), grid, dim3(WG), 0, st, p); break;
+            }
+            return hipGetLastError() == hipSuccess ? 0 : -2;
+        }
         if (p.wide == 1) go(std::integral_constant<int, 1>{});
         else if (p.wide == 2) go(std::integral_constant<int, 2>{});
         else go(std::integral_constant<int, 0>{});
