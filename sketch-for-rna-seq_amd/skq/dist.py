@@ -42,8 +42,16 @@ def max_over_ranks(value, device=None):
 
 
 def _allreduce(t, op=None):
+    """Sum (or op) over ranks in place. RCCL takes device tensors directly; on gloo (CPU tests and
+    one-GPU rehearsals) a device tensor goes through host memory."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM if op is None else op)
+        op = dist.ReduceOp.SUM if op is None else op
+        if t.is_cuda and dist.get_backend() == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
     return t
 
 

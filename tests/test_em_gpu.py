@@ -180,3 +180,51 @@ def test_no_reads_after_select():
     em.select(np.array([1], np.uint8))
     with pytest.raises(skq.SkqError):
         em.add(np.array([0, 1], np.uint64), np.array([1], np.uint32), np.array([2], np.uint32))
+
+
+def _dist_em_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    from skq import dist as sdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o, t, s = random_candidates(random.Random(21), 20_000, 900)
+        start, count = sdist.shard(len(o) - 1, rank, world)
+        em = skq.EMSet(900)
+        em.add(o[start:start + count + 1], t, s)
+        pi, it = sdist.em_gpu(em, 20, 0.01, device=torch.device("cuda", 0))
+        counts, assigned = sdist.assign_gpu(em, pi)
+        q.put((rank, pi.cpu().numpy(), it, counts.cpu().numpy(), assigned.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_em_two_ranks():
+    """skq/dist.py's em_gpu / assign_gpu with two ranks (processes) on this GPU, gloo standing in
+    for RCCL: per-rank E-steps on device, posterior sums all-reduced each round."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_em_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=100) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    o, t, s = random_candidates(random.Random(21), 20_000, 900)
+    pi_ref, it_ref = orc.em(o, t, s, 900)
+    c_ref, a_ref = orc.assign(o, t, s, 900, pi_ref)
+    for _, pi, it, counts, assigned in got:
+        assert it == it_ref
+        np.testing.assert_allclose(pi, pi_ref, rtol=RTOL, atol=0)
+        np.testing.assert_allclose(counts, c_ref, rtol=RTOL, atol=1e-300)
+        np.testing.assert_array_equal(assigned, a_ref)
+    assert got[0][1].tobytes() == got[1][1].tobytes()
