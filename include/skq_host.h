@@ -34,6 +34,10 @@ typedef struct skq_tables skq_tables;
  * windows holding any other byte skipped. nthreads <= 0: hardware concurrency. */
 int skq_tables_build(uint32_t ntx, const uint8_t* seqs, const uint64_t* offs, uint32_t nk,
                      const uint32_t* ks, uint32_t threshold, int nthreads, skq_tables** out);
+/* The same tables built on the GPU (host arrays in; transcripts sketched by one workgroup each,
+ * one radix sort per k): identical output to skq_tables_build. */
+int skq_tables_build_gpu(int device, uint32_t ntx, const uint8_t* seqs, const uint64_t* offs,
+                         uint32_t nk, const uint32_t* ks, uint32_t threshold, skq_tables** out);
 /* from (hash, tid) pairs per distinct k (duplicates removed) */
 int skq_tables_from_pairs(uint32_t ntables, const uint32_t* ks, const uint64_t* npairs,
                           const uint32_t* const* hashes, const uint32_t* const* tids,

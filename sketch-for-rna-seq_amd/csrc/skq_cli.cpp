@@ -60,9 +60,15 @@ void build_and_save_index(const std::string& fasta, const std::string& out, cons
     const uint64_t* offs = nullptr;
     check(skq_seqs_view(tx, &bytes, &offs, nullptr, nullptr), "sequences");
     skq_tables* tabs = nullptr;
-    check(skq_tables_build((uint32_t)skq_seqs_count(tx), bytes, offs, (uint32_t)ks.size(), ks.data(),
-                           skq_threshold((double)kSketchSize), 0, &tabs),
-          "index build");
+    // on the GPU when there is one (skq_tables_build_gpu), else on host threads: the same tables
+    if (skq_device_count() > device())
+        check(skq_tables_build_gpu(device(), (uint32_t)skq_seqs_count(tx), bytes, offs, (uint32_t)ks.size(), ks.data(),
+                                   skq_threshold((double)kSketchSize), &tabs),
+              "index build");
+    else
+        check(skq_tables_build((uint32_t)skq_seqs_count(tx), bytes, offs, (uint32_t)ks.size(), ks.data(),
+                               skq_threshold((double)kSketchSize), 0, &tabs),
+              "index build");
     const std::chrono::duration<double> dt = std::chrono::steady_clock::now() - t0;
     std::cout << "Index built in " << dt.count() << " seconds." << std::endl;
     check(skq_legacy_index_write(out.c_str(), (uint32_t)ks.size(), ks.data(), tx, tabs), "save_index");

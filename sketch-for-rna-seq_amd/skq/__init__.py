@@ -75,6 +75,7 @@ def lib():
             "skq_session_set_stamps": (i32, [vp, vp]),
             "skq_session_kernel_time": (i32, [vp, i32, C.POINTER(dbl), C.POINTER(u64)]),
             "skq_tables_build": (i32, [u32, vp, vp, u32, vp, u32, i32, C.POINTER(vp)]),
+            "skq_tables_build_gpu": (i32, [i32, u32, vp, vp, u32, vp, u32, C.POINTER(vp)]),
             "skq_tables_count": (u32, [vp]),
             "skq_tables_get": (i32, [vp, u32, C.POINTER(_KmerTable)]),
             "skq_tables_free": (i32, [vp]),
@@ -330,6 +331,20 @@ def build_tables(seqs, offs, ks, thr=None, nthreads=0):
     h = C.c_void_p()
     _check(lib().skq_tables_build(len(offs) - 1, _p(seqs), _p(offs), len(ka), _p(ka), thr, nthreads,
                                   C.byref(h)))
+    try:
+        return _tables_dict(h)
+    finally:
+        lib().skq_tables_free(h)
+
+
+def build_tables_gpu(seqs, offs, ks, thr=None, device=0):
+    """The same tables as build_tables, built on the GPU (skq_tables_build_gpu)."""
+    thr = threshold() if thr is None else thr
+    seqs = np.ascontiguousarray(seqs, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    ka = np.array(ks, np.uint32)
+    h = C.c_void_p()
+    _check(lib().skq_tables_build_gpu(device, len(offs) - 1, _p(seqs), _p(offs), len(ka), _p(ka), thr, C.byref(h)))
     try:
         return _tables_dict(h)
     finally:
