@@ -123,6 +123,9 @@ struct skq_session {
     std::vector<TimedLaunch> timed;
     int variant = 0;
     uint64_t* stamps = nullptr;  // development: k_map1 phase clocks (skq_session_set_stamps)
+    // side stream for the totals (k_bin_sum runs beside the slow paths), created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork{}, ev_join{};
 };
 
 int skq::session_device(const skq_session* s) { return s->idx->device; }
@@ -647,6 +650,12 @@ int skq_session_free(skq_session* s) {
         (void)hipEventDestroy(t.start);
         (void)hipEventDestroy(t.stop);
     }
+    if (s->side) {
+        (void)hipStreamSynchronize(s->side);
+        (void)hipStreamDestroy(s->side);
+        (void)hipEventDestroy(s->ev_fork);
+        (void)hipEventDestroy(s->ev_join);
+    }
     dev_free(s->status);
     dev_free(s->hash_cnt);
     dev_free(s->hashes);
@@ -745,6 +754,43 @@ int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_off
     return sketch_impl(s, d_seqs, d_offs, fixed_len, n_seqs, max_len, threshold, 1, stream);
 }
 
+// The tail of a chain: the slow chain path (after the slow sketch path, when given) and the
+// per-transcript totals. When the count kernel binned the fast reads' candidates, k_bin_sum only
+// reads those bins and adds into tx_acc, as k_chain_slow does for its reads: it runs on the
+// session's side stream beside the slow paths, and the fold waits for both.
+static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
+                      hipStream_t st) {
+    const bool fork = accumulate && p.slow_totals && s->variant != 14;
+    hipEvent_t t0{};
+    if (fork) {
+        if (!s->side) {
+            HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(s->ev_fork, st));
+        HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+        record(s, 3, &t0, s->side);
+        if (skq::launch_bin(p, 1, s->side)) return fail(-3, "totals launch failed");
+        record_stop(s, 3, t0, s->side);
+        HIP_TRY(hipEventRecord(s->ev_join, s->side));
+    }
+    if (sp && skq::launch_sketch_slow(*sp, st)) return fail(-3, "sketch slow-path launch failed");
+    if (skq::launch_chain_slow(p, st)) return fail(-3, "chain slow-path launch failed");
+    if (accumulate) {
+        if (fork) {
+            HIP_TRY(hipStreamWaitEvent(st, s->ev_join, 0));
+        } else {
+            record(s, 3, &t0, st);
+            if (skq::launch_bin(p, p.slow_totals, st)) return fail(-3, "totals launch failed");
+            record_stop(s, 3, t0, st);
+        }
+        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, st))
+            return fail(-3, "totals fold launch failed");
+    }
+    return 0;
+}
+
 static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const uint32_t* hash_cnt,
                       const uint32_t* hashes, const uint64_t* hash_offs, const uint8_t* present,
                       uint32_t hcap, double fraction, int accumulate, bool probed, void* stream,
@@ -817,15 +863,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     record(s, 2, &t0, st);
     if (skq::launch_count(p, stream)) return fail(-3, "count launch failed");
     record_stop(s, 2, t0, st);
-    if (skq::launch_chain_slow(p, stream)) return fail(-3, "chain slow-path launch failed");
-    if (accumulate) {
-        record(s, 3, &t0, st);
-        if (skq::launch_bin(p, p.slow_totals, stream))
-            return fail(-3, "totals launch failed");
-        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, ix->ntx, stream))
-            return fail(-3, "totals fold launch failed");
-        record_stop(s, 3, t0, st);
-    }
+    if (int rc = chain_tail(s, nullptr, p, accumulate, st)) return rc;
     s->have_chain = true;
     return 0;
 }
@@ -867,15 +905,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     record(s, 0, &t0, st);
     if (int rc = skq::launch_map1(sp, cp, stream)) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
     record_stop(s, 0, t0, st);
-    if (skq::launch_sketch_slow(sp, stream)) return fail(-3, "sketch slow-path launch failed");
-    if (skq::launch_chain_slow(cp, stream)) return fail(-3, "chain slow-path launch failed");
-    if (accumulate) {
-        record(s, 3, &t0, st);
-        if (skq::launch_bin(cp, cp.slow_totals, stream)) return fail(-3, "totals launch failed");
-        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, stream))
-            return fail(-3, "totals fold launch failed");
-        record_stop(s, 3, t0, st);
-    }
+    if (int rc = chain_tail(s, &sp, cp, accumulate, st)) return rc;
     s->have_chain = true;
     return 0;
 }
