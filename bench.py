@@ -167,10 +167,11 @@ def main():
         # binned candidates in (4 B each), per-transcript sums out (amortised: 16 B x ntx / n)
         "totals": 4 * Cn + 16.0 * tx.ntx / n,
     }
+    fused_name = "k_map1" if nk == 1 else "k_mapk"  # (k_mapk: 2..4 k slots)
     if map1:  # the fused kernel: read in, one lookup per hash, postings, hashes + candidates out
-        b_kern = {"k_map1": L + 1 + 4 * nk + 4 * h + 8 * h + b_chain, "totals": b_kern["totals"]}
+        b_kern = {fused_name: L + 1 + 4 * nk + 4 * h + 8 * h + b_chain, "totals": b_kern["totals"]}
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
-    names = ("k_map1" if map1 else "k_sketch", "k_probe", count_name, "totals")
+    names = (fused_name if map1 else "k_sketch", "k_probe", count_name, "totals")
     avg = {name: ms / cnt for name, (ms, cnt) in zip(names, kt) if cnt}
     kname = max(avg, key=avg.get)                       # dominant kernel
     achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
@@ -224,7 +225,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname],
                          "requests": requests},
-            "path": {"bytes_per_read": b_path, "probe": ("k_map1 (sketch + wide-entry gathers + count fused)" if map1 else
+            "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + wide-entry gathers + count fused)" if map1 else
                                                 "fused in k_sketch" if fused else "k_probe"),
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
                      "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,

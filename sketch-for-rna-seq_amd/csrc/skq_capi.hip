@@ -875,17 +875,20 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
                       fraction, accumulate, s->probed, stream);
 }
 
-// Fused map (k_map1): wide tables, one k slot, a raw capacity of 16 or 32 (variant 6 and the
-// sketch-side timing variants take the two-kernel path)
+// Fused map: k_map1 (wide or block tables, one k slot, a raw capacity of 16 or 32) or k_mapk
+// (wide tables, 2..4 k slots, capacity 16); variant 6 and the sketch-side timing variants take
+// the two-kernel path
 static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,
                         uint32_t threshold) {
     const skq_index* ix = s->idx;
-    if ((ix->mode != 3 && ix->mode != 4) || ix->nk != 1) return false;
     if (s->variant == 1 || s->variant == 2 || s->variant == 4 || s->variant == 6) return false;
     if (!d_offs) max_len = fixed_len;
     const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
     const uint32_t hcap = pick_hcap(Lc, ix->mink, threshold);
-    return hcap == 16 || hcap == 32;
+    if (ix->nk == 1) return (ix->mode == 3 || ix->mode == 4) && (hcap == 16 || hcap == 32);
+    // 2..4 k slots: k_mapk (wide tables, hcap 16 or 32); variants 13 and 15 keep k_sketch + count (A/B)
+    return ix->mode == 3 && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32) && s->variant != 13 &&
+           s->variant != 15;
 }
 
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
@@ -903,7 +906,8 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
     hipEvent_t t0{};
     record(s, 0, &t0, st);
-    if (int rc = skq::launch_map1(sp, cp, stream)) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
+    const int rc = s->idx->nk == 1 ? skq::launch_map1(sp, cp, stream) : skq::launch_mapk(sp, cp, stream);
+    if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
     record_stop(s, 0, t0, st);
     if (int rc = chain_tail(s, &sp, cp, accumulate, st)) return rc;
     s->have_chain = true;

@@ -175,6 +175,8 @@ int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream);
 // fused sketch + chain (k_map1: quant mode, one k slot, wide tables, hcap 16 or 32; -4 otherwise)
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
+// fused sketch + chain for 2..4 k slots (k_mapk: wide tables, hcap 16 or 32; -4 otherwise)
+int launch_mapk(const SketchParams& p, const ChainParams& cp, void* stream);
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream);

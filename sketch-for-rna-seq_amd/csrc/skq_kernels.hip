@@ -1594,38 +1594,19 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
 // slot), slot s of read o in column (o + s) & 63 of the wave (distinct LDS banks). Then the
 // filter of src/sparse_chaining.cpp:76-110 at every k, the candidates, and the binning epilogue.
 // Reads with more than TS distinct transcripts go to the slow chain path, as in k_count3.
-constexpr uint32_t CW_P = 512;
+// The count phase over wide tables for 2..4 k slots, one wave (k_countw, k_mapk): read r's
+// cnts[i] retained hashes of k slot i are at lofs (cnts zero for reads not counted); the wave's
+// hashes are listed at hl / ow in passes of `cap`; lane pairs gather the entries and insert into
+// the per-read tables in the wave's columns of the 2 * TS rows at colbase (tid words EMPTY and
+// count words 0 on entry); flagw (the wave's 64 words, zeroed) marks reads with more than TS
+// transcripts. Writes each counted read's candidates, or lists it for the slow chain path;
+// returns the candidate count, key[] holding them in output order. Every lane must call it.
 template <int NK>
-__global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
-    static_assert(NK >= 2 && NK <= NK_FAST, "2..4 k slots (8-bit counts packed per k)");
-    static_assert(2 * TS >= CCAP, "the binned region reuses the count tables");
-    __shared__ __attribute__((aligned(16))) uint32_t s_tabs[2 * TS * WG];
-    __shared__ uint32_t s_hl[WG / 64][CW_P];
-    __shared__ uint8_t s_ow[WG / 64][CW_P];
-    __shared__ uint32_t s_flag[WG];
-    __shared__ uint32_t s_bc[WG + 1];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint64_t r = (uint64_t)blockIdx.x * WG + t;
-    const bool inb = r < p.n;
-    const uint64_t rr = inb ? r : p.n - 1;  // (p.n > 0)
-    const bool bin = p.accumulate && p.bin_nb;  // uniform
+__device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64_t r, uint64_t rr, bool act,
+                                                    uint32_t (&cnts)[NK], uint32_t* colbase, uint32_t* hl,
+                                                    uint8_t* ow, uint32_t cap, uint32_t* flagw, uint32_t lane,
+                                                    uint32_t (&key)[TS]) {
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
-#pragma unroll
-    for (int sl = 0; sl < TS; ++sl) {
-        s_tabs[(2 * sl) * WG + t] = EMPTY;
-        s_tabs[(2 * sl + 1) * WG + t] = 0;
-    }
-    s_flag[t] = 0;
-    if (bin) s_bc[t] = 0;
-    // the read's status, slow flag and per-k counts (as count_read)
-    const uint32_t st = p.status[rr], pf = p.pflag[rr];
-    uint32_t cnts[NK];
-#pragma unroll
-    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, rr, i);
-    const bool ok = inb && (st & SKQ_STATUS_MASK) == SKQ_READ_OK;
-    if (ok && pf) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
-    const bool act = ok && !pf;
-    if (inb && !act) p.cand_cnt[r] = 0;
     uint32_t m = 0;
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
@@ -1635,7 +1616,6 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
     const uint32_t incl = wave_incl_scan(m, lane);
     const uint32_t off = incl - m;
     const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes, all k slots
-    uint32_t* colbase = s_tabs + wv * 64;
     const bool odd = lane & 1u;
     auto wd_of = [&](uint32_t i) -> const uint32_t* {
         const uint32_t* w = p.wdir[0];
@@ -1662,7 +1642,7 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
                 return;
             }
         }
-        atomicOr(&s_flag[wv * 64 + o], 1u);  // more than TS distinct transcripts
+        atomicOr(&flagw[o], 1u);  // more than TS distinct transcripts
     };
     auto ins = [&](uint32_t x, uint32_t o, uint32_t inc) {
         const uint32_t sl = Counter<1, WG>::slot_of(x), c = (o + sl) & 63u;
@@ -1677,8 +1657,7 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) hx[i][u] = (uint32_t)u < cnts[i] ? src[(uint64_t)u * p.n] : 0u;
     }
-    __syncthreads();
-    for (uint32_t pb = 0; pb < M; pb += CW_P) {  // wave-uniform
+    for (uint32_t pb = 0; pb < M; pb += cap) {  // wave-uniform
         // this lane's entries that fall in the pass, straight from the sketch's hash rows: the
         // first 8 of every k slot in one round trip (all loads issued before any store), the
         // rest (reads with more than 8 at a k) 8 at a time
@@ -1689,9 +1668,9 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const uint32_t ee = e + u;
-                    if ((uint32_t)u < cnts[i] && ee >= pb && ee < pb + CW_P) {
-                        s_hl[wv][ee - pb] = hx[i][u];
-                        s_ow[wv][ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
+                    if ((uint32_t)u < cnts[i] && ee >= pb && ee < pb + cap) {
+                        hl[ee - pb] = hx[i][u];
+                        ow[ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
                     }
                 }
                 e += cnts[i];
@@ -1711,9 +1690,9 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const uint32_t ee = e + j0 + u;
-                        if (j0 + u < c && ee >= pb && ee < pb + CW_P) {
-                            s_hl[wv][ee - pb] = x[u];
-                            s_ow[wv][ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
+                        if (j0 + u < c && ee >= pb && ee < pb + cap) {
+                            hl[ee - pb] = x[u];
+                            ow[ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
                         }
                     }
                 }
@@ -1723,7 +1702,7 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t ne = min(M - pb, CW_P);
+        const uint32_t ne = min(M - pb, cap);
         constexpr int R = 4;  // rounds of 32 entries in flight together
         for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
             uint4 w[R];
@@ -1733,8 +1712,8 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
             for (int u = 0; u < R; ++u) {
                 const uint32_t ee = e0 + 32 * u + (lane >> 1);
                 const bool in = ee < ne;
-                const uint32_t h = s_hl[wv][in ? ee : 0];
-                own[u] = s_ow[wv][in ? ee : 0];
+                const uint32_t h = hl[in ? ee : 0];
+                own[u] = ow[in ? ee : 0];
                 const uint32_t i = own[u] >> 6;
                 okk[u] = in && h < wlen_of(i);
                 w[u] = *reinterpret_cast<const uint4*>(wd_of(i) + (okk[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
@@ -1781,10 +1760,9 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    uint32_t key[TS];
     uint32_t nc = 0;
     if (act) {
-        if (s_flag[t] == 0) {
+        if (flagw[lane] == 0) {
             // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
             uint32_t tx[TS], cx[TS], mx[NK] = {};
 #pragma unroll
@@ -1833,6 +1811,45 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
             p.cand_cnt[r] = 0;
         }
     }
+    return nc;
+}
+
+constexpr uint32_t CW_P = 512;
+template <int NK>
+__global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
+    static_assert(NK >= 2 && NK <= NK_FAST, "2..4 k slots (8-bit counts packed per k)");
+    static_assert(2 * TS >= CCAP, "the binned region reuses the count tables");
+    __shared__ __attribute__((aligned(16))) uint32_t s_tabs[2 * TS * WG];
+    __shared__ uint32_t s_hl[WG / 64][CW_P];
+    __shared__ uint8_t s_ow[WG / 64][CW_P];
+    __shared__ uint32_t s_flag[WG];
+    __shared__ uint32_t s_bc[WG + 1];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint64_t r = (uint64_t)blockIdx.x * WG + t;
+    const bool inb = r < p.n;
+    const uint64_t rr = inb ? r : p.n - 1;  // (p.n > 0)
+    const bool bin = p.accumulate && p.bin_nb;  // uniform
+    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+#pragma unroll
+    for (int sl = 0; sl < TS; ++sl) {
+        s_tabs[(2 * sl) * WG + t] = EMPTY;
+        s_tabs[(2 * sl + 1) * WG + t] = 0;
+    }
+    s_flag[t] = 0;
+    if (bin) s_bc[t] = 0;
+    // the read's status, slow flag and per-k counts (as count_read)
+    const uint32_t st = p.status[rr], pf = p.pflag[rr];
+    uint32_t cnts[NK];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) cnts[i] = hash_count(p, rr, i);
+    const bool ok = inb && (st & SKQ_STATUS_MASK) == SKQ_READ_OK;
+    if (ok && pf) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+    const bool act = ok && !pf;
+    if (inb && !act) p.cand_cnt[r] = 0;
+    uint32_t key[TS];
+    __syncthreads();  // (the tables, flags and binning counts above are set)
+    const uint32_t nc = wide_count_wave<NK>(p, r, rr, act, cnts, s_tabs + wv * 64, s_hl[wv], s_ow[wv], CW_P,
+                                            s_flag + wv * 64, lane, key);
     // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
     if (bin) bin_candidates(p, t, blockIdx.x, nc, key, s_bc, s_tabs);
 }
@@ -2307,6 +2324,222 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(5);
 }
 
+// Fused map kernel for 2..4 k slots over wide tables (the multi-k quant path): k_map1's staging
+// and validity, the ntHash roll of every k slot (each sorted retained set written out as k_sketch
+// writes it), then wide_count_wave over those sets (read back while they are still in L2) and the
+// binning epilogue, so the gathers of some waves overlap the hashing of others. LDS: the roll
+// terms; per wave the staged codes (the count phase's hash list once every lane has hashed);
+// max(HCAP + 1, 2 * TS) rows of WG words (the bad-chunk bits in row 0 of the wave's columns,
+// then the raw windows, then the count tables); per-read overflow flags; the binning counts.
+__host__ __device__ inline size_t mapk_wave_bytes(uint32_t wc) {
+    const size_t a = sketch_codes_bytes(wc), b = (size_t)128 * 5;  // >= 128 list entries a pass
+    return ((a > b ? a : b) + 15) & ~(size_t)15;
+}
+
+__host__ __device__ constexpr uint32_t mapk_rows(uint32_t hcap) { return hcap + 1 > 2 * TS ? hcap + 1 : 2 * TS; }
+
+size_t mapk_lds_bytes(uint32_t nk, uint32_t wave_chunks, uint32_t hcap) {
+    return sketch_tab_bytes(nk) + (WG / 64) * mapk_wave_bytes(wave_chunks) + (size_t)mapk_rows(hcap) * WG * 4 +
+           (size_t)WG * 4 + (size_t)(WG + 1) * 4;
+}
+
+template <int NK, int HCAP>
+__global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    const uint32_t wc = p.tile_chunks;  // chunks per wave
+    const size_t wave_bytes = mapk_wave_bytes(wc);
+    uint2* s_tab = reinterpret_cast<uint2*>(smem);
+    const uint2* s_seed = s_tab + NK * 16;
+    unsigned char* s_wave = smem + sketch_tab_bytes(NK) + wv * wave_bytes;
+    uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
+    uint32_t* s_rows = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(NK) + (WG / 64) * wave_bytes);
+    uint32_t* s_flag = s_rows + mapk_rows(HCAP) * WG;
+    uint32_t* s_bc = s_flag + WG;
+    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_rows + wv * 64);  // (row 0 of the wave's columns)
+    const bool bin = cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
+    for (uint32_t e = tid; e < NK * 16 + 4; e += WG) {
+        const uint64_t v = p.rolltab[e];
+        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
+    }
+    s_flag[tid] = 0;
+    s_bc[tid] = 0;
+    __syncthreads();
+
+    const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
+    const uint32_t nr = r0 < p.n ? (uint32_t)min((uint64_t)64, p.n - r0) : 0u;  // wave-uniform
+    const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
+    const uintptr_t abase = base & ~(uintptr_t)15;
+    const uint64_t delta = base - abase;
+    uint64_t c0 = 0;
+    uint32_t nch = 0;
+    if (nr) {
+        uint64_t s0, l0, sl, ll;
+        read_extent(p.offs, p.fixed_len, r0, s0, l0);
+        read_extent(p.offs, p.fixed_len, r0 + nr - 1, sl, ll);
+        c0 = (s0 + delta) >> 4;
+        const uint64_t c1 = (sl + ll + delta + 15) >> 4;
+        nch = (uint32_t)min((uint64_t)wc, c1 - c0);
+        const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
+        constexpr uint32_t SU = 10;
+        for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
+            uint4 vv[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * 64, nch - 1)];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; ++u) {
+                const uint32_t c = cb + u * 64;
+                const uint4 v = vv[u];
+                const uint32_t cs = c < nch ? c : wc + 1;
+                const uint32_t ta = (v.x >> 1) & 0x03030303u, tb = (v.y >> 1) & 0x03030303u;
+                const uint32_t tc = (v.z >> 1) & 0x03030303u, td = (v.w >> 1) & 0x03030303u;
+                constexpr uint32_t W4 = 0x40100401u;
+                const uint32_t code = __builtin_amdgcn_udot4(ta, W4, 0u, false) |
+                                      (__builtin_amdgcn_udot4(tb, W4, 0u, false) << 8) |
+                                      (__builtin_amdgcn_udot4(tc, W4, 0u, false) << 16) |
+                                      (__builtin_amdgcn_udot4(td, W4, 0u, false) << 24);
+                constexpr uint32_t GTCA = 0x47544341u;
+                const uint32_t x = (__builtin_amdgcn_perm(0u, GTCA, ta) ^ v.x) | (__builtin_amdgcn_perm(0u, GTCA, tb) ^ v.y) |
+                                   (__builtin_amdgcn_perm(0u, GTCA, tc) ^ v.z) | (__builtin_amdgcn_perm(0u, GTCA, td) ^ v.w);
+                s_codes[cs] = code;
+                const uint64_t wbits = __ballot(x != 0);
+                if (lane == 0 && c < nch) s_badw[c >> 6] = wbits;
+            }
+        }
+        if (lane == 0) s_codes[nch] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    const bool live = lane < nr;
+    const uint64_t r = live ? r0 + lane : 0;
+    uint64_t start = 0, len = 0;
+    if (live) read_extent(p.offs, p.fixed_len, r, start, len);
+    const uint64_t q0 = start + delta - c0 * 16;
+    bool slow = live && (len > (uint64_t)LFAST || q0 + len > (uint64_t)nch * 16);
+    uint8_t st = SKQ_READ_OK;
+    if (live && !slow) {
+        // is_valid_sequence (src/data_io.cpp:17-34), as in k_sketch
+        bool bad = false;
+        if (len) {
+            const uint32_t ca = (uint32_t)(q0 >> 4), cz = (uint32_t)((q0 + len - 1) >> 4);
+            for (uint32_t wd = ca >> 6; wd <= (cz >> 6); ++wd) {
+                uint64_t m = s_badw[wd];
+                const uint32_t lo = wd == (ca >> 6) ? (ca & 63) : 0u, hi = wd == (cz >> 6) ? (cz & 63) : 63u;
+                m &= (hi == 63 ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+                bad |= m != 0;
+            }
+            if (bad) {
+                bad = false;
+                const uint8_t* rb = p.reads + start;
+                for (uint64_t q = 0; q < len; ++q) {
+                    const uint8_t ch = rb[q];
+                    bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+                }
+            }
+        }
+        if (bad) st = SKQ_READ_INVALID;
+        else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
+    }
+
+    uint32_t cnts[NK];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) cnts[i] = 0;
+    const bool hashing = live && !slow && st == SKQ_READ_OK;
+    if (hashing) {
+        const uint32_t T = p.threshold;
+        const uint32_t L = (uint32_t)len;
+        auto codes16 = [&](uint32_t q) -> uint32_t {
+            const uint32_t d = q >> 4;
+            return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
+        };
+        uint32_t* raw = s_rows + tid;
+#pragma unroll 1
+        for (int i = 0; i < NK; ++i) {
+            const uint32_t k = p.ks[i];
+            const uint2* tab = s_tab + i * 16;
+            uint32_t hlo = 0, hhi = 0;
+            for (uint32_t b = 0; b < k; b += 16) {
+                const uint32_t w = codes16((uint32_t)q0 + b);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (b + j < k) roll33b(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
+            }
+            raw[0] = hlo;
+            uint32_t nraw = hlo <= T ? 1u : 0u;  // src/sketch.cpp:33-35
+            const uint32_t nw = L - k + 1;
+            const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
+            for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
+                const uint32_t win = codes16(qin + w0 - 1);
+                const uint32_t wout = codes16(qout + w0 - 1);
+                const uint32_t jn = nw - w0;
+                uint2 e[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) e[j] = tab[((win >> (2 * j)) & 3u) * 4 + ((wout >> (2 * j)) & 3u)];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    roll33b(hlo, hhi, e[j]);
+                    const bool rec = hlo <= T && (uint32_t)j < jn;
+                    raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
+                    nraw += rec ? 1u : 0u;
+                }
+            }
+            if (nraw > HCAP) {
+                slow = true;
+                break;
+            }
+            // set semantics: sort, drop repeats; SoA rows as k_sketch writes them
+            uint32_t v[HCAP];
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_rows[j * WG + tid] : 0xFFFFFFFFu;
+            bitonic_sort<HCAP>(v);
+            uint32_t* out = p.hashes + (uint64_t)i * p.hcap * p.n + r;
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j)
+                if ((uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1])) out[(uint64_t)(m++) * p.n] = v[j];
+            p.hash_cnt[(uint64_t)i * p.n + r] = m;
+            cnts[i] = m;
+        }
+    }
+    if (live) {
+        if (slow) {
+            st = ST_SLOW1;
+            list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
+            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+        } else if (st != SKQ_READ_OK) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
+        }
+        p.status[r] = st;
+        p.pflag[r] = slow ? 1 : 0;  // (a later skq_chain on these results reads it)
+    }
+    const bool act = hashing && !slow;
+    if (!act) {
+#pragma unroll
+        for (int i = 0; i < NK; ++i) cnts[i] = 0;
+    }
+    if (live && !act) cp.cand_cnt[r] = 0;
+    // every lane of the wave has hashed: this wave's columns of the rows become its count tables,
+    // its staged codes the hash list
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int rw = 0; rw < 2 * TS; ++rw) s_rows[rw * WG + tid] = (rw & 1) ? 0u : 0xFFFFFFFFu;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t cap = (uint32_t)(wave_bytes / 5) & ~31u;  // list entries a pass: hashes, then owners
+    uint32_t key[TS];
+    const uint32_t nc = wide_count_wave<NK>(cp, r, r, act, cnts, s_rows + wv * 64, reinterpret_cast<uint32_t*>(s_wave),
+                                            s_wave + (size_t)cap * 4, cap, s_flag + wv * 64, lane, key);
+    // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
+    if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_rows);
+}
+
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
 // LDS (global scratch beyond SLOW_CAP), sorted, and counted per transcript run.
 __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
@@ -2771,6 +3004,31 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
         if (cp.wide == 2) hipLaunchKernelGGL((k_map1<32, 4, true>), grid, dim3(WG), lds, st, p, cp);
         else hipLaunchKernelGGL((k_map1<32, 4, false>), grid, dim3(WG), lds, st, p, cp);
         break;
+    default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_mapk(const SketchParams& p, const ChainParams& cp, void* stream) {
+    if (p.n == 0) return 0;
+    if (p.hcap != 16 && p.hcap != 32) return -4;
+    const dim3 grid((unsigned)((p.n + WG - 1) / WG));
+    const size_t lds = mapk_lds_bytes(p.nk, p.tile_chunks, p.hcap);
+    if (lds > 160 * 1024) return -4;
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    auto go = [&](auto kern) {
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+        hipLaunchKernelGGL(kern, grid, dim3(WG), lds, st, p, cp);
+    };
+    switch (p.nk * 100 + p.hcap) {
+    case 216: go(k_mapk<2, 16>); break;
+    case 316: go(k_mapk<3, 16>); break;
+    case 416: go(k_mapk<4, 16>); break;
+    case 232: go(k_mapk<2, 32>); break;
+    case 332: go(k_mapk<3, 32>); break;
+    case 432: go(k_mapk<4, 32>); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -25,6 +25,7 @@ ap.add_argument("--variants", default="0", help="chain kernel variants to A/B (0
 ap.add_argument("--pipeline", type=int, default=0, help="also time N batches on two alternating streams")
 ap.add_argument("--stamps", action="store_true", help="k_map1 per-wave phase clocks of one launch")
 ap.add_argument("--pipe-variant", type=int, default=0, help="variant the pipelined batches use")
+ap.add_argument("--acc-all", action="store_true", help="time every variant with totals accumulated too")
 a = ap.parse_args()
 ks = [int(x) for x in a.ks.split(",")]
 t0 = time.time()
@@ -47,7 +48,7 @@ def run_variant(v, acc):
 
 variants = {}
 for v in [int(x) for x in a.variants.split(",")]:
-    if v == 0:
+    if v == 0 or a.acc_all:
         variants["v%d+acc" % v] = run_variant(v, True)
     variants["v%d" % v] = run_variant(v, False)
 res = {k: [] for k in variants}
