@@ -42,7 +42,7 @@ void print_help(const std::string& prog) {
               << "Quant mode usage:\n"
               << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
               << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_BATCH (reads per batch),\n"
-              << "             SKQ_CHUNK_MB (FASTQ bytes per device chunk, default 256).\n";
+              << "             SKQ_CHUNK_MB (FASTQ MiB per device chunk, default 64).\n";
 }
 
 const float kSketchSize = 0.05f;  // src/main.cpp:43
@@ -94,7 +94,7 @@ void quantification(const std::string& index_path, const std::string& reads_path
     skq_index* ix = nullptr;
     check(skq_index_from_tables(device(), ntx, nk, ks, tabs, &ix), "device index");
 
-    uint64_t batch = 1u << 22;
+    uint64_t batch = 1u << 21;  // reads per batch (2M and 64-MiB chunks: tools/ingest_bench.py sweep)
     if (const char* e = std::getenv("SKQ_BATCH")) batch = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     skq_session* s = nullptr;
     check(skq_session_create(ix, batch, 256, &s), "session");

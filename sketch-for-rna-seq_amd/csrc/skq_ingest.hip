@@ -570,7 +570,7 @@ int skq_ingest_open(skq_session* s, const char* path, uint64_t chunk_bytes, int 
     g->s = s;
     g->device = skq::session_device(s);
     g->max_reads = skq::session_max_reads(s);
-    g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (256ull << 20), 1u << 12);
+    g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (64ull << 20), 1u << 12);  // (64 MiB: tools/ingest_bench.py sweep)
     g->io_threads = io_threads > 0 ? io_threads : 4;
     g->fd = ::open(path, O_RDONLY);
     if (g->fd < 0) {

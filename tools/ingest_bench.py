@@ -45,9 +45,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--ntx", type=int, default=200_000)
-    ap.add_argument("--chunk", type=int, default=256, help="MiB per chunk")
+    ap.add_argument("--chunk", type=int, default=64, help="MiB per chunk")
     ap.add_argument("--io-threads", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=4_000_000, help="session max_reads")
+    ap.add_argument("--batch", type=int, default=2_000_000, help="session max_reads")
     ap.add_argument("--export", action="store_true", help="copy every batch's candidates to the host")
     ap.add_argument("--em", action="store_true",
                     help="quant end to end: candidates appended on the device, EM (20 rounds) + assignment")
