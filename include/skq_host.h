@@ -114,7 +114,8 @@ int skq_em(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
            int nthreads, double* pi, int* iterations);
 /* The EM round split for read-sharded drivers (skq/dist.py; the GPU forms are skq_em_estep /
  * skq_em_mstep in skq.h): post[ntx] = posterior sums of these reads under pi; then, with post
- * summed over all shards, pi = (post + (double)(0.01f / R)) + (double)0.01f, *change = sum |d pi|. */
+ * summed over all shards, pi = (post + (double)(0.01f / R)) + (double)0.01f, *change = sum |d pi|.
+ * (skq_em_estep_host runs on the calling thread; nthreads is reserved.) */
 int skq_em_estep_host(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand_tid,
                       const uint32_t* cand_score, uint32_t ntx, const double* pi, int nthreads,
                       double* post);
