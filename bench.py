@@ -224,7 +224,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname],
-                         "requests": requests},
+                         "requests": requests,
+                         # the PMC bytes per launch over the same launch time: every random entry
+                         # gather moves a whole 128-B line
+                         "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None},
             "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + wide-entry gathers + count fused)" if map1 else
                                                 "fused in k_sketch" if fused else "k_probe"),
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
