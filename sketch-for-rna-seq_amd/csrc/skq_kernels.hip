@@ -1887,7 +1887,7 @@ size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
             cp.stamps[((uint64_t)blockIdx.x * (WG / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-template <int HCAP, int MB, bool BLK>
+template <int HCAP, int MB, bool BLK, bool NT = true>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1929,7 +1929,14 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
             uint4 vv[SU];
 #pragma unroll
-            for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * 64, nch - 1)];
+            for (uint32_t u = 0; u < SU; ++u)
+                if (NT) {  // (non-temporal: the streamed bases do not evict the entries' lines; +2 %)
+                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + min(cb + u * 64, nch - 1)));
+                    vv[u] = make_uint4(x.x, x.y, x.z, x.w);
+                } else {
+                    vv[u] = src[min(cb + u * 64, nch - 1)];
+                }
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u) {
                 const uint32_t c = cb + u * 64;
@@ -2386,7 +2393,11 @@ __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
         for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
             uint4 vv[SU];
 #pragma unroll
-            for (uint32_t u = 0; u < SU; ++u) vv[u] = src[min(cb + u * 64, nch - 1)];
+            for (uint32_t u = 0; u < SU; ++u) {  // (non-temporal, as k_map1)
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + min(cb + u * 64, nch - 1)));
+                vv[u] = make_uint4(x.x, x.y, x.z, x.w);
+            }
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u) {
                 const uint32_t c = cb + u * 64;
@@ -2998,6 +3009,7 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
         // (MB: gather rounds in flight; variant 11 = 8, a development A/B)
         if (cp.wide == 2) hipLaunchKernelGGL((k_map1<16, 4, true>), grid, dim3(WG), lds, st, p, cp);
         else if (cp.variant == 11) hipLaunchKernelGGL((k_map1<16, 8, false>), grid, dim3(WG), lds, st, p, cp);
+        else if (cp.variant == 17) hipLaunchKernelGGL((k_map1<16, 4, false, false>), grid, dim3(WG), lds, st, p, cp);
         else hipLaunchKernelGGL((k_map1<16, 4, false>), grid, dim3(WG), lds, st, p, cp);
         break;
     case 32:
