@@ -431,3 +431,31 @@ def test_very_long_reads_and_large_postings():
         out = run_gpu(gi, reads, thr=th)
         ref = oi.map_batch(reads, thr=th)
         compare(out, ref, len(reads), 1)
+
+
+@pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
+def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
+    """With wide tables, 2-4 k slots map through the fused k_mapk (no separate count launch);
+    every other probe structure through k_sketch + a count kernel. Both bit-exact."""
+    gi, oi = build(ks, tx=tx300)
+    bases, _, _ = synth.reads(tx300, 2000, read_len, seed=77, err=0.002)
+    reads = [bases[i * read_len:(i + 1) * read_len].tobytes() for i in range(2000)]
+    buf, offs = skq.pack_reads(reads)
+    s = skq.Session(gi, len(reads), read_len)
+    d_buf = skq.DeviceBuffer.from_numpy(buf)
+    s.enable_timing(True)
+    s.map(d_buf.ptr, None, len(reads), read_len, fixed_len=read_len)
+    s.check()
+    s.enable_timing(False)
+    count_launches = s.kernel_time(2)[1]
+    if probe_mode == "wide":
+        assert count_launches == 0 and s.kernel_time(0)[1] == 1
+    else:
+        assert count_launches == 1
+    out = s.export()
+    out["totals"] = s.totals()
+    ref = oi.map_batch(reads)
+    compare(out, ref, len(reads), len(ks))
+    tr, ts = totals_from(ref, len(reads), tx300.ntx)
+    np.testing.assert_array_equal(out["totals"][0], tr)
+    np.testing.assert_array_equal(out["totals"][1], ts)
