@@ -234,8 +234,6 @@ int skq_stream_sync(void* stream);
  * kind: 0 = k_sketch, 1 = k_probe, 2 = k_count, 3 = per-transcript totals (k_bin + k_bin_sum +
  * k_fold_totals). Used by bench.py for the roofline figure. */
 int skq_session_enable_timing(skq_session* s, int enable);
-/* Development A/B switch for the chain kernel (0 = default). Not needed by users. */
-int skq_session_set_variant(skq_session* s, int variant);
 /* Development: device buffer of 8 uint64 per wave of the fused map kernel that receives the
  * wave's phase clocks (s_memtime); NULL turns it off. Not needed by users. */
 int skq_session_set_stamps(skq_session* s, void* d_stamps);

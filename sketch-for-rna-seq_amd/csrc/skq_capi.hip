@@ -121,7 +121,6 @@ struct skq_session {
     const uint64_t* x_offs = nullptr;
     bool timing = false;
     std::vector<TimedLaunch> timed;
-    int variant = 0;
     uint64_t* stamps = nullptr;  // development: k_map1 phase clocks (skq_session_set_stamps)
     // side stream for the totals (k_bin_sum runs beside the slow paths), created on first use
     hipStream_t side = nullptr;
@@ -608,7 +607,6 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     s->cand_ext_cap = 1ull << 22;
     s->scratch_cap = 1ull << 24;
     const uint32_t hcap0 = pick_hcap(Lc, ix->mink, skq_threshold((double)0.05f));
-    if (const char* e = std::getenv("SKQ_VARIANT")) s->variant = std::atoi(e);  // development A/B
     int rc = 0;
     if ((rc = dev_alloc(&s->status, max_reads)) || (rc = dev_alloc(&s->hash_cnt, max_reads * ix->nk)) ||
         (rc = dev_alloc(&s->hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&s->ovf1, s->ovf_cap)) ||
@@ -722,7 +720,6 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     }
     p.lofs = s->lofs;
     p.pflag = s->pflag;
-    p.variant = s->variant;
     p.nthash = nthash;
     if (prep) {
         *prep = p;
@@ -762,7 +759,7 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
                       hipStream_t st) {
     // (small batches: the extra stream hand-offs cost more than the overlap gains: 1M reads ran
     // 12 % faster serial, 10M reads faster forked)
-    const bool fork = accumulate && p.slow_totals && s->variant != 14 && p.n >= (1u << 22);
+    const bool fork = accumulate && p.slow_totals && p.n >= (1u << 22);
     hipEvent_t t0{};
     if (fork) {
         if (!s->side) {
@@ -835,7 +832,6 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     // wide tables: the count kernel reads the sketch's hashes and gathers the entries itself
     p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 4 ? 2 : 0;
     if (p.wide) {
-        if (s->variant == 4) return fail(-1, "variant 4 (k_count) does not read wide tables");
         p.lofs = const_cast<uint32_t*>(hashes);
         for (uint32_t i = 0; i < ix->nk; ++i) {
             p.wdir[i] = ix->wdir[i];
@@ -843,7 +839,6 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
             p.wovf[i] = ix->wovf[i];
         }
     }
-    p.variant = s->variant;
     p.stamps = s->stamps;
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
@@ -878,19 +873,17 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
 }
 
 // Fused map: k_map1 (wide or block tables, one k slot, a raw capacity of 16 or 32) or k_mapk
-// (wide tables, 2..4 k slots, capacity 16); variant 6 and the sketch-side timing variants take
-// the two-kernel path
+// (wide tables, 2..4 k slots, capacity 16); anything else takes the two-kernel path (a caller
+// can always ask for that path itself with skq_sketch + skq_chain)
 static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,
                         uint32_t threshold) {
     const skq_index* ix = s->idx;
-    if (s->variant == 1 || s->variant == 2 || s->variant == 4 || s->variant == 6) return false;
     if (!d_offs) max_len = fixed_len;
     const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
     const uint32_t hcap = pick_hcap(Lc, ix->mink, threshold);
     if (ix->nk == 1) return (ix->mode == 3 || ix->mode == 4) && (hcap == 16 || hcap == 32);
-    // 2..4 k slots: k_mapk (wide tables, hcap 16 or 32); variants 13 and 15 keep k_sketch + count (A/B)
-    return ix->mode == 3 && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32) && s->variant != 13 &&
-           s->variant != 15;
+    // 2..4 k slots: k_mapk (wide tables, hcap 16 or 32)
+    return ix->mode == 3 && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32);
 }
 
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
@@ -904,7 +897,6 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         return rc;
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (s->variant == 12) cp.slow_totals = 0;  // development A/B: totals binned by k_bin afterwards
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
     hipEvent_t t0{};
     record(s, 0, &t0, st);
@@ -1111,12 +1103,6 @@ int skq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
 
 int skq_stream_sync(void* stream) {
     HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
-    return 0;
-}
-
-int skq_session_set_variant(skq_session* s, int variant) {
-    if (!s) return fail(-1, "null session");
-    s->variant = variant;
     return 0;
 }
 

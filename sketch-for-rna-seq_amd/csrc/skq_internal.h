@@ -93,7 +93,6 @@ struct SketchParams {
     const uint32_t* rovf[SKQ_MAX_K]; // list offsets of the 3rd+ key of a block
     uint32_t* lofs;
     uint8_t* pflag;
-    int variant;  // development A/B switch (0 = default)
     // ntHash mode (createSketch_FracMinhash_direct on arbitrary sequences, transcripts): no read
     // is rejected; windows holding a byte outside ACGTUacgtu are skipped (src/sketch.cpp:31-36
     // through ntHash); a k longer than the sequence yields an empty set for that k.
@@ -139,7 +138,6 @@ struct ChainParams {
     uint32_t* bin_hdr;
     uint32_t* bin_region;
     int slow_totals;
-    int variant;               // development A/B switch (0 = default)
     uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
     // wide direct tables (DESIGN.md "Index"): entry h of k slot i is 8 words at wdir[i] + 8h,
     // [n, t0..t6] for lists of n <= 7 transcripts, [0x80000000 | list offset, t0..t6] for longer

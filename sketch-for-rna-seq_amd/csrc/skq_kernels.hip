@@ -480,21 +480,14 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
                     // every gather issues (index 0 when there is nothing to probe) so all are in
                     // flight together; a guarded load would be waited for one at a time
                     const bool want = ((keepm >> j) & 1ull) && v[j] < dl;
-                    const uint32_t x = p.variant == 1 ? v[j] : dir[want ? v[j] : 0u];
+                    const uint32_t x = dir[want ? v[j] : 0u];
                     lo[j] = want ? x : ~0u;
                 }
                 uint32_t* lout = p.lofs + (uint64_t)i * p.hcap * p.n + r;
                 uint32_t mm = 0;
-                if (p.variant == 2) {
-                    uint32_t x = 0;
-#pragma unroll
-                    for (int j = 0; j < HCAP; ++j) x ^= lo[j];
-                    if (x == 0x12345678u) lout[0] = x;
-                } else {
 #pragma unroll
                 for (int j = 0; j < HCAP; ++j)
                     if ((keepm >> j) & 1ull) lout[(uint64_t)(mm++) * p.n] = lo[j];
-                }
             }
         }
     }
@@ -944,10 +937,6 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
         p.cand_cnt[r] = 0;  // not sketched (invalid or short read)
         return;
     }
-    if (p.variant >= 1 && p.variant <= 2) {  // sketch-side timing variants: lofs hold no offsets
-        p.cand_cnt[r] = 0;
-        return;
-    }
     if (pf) {  // flagged by k_probe / the fused sketch: the slow chain path takes it
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
         p.cand_cnt[r] = 0;
@@ -1110,13 +1099,12 @@ struct Counter {
     static constexpr int W = NK == 1 ? 1 : 2;
     uint32_t* tab;   // this lane's slot 0
     uint32_t* pend;  // this lane's parked item 0
-    bool one;        // development A/B (variant 5): single-slot insert
     uint32_t occ = 0;  // bit s: slot s holds a transcript
     uint32_t np = 0;   // parked items
 
-    __device__ Counter(uint32_t* t, uint32_t* pe, bool single) : tab(t), pend(pe), one(single) {}
+    __device__ Counter(uint32_t* t, uint32_t* pe) : tab(t), pend(pe) {}
     __device__ static uint32_t slot_of(uint32_t x) { return (x * 0x9E3779B1u) >> 28; }
-    __device__ uint32_t slot2_of(uint32_t x) const { return one ? slot_of(x) : (x * 0x85EBCA77u) >> 28; }
+    __device__ static uint32_t slot2_of(uint32_t x) { return (x * 0x85EBCA77u) >> 28; }
     __device__ uint32_t& at(uint32_t w) { return tab[w * WG]; }
 
     // transcript x gains rl at k slot i. Two candidate slots, checked in order (slots are never
@@ -1337,13 +1325,12 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
     for (int i = 0; i < NK; ++i) asm volatile("" : "+v"(cnts[i]));
 #pragma unroll
     for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(lv0[u]));
-    // (sketch-side timing variants 1 and 2: lofs hold no offsets)
-    const bool ok = inb && (st & SKQ_STATUS_MASK) == SKQ_READ_OK && p.variant != 1 && p.variant != 2;
+    const bool ok = inb && (st & SKQ_STATUS_MASK) == SKQ_READ_OK;
     if (ok && pf) list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
     const bool act = ok && !pf;
     if (inb && !act) p.cand_cnt[r] = 0;
     if (!COOP && !act) return 0;
-    Counter<NK, WG> c(&s_tab[0][t], &s_pend[0][t], p.variant == 5);
+    Counter<NK, WG> c(&s_tab[0][t], &s_pend[0][t]);
     // k slots expanded at compile time (an unrolled loop this size exceeds the unroller's limit,
     // and a rolled one would put cnts/lv0 in scratch)
     static_for<NK>([&](auto ic) {
@@ -1999,10 +1986,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
     for (int j = 0; j < HCAP; ++j) v[j] = 0xFFFFFFFFu;
     uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
-    // development timing variants (tools/kbench.py; results not valid): 8 skips the count
-    // phase, 9 gathers the entries without inserting them, 10 skips the hashing
-    const int var = cp.variant;
-    const bool hashing = live && !slow && st == SKQ_READ_OK && var != 10;
+    const bool hashing = live && !slow && st == SKQ_READ_OK;
     if (hashing) {
         const uint32_t T = p.threshold;
         const uint32_t L = (uint32_t)len;
@@ -2084,7 +2068,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
     const uint32_t incl = wave_incl_scan(m, lane);
     const uint32_t off = incl - m;
-    const uint32_t M = var == 8 ? 0u : __shfl(incl, 63, 64);  // the wave's retained hashes
+    const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
@@ -2232,13 +2216,6 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 own[u] = s_own[in ? e : 0];
                 ok[u] = in && h < wlen;
                 w[u] = *reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
-            }
-            if (var == 9) {
-                uint32_t dz = 0;
-#pragma unroll
-                for (int u = 0; u < R; ++u) dz ^= ok[u] ? (w[u].x ^ w[u].y ^ w[u].z ^ w[u].w) + own[u] : 0u;
-                if (dz == 0x9E3779B9u) atomicOr(s_flag + lane, 1u);
-                continue;
             }
             // the inserts of each entry: the four first attempts (a CAS at each tid's home slot)
             // are issued before any result is looked at, one LDS round trip; a tid already there
@@ -2866,7 +2843,7 @@ __global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* rea
 // ---------------------------------------------------------------------------------------------
 // launchers
 
-static bool use_count3(const ChainParams& p) { return p.ntx <= (1u << 22) && p.variant != 4; }
+static bool use_count3(const ChainParams& p) { return p.ntx <= (1u << 22); }
 
 bool count_bins(const ChainParams& p) { return use_count3(p) && p.nk <= (uint32_t)NK_FAST && p.bin_nb > 0; }
 
@@ -2910,8 +2887,7 @@ int launch_probe(const ChainParams& p, void* stream) {
 int launch_count(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    // k_count3 (32-bit sort keys) unless transcript ids need more than 22 bits; variant 4 forces
-    // the wide kernel for A/B timing
+    // k_count3 (32-bit sort keys) unless transcript ids need more than 22 bits
     if (use_count3(p)) {
         const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
         auto go = [&](auto mode) {
@@ -2924,9 +2900,8 @@ int launch_count(const ChainParams& p, void* stream) {
             default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, st, p); break;
             }
         };
-        // wide tables, 2..4 k slots: the entry-parallel count (variant 13: k_count3, A/B)
-        if (p.wide == 1 && p.nk >= 2 && p.nk <= (uint32_t)NK_FAST && p.status && !p.present && !p.hash_offs &&
-            p.variant != 13) {
+        // wide tables, 2..4 k slots: the entry-parallel count
+        if (p.wide == 1 && p.nk >= 2 && p.nk <= (uint32_t)NK_FAST && p.status && !p.present && !p.hash_offs) {
             switch (p.nk) {
             case 2: hipLaunchKernelGGL((k_countw<2>), grid, dim3(WG), 0, st, p); break;
             case 3: hipLaunchKernelGGL((k_countw<3>), grid, dim3(WG), 0, st, p); break;
@@ -3006,10 +2981,8 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (p.hcap) {
     case 16:
-        // (MB: gather rounds in flight; variant 11 = 8, a development A/B)
+        // (MB: gather rounds in flight)
         if (cp.wide == 2) hipLaunchKernelGGL((k_map1<16, 4, true>), grid, dim3(WG), lds, st, p, cp);
-        else if (cp.variant == 11) hipLaunchKernelGGL((k_map1<16, 8, false>), grid, dim3(WG), lds, st, p, cp);
-        else if (cp.variant == 17) hipLaunchKernelGGL((k_map1<16, 4, false, false>), grid, dim3(WG), lds, st, p, cp);
         else hipLaunchKernelGGL((k_map1<16, 4, false>), grid, dim3(WG), lds, st, p, cp);
         break;
     case 32:

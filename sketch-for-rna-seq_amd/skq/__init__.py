@@ -71,7 +71,6 @@ def lib():
             "skq_memcpy_d2h": (i32, [vp, vp, C.c_size_t, vp]),
             "skq_stream_sync": (i32, [vp]),
             "skq_session_enable_timing": (i32, [vp, i32]),
-            "skq_session_set_variant": (i32, [vp, i32]),
             "skq_session_set_stamps": (i32, [vp, vp]),
             "skq_session_kernel_time": (i32, [vp, i32, C.POINTER(dbl), C.POINTER(u64)]),
             "skq_tables_build": (i32, [u32, vp, vp, u32, vp, u32, i32, C.POINTER(vp)]),
@@ -287,9 +286,6 @@ class Session:
 
     def reset_totals(self, stream=None):
         _check(lib().skq_session_reset_totals(self.h, stream))
-
-    def set_variant(self, v):
-        _check(lib().skq_session_set_variant(self.h, int(v)))
 
     def set_stamps(self, d_ptr):
         """Development: k_map1 phase clocks into a device buffer of 8 u64 per wave (0 = off)."""

@@ -4,6 +4,7 @@ Every comparison is exact: retained-hash sets per (read, k), per-read status, an
 lists (tid, score) in the normalised order (score desc, tid asc).
 """
 import random
+import sys
 
 import numpy as np
 import pytest
@@ -13,19 +14,20 @@ import skq
 from skq import synth
 
 pytestmark = pytest.mark.gpu
+SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the wide-split mode)
 
 
-@pytest.fixture(autouse=True, params=["block", "wide", "wide-split", "dir", "bucket"])
+@pytest.fixture(autouse=True, params=["block", "wide", "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
     """Every test runs with each index probe structure: block tables and wide direct tables
     gathered by the count kernel, 4-B direct tables probed inside the sketch kernel, and the bucket table probed by
     k_probe (SKQ_DIRECT_MB=0)."""
     if request.param == "bucket":
         monkeypatch.setenv("SKQ_DIRECT_MB", "0")
-    elif request.param == "wide-split":  # wide tables through k_sketch + k_count3 (no fused map)
+    elif request.param == "wide-split":  # wide tables through skq_sketch + skq_chain (no fused map)
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
         monkeypatch.setenv("SKQ_PROBE", "wide")
-        monkeypatch.setenv("SKQ_VARIANT", "6")
+        monkeypatch.setattr(sys.modules[__name__], "SPLIT", True)
     else:
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
         monkeypatch.setenv("SKQ_PROBE", request.param)
@@ -60,8 +62,12 @@ def run_gpu(index, reads, fixed_len=0, fraction=0.9, thr=None, max_len=None):
     s = skq.Session(index, max(n, 1), max_len)
     d_buf = skq.DeviceBuffer.from_numpy(buf)
     d_offs = None if fixed_len else skq.DeviceBuffer.from_numpy(offs)
-    s.map(d_buf.ptr, d_offs.ptr if d_offs else None, n, max_len, fixed_len=fixed_len, thr=thr,
-          fraction=fraction)
+    if SPLIT:
+        s.sketch(d_buf.ptr, d_offs.ptr if d_offs else None, n, max_len, fixed_len=fixed_len, thr=thr)
+        s.chain(fraction=fraction)
+    else:
+        s.map(d_buf.ptr, d_offs.ptr if d_offs else None, n, max_len, fixed_len=fixed_len, thr=thr,
+              fraction=fraction)
     s.check()
     out = s.export()
     out["totals"] = s.totals()

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel timing of variants on one data set (development tool; interleaved rounds in one
-process, as the CDNA guide's methodology asks). Prints one line per variant."""
+"""Per-kernel timing of index layouts (probe modes) on one data set (development tool; interleaved
+rounds in one process, as the CDNA guide's methodology asks). Prints one line per layout."""
 import argparse
 import ctypes as C
 import os
@@ -21,53 +21,64 @@ ap.add_argument("--reads", type=int, default=10_000_000)
 ap.add_argument("--len", type=int, default=150)
 ap.add_argument("--ks", default="31")
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="0", help="chain kernel variants to A/B (0 = default)")
+ap.add_argument("--probes", default="auto", help="index layouts to A/B (SKQ_PROBE values; auto = default)")
 ap.add_argument("--pipeline", type=int, default=0, help="also time N batches on two alternating streams")
 ap.add_argument("--stamps", action="store_true", help="k_map1 per-wave phase clocks of one launch")
-ap.add_argument("--pipe-variant", type=int, default=0, help="variant the pipelined batches use")
-ap.add_argument("--acc-all", action="store_true", help="time every variant with totals accumulated too")
+ap.add_argument("--acc-all", action="store_true", help="time every layout with totals accumulated too")
 a = ap.parse_args()
 ks = [int(x) for x in a.ks.split(",")]
 t0 = time.time()
 tx = synth.transcriptome(a.ntx, seed=1)
 tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
-index = skq.Index(ks, tx.ntx, tables)
+indexes, sessions = {}, {}
+for pm in a.probes.split(","):
+    if pm == "auto":
+        os.environ.pop("SKQ_PROBE", None)
+    else:
+        os.environ["SKQ_PROBE"] = pm
+    indexes[pm] = skq.Index(ks, tx.ntx, tables)
+    print(pm, indexes[pm].stats(), flush=True)
+os.environ.pop("SKQ_PROBE", None)
 bases, _, _ = synth.reads(tx, a.reads, a.len, seed=1000, err=0.001)
 dev = torch.device("cuda", 0)
 d = torch.from_numpy(bases).to(dev)
-s = skq.Session(index, a.reads, a.len)
+for pm, ix in indexes.items():
+    sessions[pm] = skq.Session(ix, a.reads, a.len)
+pm0 = a.probes.split(",")[0]
+s, index = sessions[pm0], indexes[pm0]
 sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 print("setup %.1fs" % (time.time() - t0), flush=True)
 
-def run_variant(v, acc):
+def run_layout(sx, acc):
     def f():
-        s.set_variant(v)
-        s.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=acc)
+        sx.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=acc)
     return f
 
 
 variants = {}
-for v in [int(x) for x in a.variants.split(",")]:
-    if v == 0 or a.acc_all:
-        variants["v%d+acc" % v] = run_variant(v, True)
-    variants["v%d" % v] = run_variant(v, False)
+for pm, sx in sessions.items():
+    if pm == pm0 or a.acc_all:
+        variants[pm + "+acc"] = run_layout(sx, True)
+    variants[pm] = run_layout(sx, False)
 res = {k: [] for k in variants}
 for rnd in range(a.rounds + 1):
     for name, fn in variants.items():
-        s.enable_timing(True)
+        sx = sessions[name.split("+")[0]]
+        sx.enable_timing(True)
         torch.cuda.synchronize()
         t = time.perf_counter()
         fn()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t) * 1e3
-        s.enable_timing(False)
-        k1 = s.kernel_time(0)[0]
-        k2 = s.kernel_time(1)[0]
-        k3 = s.kernel_time(2)[0]
-        k4 = s.kernel_time(3)[0]
+        sx.enable_timing(False)
+        k1 = sx.kernel_time(0)[0]
+        k2 = sx.kernel_time(1)[0]
+        k3 = sx.kernel_time(2)[0]
+        k4 = sx.kernel_time(3)[0]
         if rnd:
             res[name].append((wall, k1, k2, k3, k4))
-print("slow reads (sketch, chain) of the last batch:", s.slow_reads())
+for pm, sx in sessions.items():
+    print(pm, "slow reads (sketch, chain) of the last batch:", sx.slow_reads())
 for name, v in res.items():
     v = np.array(v)
     med = np.median(v, axis=0)
@@ -81,8 +92,6 @@ if a.pipeline:
     st = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     ses = [s, s2]
     for acc in (True, False):
-        for sx in ses:
-            sx.set_variant(a.pipe_variant)
         best = 1e9
         for rnd in range(a.rounds + 1):
             torch.cuda.synchronize()
@@ -100,9 +109,8 @@ if a.pipeline:
 
 if a.stamps:
     nw = (a.reads + 255) // 256 * 4
-    for v in [int(x) for x in a.variants.split(",")]:
+    for v, s in sessions.items():
         buf = torch.zeros(nw * 8, dtype=torch.int64, device=dev)
-        s.set_variant(v)
         s.set_stamps(buf.data_ptr())
         for acc in (True, False):
             s.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=acc)
@@ -110,7 +118,7 @@ if a.stamps:
             st = buf.view(nw, 8).cpu().numpy().astype(np.int64)
             t0 = st[:, 0].min()
             span = st[:, 5 if acc else 4].max() - t0
-            print("stamps v%d acc=%d: span %d ticks; per-wave phase ticks (median / mean / p90):" % (v, acc, span))
+            print("stamps %s acc=%d: span %d ticks; per-wave phase ticks (median / mean / p90):" % (v, acc, span))
             names = ["stage", "hash+sort", "gather+insert", "filter+emit", "bin"]
             for i in range(4 + acc):
                 dd = st[:, i + 1] - st[:, i]
