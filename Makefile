@@ -13,6 +13,11 @@ oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
 
 .PHONY: oracle
 
+# the reference's own chain / EM / IO code, test-only (oracle/ref.mk; skipped without /root/reference)
+ref:
+	$(MAKE) -f oracle/ref.mk
+.PHONY: ref
+
 HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
 LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o \
             $(OUT)/obj/skq_io.o $(OUT)/obj/skq_ingest.o $(OUT)/obj/skq_em.o \
@@ -38,6 +43,6 @@ $(OUT)/skq: $(CSRC)/skq_cli.cpp $(OUT)/libskq.so include/skq.h include/skq_host.
 $(OUT)/skq_dropin_check: tests/dropin_check.cpp $(OUT)/libskq.so $(wildcard include/dropin/*.h)
 	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude/dropin $< -o $@ -L$(OUT) -lskq -Wl,-rpath,'$$ORIGIN'
 
-all: lib oracle $(OUT)/skq $(OUT)/skq_dropin_check
+all: lib oracle ref $(OUT)/skq $(OUT)/skq_dropin_check
 .PHONY: lib all
 .DEFAULT_GOAL := all

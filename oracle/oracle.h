@@ -8,9 +8,13 @@
  *   - the rolling hash is pinned by ntHash's own constant tables, read as data from the
  *     reference's prebuilt binary (tests/golden/nthash_tables.json) and by the known-answer
  *     vectors of SURVEY.md §8c;
- *   - sketch/threshold/chain/record semantics are restated from the reference source text and
- *     pinned end-to-end only by the edge-case fixture of SURVEY.md §8c (tests/golden/edge/).
- *   The reference itself is unbuildable here (it needs the absent third-party ntHash library).
+ *   - the chain (sparse_chain), EM, assignment and is_valid_sequence are pinned against the
+ *     reference's OWN code: /root/reference/src/{sparse_chaining,data_io,isoform_assignment}.cpp
+ *     compile unmodified here (oracle/ref.mk -> oracle/_ref/libref.so, harness
+ *     oracle/ref_harness.cpp) and tests/test_ref_pinned.py compares them with this file;
+ *   - the record rules are pinned by the edge-case fixture of SURVEY.md §8c (tests/golden/edge/).
+ *   Only the reference's kmer.cpp / sketch.cpp / main.cpp are unbuildable here: they need the
+ *   absent third-party ntHash library, and no stand-in for it is written.
  *
  * Third-party algorithm restated: bcgsc ntHash >= 2.3 (not vendored in the reference, version
  * not pinned by its build; identified from symbols in build/test):

@@ -387,6 +387,20 @@ def fasta_load(path):
         lib().skq_seqs_free(h)
 
 
+def csv_write(path, fasta_path, counts, assigned, pi):
+    """output_to_csv (src/data_io.cpp:133-152) through skq_csv_write, for the transcripts of
+    fasta_path (load_fasta order = dense ids)."""
+    h = C.c_void_p()
+    _check(lib().skq_fasta_load(str(fasta_path).encode(), C.byref(h)))
+    try:
+        c = np.ascontiguousarray(counts, np.float64)
+        a = np.ascontiguousarray(assigned, np.uint8)
+        p = np.ascontiguousarray(pi, np.float64)
+        _check(lib().skq_csv_write(str(path).encode(), h, _p(c), _p(a), _p(p)))
+    finally:
+        lib().skq_seqs_free(h)
+
+
 def legacy_index_read(path):
     """load_index (src/data_io.cpp:233-304): (ks, names, sequences, {k: (keys, offs, tids)})."""
     h = C.c_void_p()

@@ -140,6 +140,24 @@ class Index:
         lib().orc_index_export(self.h, i, ptr(keys), ptr(offs), ptr(tids))
         return keys[:nkeys], offs, tids[:npost]
 
+    def chain(self, sketches, fraction=CHAIN_FRACTION, present=None):
+        """orc_chain_read per read: sketches[r][i] = read r's hash set at k slot i (present[r][i]
+        False: no sketch at that k). Per read a list of (tid, score), score desc then tid asc."""
+        nk = len(self.ks)
+        out = []
+        cap = max(self.ntx, 1)
+        ot = np.zeros(cap, np.uint32)
+        os_ = np.zeros(cap, np.uint32)
+        for r, sk in enumerate(sketches):
+            arrs = [np.ascontiguousarray(np.array(list(sk[i]) or [0], np.uint32)) for i in range(nk)]
+            nh = np.array([len(sk[i]) for i in range(nk)], np.uint32)
+            pr = np.array([1 if (present is None or present[r][i]) else 0 for i in range(nk)], np.int32)
+            hp = (C.c_void_p * nk)(*[a.ctypes.data for a in arrs])
+            c = lib().orc_chain_read(self.h, hp, ptr(nh), ptr(pr), fraction, ptr(ot), ptr(os_), cap)
+            assert c != C.c_size_t(-1).value
+            out.append(list(zip(ot[:c].tolist(), os_[:c].tolist())))
+        return out
+
     def map_batch(self, reads, offs=None, thr=None, fraction=CHAIN_FRACTION, hcap=None, ccap=None):
         """reads: list of bytes (or a flat uint8 array + offs). Returns dict of numpy arrays."""
         thr = threshold() if thr is None else thr
