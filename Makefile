@@ -9,7 +9,7 @@ CXXFLAGS_COMMON := -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 
 oracle: oracle/liboracle.so
 oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
-	gcc -O2 -Wall -Wextra -std=c11 -fPIC -shared $< -o $@
+	gcc -O2 -Wall -Wextra -std=c11 -fPIC -shared -pthread $< -o $@
 
 .PHONY: oracle
 

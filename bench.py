@@ -1,25 +1,75 @@
 #!/usr/bin/env python3
 """bench.py — reads/s of the quant hot path (FracMinHash sketch + sparse chain) on MI355X.
 
-Workload (BASELINE.json configs[2], the metric's config): synthetic 150 bp forward-strand reads
-against a ~200k-transcript GENCODE-scale synthetic index, k = 31, sketch fraction (double)0.05f,
-chain fraction 0.9. One step = one pass of the hot path (k_sketch, k_probe, k_count, slow paths included)
-over one batch of `--reads` reads already resident in HBM, plus — when N > 1 — the one RCCL
-all-reduce of the per-transcript totals (reads, score) over xGMI.
+Workloads (BASELINE.json configs):
+  N = 1: cfg3 (the metric's config) — synthetic 10M x 150 bp reads vs a ~200k-transcript
+         GENCODE-scale synthetic index, k = 31, sketch fraction (double)0.05f, chain 0.9;
+  N > 1: cfg4 — 12.5M x 150 bp reads per GPU, so N = 8 processes the 100M reads of cfg4 per
+         step (weak scaling: reads per GPU fixed; N = 2 / 4 process 25M / 50M).
+One step = one pass of the hot path over one batch already resident in HBM (skq_map: the fused
+sketch + probe + count kernel, the slow paths and the per-transcript totals) plus, for N > 1, the
+one RCCL all-reduce of the per-transcript totals (reads, score) over xGMI.
 
-One process per GPU (torch.distributed.run); reads are sharded (each rank its own seeded batch,
-weak scaling), the index is replicated. rank 0 prints one JSON line.
+One process per GPU. `python bench.py --gpus N` with N > 1 and no torch.distributed environment
+starts its own N ranks (a child `python -m torch.distributed.run`, never an exec) and exits with
+their status; the driver may also launch it under torch.distributed.run itself. Reads are
+sharded (each rank its own seeded batch), the index is replicated; rank 0 prints one JSON line.
+
+After the timed steps (rank 0): the parity sample — the first --cpu-reads reads of the batch as
+FASTQ text through the CPU oracle (oracle/oracle.c, the checker), compared bit-exact with the GPU's
+statuses, retained-hash sets, candidate lists and per-transcript totals for the same reads; a
+mismatch exits non-zero. At N = 1 the same oracle runs are the CPU baseline (P threads and 1).
 """
 import argparse
-import ctypes as C
-import json
 import os
+import socket
+import subprocess
 import sys
-import time
 
-import numpy as np
-import torch  # first: libskq.so then binds to torch's HIP runtime (one runtime per process)
-import torch.distributed as dist
+
+def _args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=None, choices=["cfg2", "cfg3", "cfg4", "cfg5"],
+                    help="default: cfg3 at N = 1, cfg4 at N > 1")
+    ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
+    ap.add_argument("--cpu-reads", type=int, default=2_000_000,
+                    help="parity sample / CPU-baseline sample (reads; N > 1: capped at 200k)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: min(16, cpus))")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the 1-thread CPU timing")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                         "several ranks on one GPU)")
+    return ap.parse_args(argv)
+
+
+def _spawn_ranks(args):
+    """--gpus N > 1 outside torch.distributed: N fresh rank processes (nothing here has touched
+    the GPU yet), rendezvous on 127.0.0.1; exit with their status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+if __name__ == "__main__":
+    _a = _args()
+    if _a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(_a))
+
+import ctypes as C  # noqa: E402
+import json  # noqa: E402
+import time  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (first: libskq.so then binds to torch's HIP runtime)
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sketch-for-rna-seq_amd"))
@@ -36,6 +86,8 @@ CONFIGS = {
                  desc="synthetic 1M x 100 bp reads vs 10k-transcript index, k=31"),
     "cfg3": dict(ntx=200_000, reads=10_000_000, read_len=150, ks=[31],
                  desc="synthetic 10M x 150 bp reads/GPU vs ~200k-transcript index, k=31"),
+    "cfg4": dict(ntx=200_000, reads=12_500_000, read_len=150, ks=[31],
+                 desc="synthetic 12.5M x 150 bp reads/GPU (100M at 8 GPUs) vs ~200k-transcript index, k=31"),
     "cfg5": dict(ntx=200_000, reads=10_000_000, read_len=150, ks=[21, 25, 31],
                  desc="synthetic 10M x 150 bp reads/GPU vs ~200k-transcript index, k={21,25,31}"),
 }
@@ -45,17 +97,15 @@ def log(*a):
     print("[bench r%s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
 
 
-def per_read_stats(sess, tables, ks, n):
+def per_read_stats(out, tables, ks, n):
     """h (retained hashes, summed over k), P (postings touched), C (candidates) per read, from
-    an export of the current results (deterministic given the inputs)."""
-    out = sess.export()
+    an export (deterministic given the inputs)."""
     nk = len(ks)
     ho = out["hash_offs"].astype(np.int64)
     hs = out["hashes"]
     P = 0
     for i, k in enumerate(ks):
         keys, offs, _ = tables[k]
-        # gather the k-slot-i hashes of every read
         starts = ho[i:-1:nk]
         ends = ho[i + 1::nk]
         lens = ends - starts
@@ -65,29 +115,65 @@ def per_read_stats(sess, tables, ks, n):
         pos = np.minimum(pos, len(keys) - 1)
         hit = keys[pos] == x
         P += int((offs[pos + 1].astype(np.int64) - offs[pos].astype(np.int64))[hit].sum())
-    h = len(hs) / n
-    return dict(h=h, P=P / n, C=len(out["cand_tid"]) / n,
-                ok=float((out["status"] == 0).mean()))
+    return dict(h=len(hs) / n, P=P / n, C=len(out["cand_tid"]) / n)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
-    ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
-    ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="CPU-baseline sample size")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
-                         "several ranks on one GPU)")
-    args = ap.parse_args()
-    cfg = dict(CONFIGS[args.config])
+def parity_check(gpu, gtot, cpu, nk):
+    """The GPU export of the sample against the oracle's FASTQ-path outputs, bit-exact: status,
+    retained-hash sets per (read, k), candidate lists (tid, score in the normalised order) and the
+    per-transcript totals. Returns a list of mismatch descriptions (empty = bit-exact)."""
+    bad = []
+    n = cpu["n"]
+    if len(gpu["status"]) != n:
+        return ["read count %d vs %d" % (len(gpu["status"]), n)]
+    st = gpu["status"].astype(np.uint8)
+    if not np.array_equal(st, cpu["status"]):
+        bad.append("status: %d reads differ" % int((st != cpu["status"]).sum()))
+    # hashes: CSR (read-major, k-minor) vs dense [n, nk, hcap]
+    ho = gpu["hash_offs"].astype(np.int64)
+    cnt = np.diff(ho).reshape(n, nk)
+    if not np.array_equal(cnt, cpu["hash_cnt"].astype(np.int64)):
+        bad.append("retained-hash counts: %d (read, k) differ" % int((cnt != cpu["hash_cnt"]).sum()))
+    else:
+        hcap = cpu["hashes"].shape[2]
+        mask = np.arange(hcap)[None, None, :] < cpu["hash_cnt"][:, :, None]
+        if not np.array_equal(cpu["hashes"][mask], gpu["hashes"][:ho[-1]]):
+            bad.append("retained hashes differ")
+    co = gpu["cand_offs"].astype(np.int64)
+    cc = np.diff(co)
+    if not np.array_equal(cc, cpu["cand_cnt"].astype(np.int64)):
+        bad.append("candidate counts: %d reads differ" % int((cc != cpu["cand_cnt"]).sum()))
+    else:
+        ccap = cpu["cand_tid"].shape[1]
+        mask = np.arange(ccap)[None, :] < cpu["cand_cnt"][:, None]
+        if not np.array_equal(cpu["cand_tid"][mask], gpu["cand_tid"][:co[-1]]):
+            bad.append("candidate transcripts differ")
+        if not np.array_equal(cpu["cand_score"][mask], gpu["cand_score"][:co[-1]]):
+            bad.append("candidate scores differ")
+    if not (np.array_equal(gtot[0], cpu["tx_reads"]) and np.array_equal(gtot[1], cpu["tx_score"])):
+        bad.append("per-transcript totals differ")
+    return bad
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main(args):
+    cname = args.config or ("cfg3" if args.gpus == 1 else "cfg4")
+    cfg = dict(CONFIGS[cname])
     if args.reads:
         cfg["reads"] = args.reads
 
     rank, world, local = sdist.world()
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     gpu = local % max(torch.cuda.device_count(), 1)  # one GPU per rank on a full node
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -136,38 +222,36 @@ def main():
     elapsed = time.perf_counter() - ts
     sess.enable_timing(False)
     sess.check(sp)
-    # (total ms, launches): sketch, probe, count, totals (k_bin_sum + fold)
+    # (total ms, launches): sketch / fused map, probe, count, totals (k_bin_sum + fold)
     kt = [sess.kernel_time(kind) for kind in range(4)]
     elapsed = sdist.max_over_ranks(elapsed, device=dev)  # the slowest rank's time
+    slow = sess.slow_reads()
 
-    # per-read workload figures on a 1M-read slice of this rank's batch
-    ns = min(n, 1_000_000)
-    sess.map(d_reads.data_ptr(), None, ns, L, fixed_len=L, stream=sp, accumulate=False)
-    st = per_read_stats(sess, tables, ks, ns)
+    # the sample: the first m reads of this rank's batch, mapped alone (fresh totals), exported
+    m = min(n, args.cpu_reads if world == 1 else min(args.cpu_reads, 200_000))
+    sess.reset_totals(sp)
+    sess.map(d_reads.data_ptr(), None, m, L, fixed_len=L, stream=sp, accumulate=True)
+    sess.check(sp)
+    gout = sess.export()
+    gtot = sess.totals()
+    st = per_read_stats(gout, tables, ks, m)
     h, P, Cn = st["h"], st["P"], st["C"]
     nk = len(ks)
     # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"); an index lookup is priced at
     # the 8 B (key, list offset) it needs, a posting at its 4 B tid
     fused = kt[1][1] == 0  # no k_probe launches: the sketch kernel probed (direct/rank table)
-    # wide tables, one k: skq_map runs ONE kernel (k_map1: sketch + entry gathers + count), timed
-    # as kind 0 with no separate count launches
+    # one fused map kernel (k_map1 / k_mapk: sketch + entry gathers + count), timed as kind 0
+    # with no separate count launches
     map1 = kt[2][1] == 0 and kt[0][1] > 0
-    # the count kernel: k_count3 (32-bit keys, bins the totals) unless ids need > 22 bits
-    count_name = "k_count3" if tx.ntx <= (1 << 22) and os.environ.get("SKQ_VARIANT") != "4" else "k_count"
+    count_name = "k_count3" if tx.ntx <= (1 << 22) else "k_count"
     b_chain = 4 * P + 4 + 8 * Cn + 4 * Cn  # postings in, candidates + count + binned totals out
     b_kern = {
-        # read bases in; retained hashes, per-k counts, status out (+ when fused: one lookup per
-        # hash, list offsets and the slow flag out)
         "k_sketch": L + 4 * h + 4 * nk + 1 + ((8 * h + 4 * h + 1) if fused else 0),
-        # status + counts + hashes in, one lookup per hash, list offsets + slow flag out
         "k_probe": 1 + 4 * nk + 4 * h + 8 * h + 4 * h + 1,
-        # status + flag + counts + list offsets in, postings, candidates (tid, score) + count out,
-        # and each candidate's 4 B binned (tid, score) for the totals
         count_name: 2 + 4 * nk + 4 * h + 4 * P + 4 + 8 * Cn + 4 * Cn,
-        # binned candidates in (4 B each), per-transcript sums out (amortised: 16 B x ntx / n)
         "totals": 4 * Cn + 16.0 * tx.ntx / n,
     }
-    fused_name = "k_map1" if nk == 1 else "k_mapk"  # (k_mapk: 2..4 k slots)
+    fused_name = "k_map1" if nk == 1 else "k_mapk"
     if map1:  # the fused kernel: read in, one lookup per hash, postings, hashes + candidates out
         b_kern = {fused_name: L + 1 + 4 * nk + 4 * h + 8 * h + b_chain, "totals": b_kern["totals"]}
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
@@ -176,16 +260,14 @@ def main():
     kname = max(avg, key=avg.get)                       # dominant kernel
     achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % cname)
+    probe = index.stats()["probe"]
     if os.path.exists(tf):                               # PMC FETCH/WRITE passes (tools/traffic.py)
         tr = json.load(open(tf))
-        if kname in tr.get("kernels", {}):
+        if kname in tr.get("kernels", {}) and tr.get("probe", probe) == probe:
             traffic = tr["kernels"][kname]["hbm_bytes_per_read"] * n
-    # the bound that binds the lookups: random fabric requests, not bytes. k_map1
-    # issues one random 32-B entry gather per retained hash; tools/micro/gather_bench measures the
-    # chip's rate for exactly that access (pair-cooperative 32-B gathers, 8 GiB table).
     requests = None
-    if map1:
+    if map1:  # random index requests per launch against the measured gather ceiling
         rps = n * h / (avg[kname] * 1e-3) / 1e9
         requests = {"random_per_read": h, "achieved": rps, "ceiling": GATHER_CEIL_GPS, "unit": "G/s",
                     "frac": rps / GATHER_CEIL_GPS,
@@ -193,31 +275,55 @@ def main():
     total_reads = n * world * args.steps
     value = total_reads / elapsed
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    parity, cpu = None, None
+    if rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import orc  # the CPU oracle: baseline only, never the measured path
-        keys, offs, tids = tables[ks[0]]
+        import orc  # the CPU oracle: the checker and the CPU baseline, never the measured path
         pairs = []
         for k in ks:
             keys, offs, tids = tables[k]
             pairs.append((np.repeat(keys, np.diff(offs.astype(np.int64))), tids))
         oi = orc.Index(ks, pairs=pairs, ntx=tx.ntx)
-        m = min(args.cpu_reads, n)
-        ro = np.arange(0, (m + 1) * L, L, dtype=np.uint64)
+        fq = synth.fastq_bytes(bases[:m * L], L)
+        try:
+            ncpu = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncpu = os.cpu_count() or 1
+        P_thr = args.cpu_threads or max(1, min(16, ncpu))
         tc = time.perf_counter()
-        orc.lib().orc_map_batch_count(oi.h, orc.ptr(bases), orc.ptr(ro), m, orc.threshold(), 0.9)
-        dt = time.perf_counter() - tc
-        cpu = {"value": m / dt, "unit": "reads/s", "cores": 1, "kind": "port",
-               "sample": "first %d reads of the same batch (in RAM), same index, oracle/oracle.c "
-                         "single-threaded, %.1fs" % (m, dt)}
+        cout = orc.fastq_map(oi, fq, nthreads=P_thr, outputs=True, hcap=64, ccap=64)
+        dt_p = time.perf_counter() - tc
+        bad = parity_check(gout, gtot, cout, nk)
+        parity = ("bit-exact, %d reads (status, retained-hash sets, candidate lists, per-transcript totals)" % m
+                  if not bad else "MISMATCH: " + "; ".join(bad))
+        log("parity sample: %s" % parity)
+        if world == 1:
+            cpu = {"value": m / dt_p, "unit": "reads/s", "cores": P_thr, "kind": "port",
+                   "cpu_model": cpu_model(),
+                   "sample": "first %d reads of the same batch as FASTQ text (%d MB in RAM), same index: "
+                             "oracle/oracle.c orc_fastq_map (record machine, is_valid_sequence, sketch, "
+                             "sparse_chain, id map, totals), %d threads over read shards, %.1fs"
+                             % (m, fq.size >> 20, P_thr, dt_p)}
+            if not args.no_cpu_baseline:
+                m1 = min(m, 1_000_000)
+                fq1 = fq[:m1 * (fq.size // m)]
+                tc = time.perf_counter()
+                orc.fastq_map(oi, fq1, nthreads=1, outputs=False, totals=True)
+                dt_1 = time.perf_counter() - tc
+                cpu["single_core"] = {"value": m1 / dt_1, "cores": 1,
+                                      "sample": "first %d reads, 1 thread, %.1fs" % (m1, dt_1)}
+            cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+            if os.path.exists(cal):  # reference sparse_chain vs the oracle's, timed in the build container
+                cpu["calibration"] = json.load(open(cal)).get("summary")
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
         res = {
             "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": args.config + ": " + cfg["desc"], "reads_per_gpu": n, "read_len": L,
+            "config": {"workload": cname + ": " + cfg["desc"], "reads_per_gpu": n, "read_len": L,
                        "transcripts": tx.ntx, "ks": ks, "sketch_fraction": "(double)0.05f",
                        "chain_fraction": 0.9, "parallelism": "read-sharded x%d, index replicated" % world
                        + (", 1 all-reduce of per-transcript totals per step" if world > 1 else "")},
@@ -225,20 +331,22 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname],
                          "requests": requests,
-                         # the PMC bytes per launch over the same launch time: every random entry
-                         # gather moves a whole 128-B line
                          "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None},
-            "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + wide-entry gathers + count fused)" if map1 else
+            "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + index gathers + count fused)" if map1 else
                                                 "fused in k_sketch" if fused else "k_probe"),
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
                      "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
-                     "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn},
+                     "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn,
+                     "slow_reads_per_batch": {"sketch": slow[0], "chain": slow[1]}},
+            "parity_sample": parity,
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and parity.startswith("MISMATCH"):
+        raise SystemExit(3)
 
 
 if __name__ == "__main__":
-    main()
+    main(_a)

@@ -469,3 +469,174 @@ void orc_assign(uint64_t nreads, const uint64_t* cand_offs, const uint32_t* cand
         }
     }
 }
+
+/* ---- the quant hot path from FASTQ bytes (src/main.cpp:107-151 + :181-185) ---------------
+ * For bench.py's cpu_baseline and its parity sample. Phase 1 (sequential, as the reference):
+ * the record machine of process_fastq_single_pass (:116-130) over the bytes: a line starting
+ * with '@' opens a record whose next three lines are sequence, '+' and quality; any other line
+ * is skipped. Phase 2 (nthreads over contiguous record ranges): is_valid_sequence, the length
+ * filter, every k's sketch and sparse_chain per record (map_one). Phase 3 (sequential): the
+ * id map — read_sketches[id] = ... (:147) keeps the LAST valid record of an id — and the
+ * per-transcript totals (candidate reads, summed scores) over the kept records. */
+#include <pthread.h>
+
+typedef struct {
+    const orc_index* ix;
+    const char* fq;
+    const uint64_t* rec;   /* per record: id start, id len, seq start, seq len */
+    uint64_t r0, r1;
+    uint32_t threshold;
+    double fraction;
+    uint8_t* status;
+    uint32_t *hash_cnt, *hashes, hcap, *cand_cnt, *cand_tid, *cand_score, ccap;
+    uint32_t* cnt_scratch; /* per record candidate count when no outputs are kept */
+    uint64_t* tx_acc;      /* per thread: (reads << 40 | score) per transcript, NULL = none */
+    int rc;
+} fq_job;
+
+static void* fq_worker(void* arg) {
+    fq_job* j = (fq_job*)arg;
+    const orc_index* ix = j->ix;
+    uint64_t maxlen = 1;
+    for (uint64_t r = j->r0; r < j->r1; ++r)
+        if (j->rec[4 * r + 3] > maxlen) maxlen = j->rec[4 * r + 3];
+    uint32_t* scratch = (uint32_t*)malloc(sizeof(uint32_t) * (maxlen + 1) * ix->nk + 4);
+    uint32_t hc[64];
+    uint32_t* ct = j->cand_tid ? NULL : (uint32_t*)malloc(sizeof(uint32_t) * (ix->ntx + 1));
+    uint32_t* cs = j->cand_tid ? NULL : (uint32_t*)malloc(sizeof(uint32_t) * (ix->ntx + 1));
+    for (uint64_t r = j->r0; r < j->r1 && j->rc == 0; ++r) {
+        uint8_t st;
+        uint32_t nc;
+        const uint8_t* s = (const uint8_t*)j->fq + j->rec[4 * r + 2];
+        const size_t len = j->rec[4 * r + 3];
+        if (j->cand_tid)
+            j->rc = map_one(ix, s, len, j->threshold, j->fraction, &st, j->hash_cnt + r * ix->nk,
+                            j->hashes + r * ix->nk * j->hcap, j->hcap, &nc, j->cand_tid + r * j->ccap,
+                            j->cand_score + r * j->ccap, j->ccap, scratch);
+        else
+            j->rc = map_one(ix, s, len, j->threshold, j->fraction, &st, hc, NULL, 0, &nc, ct, cs, ix->ntx + 1,
+                            scratch);
+        j->status[r] = st;
+        j->cnt_scratch[r] = nc;
+        if (j->tx_acc && !j->cand_tid) /* totals straight from this record's candidates */
+            for (uint32_t c = 0; c < nc; ++c) j->tx_acc[ct[c]] += (1ull << 40) | cs[c];
+    }
+    free(scratch);
+    free(ct);
+    free(cs);
+    return NULL;
+}
+
+static uint64_t fnv1a(const char* s, uint64_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (uint64_t q = 0; q < n; ++q) h = (h ^ (uint8_t)s[q]) * 1099511628211ull;
+    return h;
+}
+
+int orc_fastq_map(const orc_index* ix, const char* fq, uint64_t len, uint32_t threshold, double fraction,
+                  int nthreads, uint64_t max_records, uint64_t* n_records, uint8_t* status, uint32_t* hash_cnt,
+                  uint32_t* hashes, uint32_t hcap, uint32_t* cand_cnt, uint32_t* cand_tid, uint32_t* cand_score,
+                  uint32_t ccap, uint8_t* kept, uint64_t* tx_reads, uint64_t* tx_score) {
+    /* phase 1: the record machine */
+    uint64_t cap = 1024, n = 0, pos = 0;
+    uint64_t* rec = (uint64_t*)malloc(sizeof(uint64_t) * 4 * cap);
+    uint64_t lines[4];
+    while (pos < len && n < max_records) {
+        const char* nl = (const char*)memchr(fq + pos, '\n', len - pos);
+        const uint64_t end = nl ? (uint64_t)(nl - fq) : len;
+        if (end == pos || fq[pos] != '@') { pos = end + 1; continue; } /* :118-120 */
+        /* header = [pos, end); then getline x3 (a missing line reads as empty) */
+        uint64_t p = end + 1;
+        for (int q = 0; q < 3; ++q) {
+            if (p >= len) { lines[q] = len; continue; }
+            const char* e = (const char*)memchr(fq + p, '\n', len - p);
+            lines[q] = p;
+            p = e ? (uint64_t)(e - fq) + 1 : len;
+        }
+        if (n == cap) { cap *= 2; rec = (uint64_t*)realloc(rec, sizeof(uint64_t) * 4 * cap); }
+        rec[4 * n] = pos + 1;
+        rec[4 * n + 1] = end - pos - 1;
+        const uint64_t ss = lines[0];
+        uint64_t se = ss;
+        while (se < len && fq[se] != '\n') ++se;
+        rec[4 * n + 2] = ss;
+        rec[4 * n + 3] = se - ss;
+        ++n;
+        pos = p;
+    }
+    *n_records = n;
+    /* phase 2: records in parallel */
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    uint8_t* st = status ? status : (uint8_t*)malloc(n + 1);
+    uint32_t* cc = cand_cnt ? cand_cnt : (uint32_t*)malloc(sizeof(uint32_t) * (n + 1));
+    fq_job jobs[256];
+    pthread_t th[256];
+    const int direct_totals = !cand_tid && tx_reads; /* per-thread totals, no per-record lists */
+    for (int t = 0; t < nthreads; ++t) {
+        fq_job* j = &jobs[t];
+        memset(j, 0, sizeof(*j));
+        j->ix = ix; j->fq = fq; j->rec = rec;
+        j->r0 = n * t / nthreads; j->r1 = n * (t + 1) / nthreads;
+        j->threshold = threshold; j->fraction = fraction;
+        j->status = st; j->hash_cnt = hash_cnt; j->hashes = hashes; j->hcap = hcap;
+        j->cand_cnt = cc; j->cand_tid = cand_tid; j->cand_score = cand_score; j->ccap = ccap;
+        j->cnt_scratch = cc;
+        j->tx_acc = direct_totals ? (uint64_t*)calloc(ix->ntx + 1, sizeof(uint64_t)) : NULL;
+        pthread_create(&th[t], NULL, fq_worker, j);
+    }
+    int rc = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+    }
+    /* phase 3: last valid record per id wins (:147), totals over the kept records */
+    uint64_t tcap = 16;
+    while (tcap < 2 * n + 2) tcap *= 2;
+    int64_t* tab = (int64_t*)malloc(sizeof(int64_t) * tcap);
+    for (uint64_t q = 0; q < tcap; ++q) tab[q] = -1;
+    uint8_t* kp = kept ? kept : (uint8_t*)malloc(n + 1);
+    memset(kp, 0, n + 1);
+    uint64_t dups = 0;
+    for (uint64_t r = 0; r < n; ++r) {
+        if (st[r] != ORC_OK) continue;
+        const char* id = fq + rec[4 * r];
+        const uint64_t il = rec[4 * r + 1];
+        uint64_t q = fnv1a(id, il) & (tcap - 1);
+        while (tab[q] >= 0) {
+            const uint64_t o = (uint64_t)tab[q];
+            if (rec[4 * o + 1] == il && !memcmp(fq + rec[4 * o], id, il)) break;
+            q = (q + 1) & (tcap - 1);
+        }
+        if (tab[q] >= 0) { kp[tab[q]] = 0; ++dups; }
+        tab[q] = (int64_t)r;
+        kp[r] = 1;
+    }
+    if (tx_reads) {
+        memset(tx_reads, 0, sizeof(uint64_t) * ix->ntx);
+        memset(tx_score, 0, sizeof(uint64_t) * ix->ntx);
+        if (direct_totals && !dups) {
+            for (int t = 0; t < nthreads; ++t)
+                for (uint32_t x = 0; x < ix->ntx; ++x) {
+                    tx_reads[x] += jobs[t].tx_acc[x] >> 40;
+                    tx_score[x] += jobs[t].tx_acc[x] & ((1ull << 40) - 1);
+                }
+        } else if (cand_tid) {
+            for (uint64_t r = 0; r < n; ++r)
+                if (kp[r])
+                    for (uint32_t c = 0; c < cc[r]; ++c) {
+                        tx_reads[cand_tid[r * ccap + c]] += 1;
+                        tx_score[cand_tid[r * ccap + c]] += cand_score[r * ccap + c];
+                    }
+        } else {
+            rc = rc ? rc : -2; /* duplicates without per-record lists: totals unavailable */
+        }
+    }
+    for (int t = 0; t < nthreads; ++t) free(jobs[t].tx_acc);
+    free(tab);
+    if (!kept) free(kp);
+    if (!status) free(st);
+    if (!cand_cnt) free(cc);
+    free(rec);
+    return rc;
+}

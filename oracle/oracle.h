@@ -98,6 +98,21 @@ int orc_map_batch(const orc_index* idx, const uint8_t* reads, const uint64_t* of
 uint64_t orc_map_batch_count(const orc_index* idx, const uint8_t* reads, const uint64_t* offs,
                              uint64_t n, uint32_t threshold, double fraction);
 
+/* The quant hot path from FASTQ bytes (src/main.cpp:107-151, :181-185), for bench.py's CPU
+ * baseline: the reference's record machine over fq[0..len) (sequential, as the reference),
+ * then per record is_valid_sequence + length filter + every k's sketch + sparse_chain on
+ * nthreads threads over contiguous record ranges, then the id map (the last valid record of an
+ * id is kept, :147). At most max_records records. Optional outputs (NULL = skipped), record
+ * order, layouts as orc_map_batch: status, hash_cnt/hashes (hcap per (record, k)),
+ * cand_cnt/cand_tid/cand_score (ccap per record); kept[n] (1 = the record kept for its id);
+ * tx_reads/tx_score[ntx]: candidate reads and summed scores per transcript over the kept
+ * records. Returns 0; -1 if a cap is exceeded; -2 if totals were asked for without per-record
+ * lists and the file has duplicate ids. */
+int orc_fastq_map(const orc_index* idx, const char* fq, uint64_t len, uint32_t threshold, double fraction,
+                  int nthreads, uint64_t max_records, uint64_t* n_records, uint8_t* status, uint32_t* hash_cnt,
+                  uint32_t* hashes, uint32_t hcap, uint32_t* cand_cnt, uint32_t* cand_tid, uint32_t* cand_score,
+                  uint32_t ccap, uint8_t* kept, uint64_t* tx_reads, uint64_t* tx_score);
+
 /* EM over the reads' candidate lists (src/isoform_assignment.cpp:9-65): pi starts uniform over
  * the ntx transcripts; E-step per read in order, posterior = pi*score * (1/denominator) when the
  * denominator exceeds 1e-10; M-step pi = (posterior_sum + 0.01f/R) + 0.01f (float pseudocount,

@@ -27,9 +27,7 @@ def shard(n, rank, world_size):
 def allreduce_totals(totals):
     """Sum a [2, ntx] int64 tensor of per-transcript totals over all ranks, in place. A no-op
     without an initialised process group (single GPU)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
-    return totals
+    return _allreduce(totals)
 
 
 def max_over_ranks(value, device=None):

@@ -93,3 +93,25 @@ def write_fastq(path, bases, read_len, tids=None, starts=None, names=None):
                 tn = names[tids[r]].split("|")[0] if names else str(tids[r])
                 hdr += b" tx=%s pos=%d" % (tn.encode(), int(starts[r]))
             f.write(hdr + b"\n" + bases[r * read_len:(r + 1) * read_len].tobytes() + b"\n+\n" + q + b"\n")
+
+
+def fastq_bytes(bases, read_len, first=0):
+    """FASTQ text of fixed-length reads (vectorised): `@read<9-digit ordinal>`, the bases, `+`,
+    quality all 'I' — the record layout write_fastq uses, with fixed-width ids."""
+    n = len(bases) // read_len
+    hdr = 1 + 4 + 9 + 1
+    rs = hdr + read_len + 1 + 2 + read_len + 1
+    out = np.empty((n, rs), np.uint8)
+    out[:, 0:5] = np.frombuffer(b"@read", np.uint8)
+    num = np.arange(first, first + n, dtype=np.int64)
+    for d in range(9):
+        out[:, 5 + 8 - d] = 48 + (num // 10 ** d) % 10
+    out[:, hdr - 1] = 10
+    out[:, hdr:hdr + read_len] = bases[:n * read_len].reshape(n, read_len)
+    o = hdr + read_len
+    out[:, o] = 10
+    out[:, o + 1] = ord("+")
+    out[:, o + 2] = 10
+    out[:, o + 3:o + 3 + read_len] = ord("I")
+    out[:, rs - 1] = 10
+    return out.reshape(-1)

@@ -59,6 +59,10 @@ def lib():
         L.orc_assign.restype = None
         L.orc_assign.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                  C.c_void_p, C.c_void_p]
+        L.orc_fastq_map.restype = C.c_int
+        L.orc_fastq_map.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_double, C.c_int, C.c_uint64,
+                                    C.c_void_p] + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 3 + \
+                                   [C.c_uint32] + [C.c_void_p] * 3
         _lib = L
     return _lib
 
@@ -184,6 +188,49 @@ class Index:
         return dict(status=st[:n], hash_cnt=hc[:n * nk].reshape(n, nk),
                     hashes=hs[:n * nk * hcap].reshape(n, nk, hcap), cand_cnt=cc[:n],
                     cand_tid=ct[:n * ccap].reshape(n, ccap), cand_score=cs[:n * ccap].reshape(n, ccap))
+
+
+def fastq_map(index, fq, nthreads=1, outputs=True, totals=True, hcap=None, ccap=None, thr=None,
+              fraction=CHAIN_FRACTION, max_records=None):
+    """orc_fastq_map over FASTQ bytes (bytes or a uint8 array): the record machine, per-record
+    sketch + chain on nthreads threads, the id map. Returns a dict: n, and when asked the
+    per-record outputs (status, hash_cnt, hashes, cand_cnt, cand_tid, cand_score, kept) and the
+    per-transcript totals (tx_reads, tx_score)."""
+    buf = np.frombuffer(fq, np.uint8) if isinstance(fq, (bytes, bytearray)) else fq
+    thr = threshold() if thr is None else thr
+    nmax = int(buf.size // 4 + 1) if max_records is None else int(max_records)
+    nrec = C.c_uint64()
+    nk = len(index.ks)
+    res = {}
+    if outputs:
+        # records are at most one per 4 lines; size the outputs from the line count
+        nl = int(np.count_nonzero(buf == 10)) // 4 + 2
+        nmax = min(nmax, nl)
+        hcap = hcap or 32
+        ccap = ccap or max(index.ntx, 1)
+        res = dict(status=np.zeros(nmax, np.uint8), hash_cnt=np.zeros(nmax * nk, np.uint32),
+                   hashes=np.zeros(nmax * nk * hcap, np.uint32), cand_cnt=np.zeros(nmax, np.uint32),
+                   cand_tid=np.zeros(nmax * ccap, np.uint32), cand_score=np.zeros(nmax * ccap, np.uint32),
+                   kept=np.zeros(nmax + 1, np.uint8))
+    txr = np.zeros(max(index.ntx, 1), np.uint64) if totals else None
+    txs = np.zeros(max(index.ntx, 1), np.uint64) if totals else None
+    g = lambda k: ptr(res[k]) if outputs else None  # noqa: E731
+    rc = lib().orc_fastq_map(index.h, ptr(buf), buf.size, thr, fraction, nthreads, nmax, C.byref(nrec),
+                             g("status"), g("hash_cnt"), g("hashes"), hcap or 0, g("cand_cnt"), g("cand_tid"),
+                             g("cand_score"), ccap or 0, g("kept"), ptr(txr) if totals else None,
+                             ptr(txs) if totals else None)
+    if rc != 0:
+        raise RuntimeError("orc_fastq_map failed (%d)" % rc)
+    n = nrec.value
+    out = dict(n=n)
+    if outputs:
+        out.update(status=res["status"][:n], hash_cnt=res["hash_cnt"][:n * nk].reshape(n, nk),
+                   hashes=res["hashes"][:n * nk * hcap].reshape(n, nk, hcap), cand_cnt=res["cand_cnt"][:n],
+                   cand_tid=res["cand_tid"][:n * ccap].reshape(n, ccap),
+                   cand_score=res["cand_score"][:n * ccap].reshape(n, ccap), kept=res["kept"][:n].astype(bool))
+    if totals:
+        out.update(tx_reads=txr[:index.ntx], tx_score=txs[:index.ntx])
+    return out
 
 
 def em(cand_offs, cand_tid, cand_score, ntx, max_iterations=20, convergence=0.01):

@@ -450,7 +450,11 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     s = skq.Session(gi, len(reads), read_len)
     d_buf = skq.DeviceBuffer.from_numpy(buf)
     s.enable_timing(True)
-    s.map(d_buf.ptr, None, len(reads), read_len, fixed_len=read_len)
+    if SPLIT:
+        s.sketch(d_buf.ptr, None, len(reads), read_len, fixed_len=read_len)
+        s.chain()
+    else:
+        s.map(d_buf.ptr, None, len(reads), read_len, fixed_len=read_len)
     s.check()
     s.enable_timing(False)
     count_launches = s.kernel_time(2)[1]

@@ -1,0 +1,137 @@
+"""GPU parity at BASELINE.json's scales (cfg2, cfg3, cfg5), through the C ABI, bit-exact against
+the CPU oracle run over the same reads as FASTQ text (orc_fastq_map, threads over read shards).
+
+  cfg2: 10k-transcript index, 100 bp reads, k = 31;
+  cfg3: ~200k-transcript GENCODE-scale index, 150 bp, k = 31 (the metric's config);
+  cfg5: the same index at k = {21, 25, 31} (the fused multi-k map).
+
+Per read: status, retained-hash sets per k, candidate lists (tid, score; score desc, tid asc);
+per transcript: candidate reads and summed scores. cfg3 is also checked at its FULL batch
+(10M reads) through the size-independent per-transcript totals, which exercise the slow paths,
+the overflow lists and the per-batch totals packing at the bench's own size.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch  # noqa: F401  (before skq: one HIP runtime per process)
+
+import orc
+import skq
+from skq import synth
+
+pytestmark = pytest.mark.gpu
+
+NTHREADS = 16  # the GPU box's CPU share
+
+
+@pytest.fixture(scope="module")
+def tx200k():
+    return synth.transcriptome(200_000, seed=1)  # bench.py's cfg3 / cfg5 transcriptome
+
+
+@pytest.fixture(scope="module")
+def tx10k():
+    return synth.transcriptome(10_000, seed=1)
+
+
+def _oracle(tables, ks, ntx):
+    pairs = []
+    for k in ks:
+        keys, offs, tids = tables[k]
+        pairs.append((np.repeat(keys, np.diff(offs.astype(np.int64))), tids))
+    return orc.Index(ks, pairs=pairs, ntx=ntx)
+
+
+def _gpu_map(index, bases, n, L):
+    s = skq.Session(index, n, L)
+    d = skq.DeviceBuffer.from_numpy(bases[:n * L])
+    s.map(d.ptr, None, n, L, fixed_len=L)
+    s.check()
+    out = s.export()
+    tot = s.totals()
+    slow = s.slow_reads()
+    s.free()
+    d.free()
+    return out, tot, slow
+
+
+def _compare(out, tot, cpu, nk):
+    n = cpu["n"]
+    np.testing.assert_array_equal(out["status"], cpu["status"])
+    ho = out["hash_offs"].astype(np.int64)
+    np.testing.assert_array_equal(np.diff(ho).reshape(n, nk), cpu["hash_cnt"].astype(np.int64))
+    hcap = cpu["hashes"].shape[2]
+    hm = np.arange(hcap)[None, None, :] < cpu["hash_cnt"][:, :, None]
+    np.testing.assert_array_equal(out["hashes"][:ho[-1]], cpu["hashes"][hm])
+    co = out["cand_offs"].astype(np.int64)
+    np.testing.assert_array_equal(np.diff(co), cpu["cand_cnt"].astype(np.int64))
+    ccap = cpu["cand_tid"].shape[1]
+    cm = np.arange(ccap)[None, :] < cpu["cand_cnt"][:, None]
+    np.testing.assert_array_equal(out["cand_tid"][:co[-1]], cpu["cand_tid"][cm])
+    np.testing.assert_array_equal(out["cand_score"][:co[-1]], cpu["cand_score"][cm])
+    np.testing.assert_array_equal(tot[0], cpu["tx_reads"])
+    np.testing.assert_array_equal(tot[1], cpu["tx_score"])
+
+
+def _case(tx, ks, L, nreads, seed, err=0.001):
+    tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=NTHREADS)
+    index = skq.Index(ks, tx.ntx, tables)
+    bases, _, _ = synth.reads(tx, nreads, L, seed=seed, err=err)
+    # a sprinkle of edge reads at scale: invalid bases and lowercase
+    rng = np.random.default_rng(seed)
+    bad = rng.choice(nreads, nreads // 1000, replace=False)
+    bases[bad * L + rng.integers(0, L, len(bad))] = ord("N")
+    low = rng.choice(nreads, nreads // 2000, replace=False)
+    bases[low * L] = ord("a")
+    out, tot, slow = _gpu_map(index, bases, nreads, L)
+    cpu = orc.fastq_map(_oracle(tables, ks, tx.ntx), synth.fastq_bytes(bases, L), nthreads=NTHREADS,
+                        hcap=64, ccap=64)
+    assert cpu["n"] == nreads
+    _compare(out, tot, cpu, len(ks))
+    st = index.stats()
+    index.free()
+    return cpu, st, slow
+
+
+def test_cfg2_10k_transcripts_100bp(tx10k):
+    cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201)
+    assert (cpu["cand_cnt"] > 0).mean() > 0.9
+    assert st["probe"] in ("wide", "hash")
+
+
+def test_cfg3_200k_transcripts_150bp(tx200k):
+    cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301)
+    assert (cpu["cand_cnt"] > 0).mean() > 0.95
+    assert st["max_list"] >= 10  # GENCODE-scale postings (long lists take the inline overflow)
+    assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
+
+
+def test_cfg5_multi_k_200k_transcripts(tx200k):
+    cpu, _, _ = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501)
+    assert (cpu["cand_cnt"] > 0).mean() > 0.95
+
+
+def test_cfg3_full_batch_totals(tx200k):
+    """The bench's own batch (10M x 150 bp, one skq_map): per-transcript totals equal the
+    oracle's over the same 10M reads as FASTQ text."""
+    ks, L, n = [31], 150, 10_000_000
+    tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
+    index = skq.Index(ks, tx200k.ntx, tables)
+    bases, _, _ = synth.reads(tx200k, n, L, seed=1000, err=0.001)  # bench.py's rank-0 batch
+    s = skq.Session(index, n, L)
+    d = skq.DeviceBuffer.from_numpy(bases)
+    s.map(d.ptr, None, n, L, fixed_len=L)
+    s.check()
+    tot = s.totals()
+    slow = s.slow_reads()
+    s.free()
+    d.free()
+    index.free()
+    cpu = orc.fastq_map(_oracle(tables, ks, tx200k.ntx), synth.fastq_bytes(bases, L), nthreads=NTHREADS,
+                        outputs=False, totals=True)
+    assert cpu["n"] == n
+    np.testing.assert_array_equal(tot[0], cpu["tx_reads"])
+    np.testing.assert_array_equal(tot[1], cpu["tx_score"])
+    assert int(tot[0].sum()) > 3 * n  # ~3.1 candidates per read
+    assert slow[0] + slow[1] > 100
