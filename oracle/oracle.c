@@ -37,6 +37,14 @@ static uint64_t srol_n(uint64_t x, unsigned d) {
  * invalid incoming base jumps pos += k and re-inits. */
 size_t orc_nthash_fwd(const char* seq, size_t len, unsigned k, uint64_t* out_hash, size_t* out_pos) {
     if (k == 0 || len < k) return (size_t)-1;
+    /* srol^k(SEED[c]) of the outgoing base, for the four distinct non-zero seeds (the roll's
+     * third term), computed once per call instead of k rotations per window */
+    static const unsigned char acgt[4] = {'A', 'C', 'G', 'T'};
+    uint64_t seed4[4], rolk4[4];
+    for (int b = 0; b < 4; ++b) {
+        seed4[b] = orc_seed(acgt[b]);
+        rolk4[b] = srol_n(seed4[b], k);
+    }
     size_t pos = 0, n = 0;
     int initialized = 0;
     uint64_t fwd = 0;
@@ -48,8 +56,11 @@ size_t orc_nthash_fwd(const char* seq, size_t len, unsigned k, uint64_t* out_has
                 pos += k;
                 need_init = 1;
             } else {
-                fwd = orc_srol(fwd) ^ orc_seed((unsigned char)seq[pos + k]) ^
-                      srol_n(orc_seed((unsigned char)seq[pos]), k);
+                const uint64_t so = orc_seed((unsigned char)seq[pos]);
+                uint64_t rk = 0;
+                for (int b = 0; b < 4; ++b)
+                    if (so == seed4[b]) rk = rolk4[b]; /* = srol_n(so, k) */
+                fwd = orc_srol(fwd) ^ orc_seed((unsigned char)seq[pos + k]) ^ rk;
                 ++pos;
             }
         }
@@ -96,7 +107,16 @@ static int cmp_u32(const void* a, const void* b) {
 
 static size_t sort_unique_u32(uint32_t* v, size_t n) {
     if (n == 0) return 0;
-    qsort(v, n, sizeof(uint32_t), cmp_u32);
+    if (n <= 32) { /* insertion sort: a read's retained set is a handful of values */
+        for (size_t i = 1; i < n; ++i) {
+            uint32_t x = v[i];
+            size_t j = i;
+            for (; j > 0 && v[j - 1] > x; --j) v[j] = v[j - 1];
+            v[j] = x;
+        }
+    } else {
+        qsort(v, n, sizeof(uint32_t), cmp_u32);
+    }
     size_t m = 1;
     for (size_t i = 1; i < n; ++i)
         if (v[i] != v[m - 1]) v[m++] = v[i];
@@ -344,6 +364,33 @@ size_t orc_chain_read(const orc_index* ix, const uint32_t* const* hashes, const 
                       const int* present, double fraction, uint32_t* out_tid,
                       uint32_t* out_score, size_t cap) {
     return chain_core(ix, hashes, nh, present, fraction, out_tid, out_score, cap);
+}
+
+/* sparse_chain over a batch of sketches in CSR form (read r, k slot i: hashes[hash_offs[r*nk+i] ..
+ * hash_offs[r*nk+i+1])), every k present; candidates out as CSR. The CPU-baseline calibration
+ * (tools/cpu_calibrate.py) times this against the reference's own sparse_chain on the same
+ * sketches. Returns 0, or -1 when cap is too small. */
+int orc_chain_batch(const orc_index* ix, uint64_t n, const uint64_t* hash_offs, const uint32_t* hashes,
+                    double fraction, uint64_t* cand_offs, uint32_t* cand_tid, uint32_t* cand_score,
+                    uint64_t cap) {
+    const unsigned nk = ix->nk;
+    const uint32_t* hp[64];
+    uint32_t nh[64];
+    int present[64];
+    uint64_t o = 0;
+    cand_offs[0] = 0;
+    for (uint64_t r = 0; r < n; ++r) {
+        for (unsigned i = 0; i < nk; ++i) {
+            hp[i] = hashes + hash_offs[r * nk + i];
+            nh[i] = (uint32_t)(hash_offs[r * nk + i + 1] - hash_offs[r * nk + i]);
+            present[i] = 1;
+        }
+        size_t c = chain_core(ix, hp, nh, present, fraction, cand_tid + o, cand_score + o, cap - o);
+        if (c == (size_t)-1) return -1;
+        o += c;
+        cand_offs[r + 1] = o;
+    }
+    return 0;
 }
 
 /* ---- batch: process_fastq_single_pass filters (src/main.cpp:132-144) + sparse_chain ----- */

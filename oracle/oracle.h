@@ -84,6 +84,12 @@ size_t orc_chain_read(const orc_index* idx, const uint32_t* const* hashes, const
                       const int* present, double fraction, uint32_t* out_tid,
                       uint32_t* out_score, size_t cap);
 
+/* orc_chain_read over a batch of sketches (CSR: read r, k slot i at hash_offs[r*nk+i]); candidates
+ * as CSR (cand_offs[n+1]). Returns 0, -1 when cap is too small. */
+int orc_chain_batch(const orc_index* idx, uint64_t n, const uint64_t* hash_offs, const uint32_t* hashes,
+                    double fraction, uint64_t* cand_offs, uint32_t* cand_tid, uint32_t* cand_score,
+                    uint64_t cap);
+
 /* ---- whole hot path over a batch of read sequences -------------------------------------- */
 enum { ORC_OK = 0, ORC_INVALID = 1, ORC_SHORT = 2 };
 /* Per read r (bytes reads[offs[r] .. offs[r+1])): status (process_fastq_single_pass filters,

@@ -12,6 +12,7 @@
 // candidates by score desc, then tid asc (std::sort in src/sparse_chaining.cpp:108-109 is
 // unstable, so only this normalised order is comparable); dumps sorted by id / key.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -37,6 +38,8 @@ struct RefIndex {
 };
 
 std::string tname(uint32_t t) { return "t" + std::to_string(t); }
+
+double g_chain_seconds = 0;  // wall time of the last ref_chain's sparse_chain call alone
 
 }  // namespace
 
@@ -67,6 +70,9 @@ void* ref_index_new(uint32_t ntx, const char* const* names, unsigned nk, const u
 
 void ref_index_free(void* h) { delete static_cast<RefIndex*>(h); }
 
+// seconds the last ref_chain spent inside sparse_chain itself (container set-up excluded)
+double ref_chain_seconds(void) { return g_chain_seconds; }
+
 // sparse_chain (src/sparse_chaining.cpp:29-115) over a batch. Read r's sketch at k slot i is
 // hashes[hash_offs[r*nk+i] .. hash_offs[r*nk+i+1]); present[r*nk+i] == 0 leaves that k out of the
 // read's MultiKmerSketch (null present: all present). kmer_lengths = ks (may name a k the index
@@ -87,7 +93,9 @@ int ref_chain(void* h, uint64_t n, unsigned nk, const unsigned* ks, const uint64
         reads["r" + std::to_string(r)] = std::move(ms);
     }
     std::vector<unsigned> kl(ks, ks + nk);
+    const auto t0 = std::chrono::steady_clock::now();
     const auto res = sparse_chain(reads, ix->map, ix->transcripts, kl, fraction);
+    g_chain_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     uint64_t o = 0;
     cand_offs[0] = 0;
     for (uint64_t r = 0; r < n; ++r) {

@@ -48,6 +48,9 @@ def lib():
         L.orc_chain_read.restype = C.c_size_t
         L.orc_chain_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
                                      C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orc_chain_batch.restype = C.c_int
+        L.orc_chain_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_double] + \
+                                     [C.c_void_p] * 3 + [C.c_uint64]
         L.orc_map_batch.restype = C.c_int
         L.orc_map_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                     C.c_double] + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 3 + [C.c_uint32]
@@ -161,6 +164,21 @@ class Index:
             assert c != C.c_size_t(-1).value
             out.append(list(zip(ot[:c].tolist(), os_[:c].tolist())))
         return out
+
+    def chain_csr(self, hash_offs, hashes, fraction=CHAIN_FRACTION):
+        """orc_chain_batch: sketches as CSR (read r, k slot i at hash_offs[r*nk+i]) -> candidates
+        (cand_offs[n+1], cand_tid, cand_score), score desc then tid asc."""
+        ho = np.ascontiguousarray(hash_offs, np.uint64)
+        hs = np.ascontiguousarray(hashes if len(hashes) else np.zeros(1), np.uint32)
+        n = (len(ho) - 1) // len(self.ks)
+        cap = max(16 * n, 1)
+        while True:
+            co = np.zeros(n + 1, np.uint64)
+            ct = np.zeros(cap, np.uint32)
+            cs = np.zeros(cap, np.uint32)
+            if lib().orc_chain_batch(self.h, n, ptr(ho), ptr(hs), fraction, ptr(co), ptr(ct), ptr(cs), cap) == 0:
+                return co, ct[:co[-1]], cs[:co[-1]]
+            cap *= 4
 
     def map_batch(self, reads, offs=None, thr=None, fraction=CHAIN_FRACTION, hcap=None, ccap=None):
         """reads: list of bytes (or a flat uint8 array + offs). Returns dict of numpy arrays."""

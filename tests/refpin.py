@@ -35,6 +35,8 @@ def lib():
         L.ref_index_free.argtypes = [vp]
         L.ref_chain.restype = C.c_int
         L.ref_chain.argtypes = [vp, u64, C.c_uint, vp, vp, vp, vp, C.c_double, vp, vp, vp, u64]
+        L.ref_chain_seconds.restype = C.c_double
+        L.ref_chain_seconds.argtypes = []
         L.ref_em_assign.restype = None
         L.ref_em_assign.argtypes = [u64, vp, vp, vp, u32, C.c_int, C.c_double, vp, vp, vp]
         L.ref_output_csv.restype = C.c_int
@@ -125,6 +127,23 @@ class Index:
                 break
             cap *= 4
         return [list(zip(ct[co[r]:co[r + 1]].tolist(), cs[co[r]:co[r + 1]].tolist())) for r in range(n)]
+
+    def chain_csr(self, ks, hash_offs, hashes, fraction=0.9):
+        """sparse_chain over sketches given as CSR (read r, k slot i at hash_offs[r*nk+i]), every k
+        present. Returns (cand_offs, cand_tid, cand_score, seconds inside sparse_chain itself)."""
+        ho = np.ascontiguousarray(hash_offs, np.uint64)
+        hs = np.ascontiguousarray(hashes if len(hashes) else np.zeros(1), np.uint32)
+        ka = np.array(ks, np.uint32)
+        n = (len(ho) - 1) // len(ks)
+        cap = max(16 * n, 1)
+        while True:
+            co = np.zeros(n + 1, np.uint64)
+            ct = np.zeros(cap, np.uint32)
+            cs = np.zeros(cap, np.uint32)
+            if lib().ref_chain(self.h, n, len(ks), _p(ka), _p(ho), _p(hs), None, fraction, _p(co), _p(ct), _p(cs),
+                               cap) == 0:
+                return co, ct[:co[-1]], cs[:co[-1]], lib().ref_chain_seconds()
+            cap *= 4
 
     def __del__(self):
         if getattr(self, "h", None):
