@@ -71,8 +71,14 @@ struct skq_index {
     const uint32_t* wdir[SKQ_MAX_K] = {};
     uint32_t* d_wovf_t[SKQ_MAX_K] = {};
     const uint32_t* wovf[SKQ_MAX_K] = {};
+    // compact tables: per distinct k, the pilots; per k slot, the view
+    uint16_t* d_wpil_t[SKQ_MAX_K] = {};
+    const uint16_t* wpil[SKQ_MAX_K] = {};
+    uint32_t wnb[SKQ_MAX_K] = {}, wseed[SKQ_MAX_K] = {};
     uint64_t dir_bytes = 0;
-    int mode = 0;  // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 4 = block tables
+    // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 4 = block tables,
+    // 5 = compact tables
+    int mode = 0;
     bool direct = false;  // every slot with a table has a direct table: the sketch probes
 };
 
@@ -340,9 +346,124 @@ int build_block(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, c
     return 0;
 }
 
-// Probe structure: wide tables when they fit SKQ_DIRECT_MB (default 49152 MiB) and half the free
-// device memory and the ids fit k_count3, else 4-B direct tables, else the bucket table alone.
-// SKQ_PROBE = wide | dir | rank forces one kind (development A/B and tests).
+// Minimal perfect hash of one k's keys, PTHash-style: keys hash into nb buckets; buckets, largest
+// first, each take the first 16-bit pilot that sends all their keys to distinct free slots among
+// nslots (cmp_slot, skq_internal.h). slot[j] receives key j's slot. false: some bucket found no
+// pilot (the caller retries with another seed).
+bool mph_place(const std::vector<uint32_t>& keys, uint32_t seed, uint64_t nslots, uint32_t nb,
+               std::vector<uint16_t>& pil, std::vector<uint32_t>& slot) {
+    const uint64_t m = keys.size();
+    std::vector<uint32_t> kh(m), start(nb + 1, 0), member(m);
+    for (uint64_t j = 0; j < m; ++j) {
+        kh[j] = skq::cmp_key_hash(keys[j], seed);
+        ++start[skq::cmp_scale(kh[j], nb) + 1];
+    }
+    uint32_t maxb = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        maxb = std::max(maxb, start[b + 1]);
+        start[b + 1] += start[b];
+    }
+    {
+        std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+        for (uint64_t j = 0; j < m; ++j) member[fill[skq::cmp_scale(kh[j], nb)]++] = (uint32_t)j;
+    }
+    // buckets by size, largest first (counting sort)
+    std::vector<uint32_t> by(maxb + 2, 0), order(nb);
+    for (uint32_t b = 0; b < nb; ++b) ++by[maxb - (start[b + 1] - start[b]) + 1];
+    for (uint32_t s = 0; s <= maxb; ++s) by[s + 1] += by[s];
+    for (uint32_t b = 0; b < nb; ++b) order[by[maxb - (start[b + 1] - start[b])]++] = b;
+    std::vector<uint64_t> taken((nslots + 63) / 64, 0);
+    auto is_taken = [&](uint32_t s) { return (taken[s >> 6] >> (s & 63)) & 1ull; };
+    pil.assign(nb, 0);
+    slot.assign(m, 0);
+    std::vector<uint32_t> cur(maxb);
+    for (const uint32_t b : order) {
+        const uint32_t a = start[b], z = start[b + 1];
+        if (a == z) break;  // (sizes descending: the rest are empty)
+        uint32_t p = 0;
+        for (; p < 65536; ++p) {
+            bool ok = true;
+            for (uint32_t q = a; q < z && ok; ++q) {
+                const uint32_t s = skq::cmp_slot(kh[member[q]], p, nslots);
+                ok = !is_taken(s);
+                for (uint32_t u = a; u < q && ok; ++u) ok = cur[u - a] != s;
+                cur[q - a] = s;
+            }
+            if (ok) break;
+        }
+        if (p == 65536) return false;
+        pil[b] = (uint16_t)p;
+        for (uint32_t q = a; q < z; ++q) {
+            taken[cur[q - a] >> 6] |= 1ull << (cur[q - a] & 63);
+            slot[member[q]] = cur[q - a];
+        }
+    }
+    return true;
+}
+
+// Compact tables: for each distinct k, each key's 8-word entry ([key, t0 | F << 22, t1..t6],
+// skq_internal.h) in one of m / 0.95 slots placed by mph_place (m / 5 buckets). A lookup reads
+// the bucket's pilot (2 B per 5 keys: 1.7 MB at 4.24M keys, held in L2) and then one 32-B entry;
+// the entries (143 MB at 4.24M keys) stay in the 256 MB Infinity Cache, which the wide direct
+// table (6.9 GB, one entry per possible key) cannot. Only for k_count3's id range (tids < 2^22).
+int build_compact(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, const std::vector<uint32_t>* dkeys,
+                  const std::vector<uint32_t>* dvals, const std::vector<uint32_t>& lists) {
+    uint64_t need = 0;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const uint64_t m = dkeys[t].size();
+        if (m == 0) continue;
+        const uint64_t nslots = std::max<uint64_t>(m + 1, (uint64_t)std::ceil((double)m / 0.95));
+        const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (m + 4) / 5);
+        // (slots are listed as slot | lane << 26 in k_map1)
+        if (nslots > (1ull << 26)) return fail(-1, "index too large for compact tables");
+        std::vector<uint16_t> pil;
+        std::vector<uint32_t> slot;
+        uint32_t seed = 0x5EED5EEDu;
+        int tries = 0;
+        while (!mph_place(dkeys[t], seed, nslots, nb, pil, slot)) {
+            if (++tries == 8) return fail(-1, "compact table placement failed");
+            seed = skq::cmp_mix(seed + 0x9E3779B9u);
+        }
+        std::vector<uint32_t> ent(nslots * 8, 0);
+        for (uint64_t j = 0; j < m; ++j) {
+            const uint32_t off = dvals[t][j], n = lists[off];
+            uint32_t* e = ent.data() + (uint64_t)slot[j] * 8;
+            e[0] = dkeys[t][j];
+            for (uint32_t q = 0; q < 7 && q < n; ++q) e[1 + q] = lists[off + 1 + q];
+            e[1] |= std::min<uint32_t>(n, skq::CMP_LONG) << 22;
+            if (n > 7) {
+                e[4] |= (off & 0x3FFu) << 22;
+                e[5] |= ((off >> 10) & 0x3FFu) << 22;
+                e[6] |= ((off >> 20) & 0x3FFu) << 22;
+                e[7] |= (off >> 30) << 22;
+            }
+        }
+        if (dev_alloc(&ix->d_wdir_t[t], nslots * 8) || dev_alloc(&ix->d_wpil_t[t], nb))
+            return fail(-3, "compact table allocation failed");
+        if (hipMemcpy(ix->d_wdir_t[t], ent.data(), nslots * 32, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(ix->d_wpil_t[t], pil.data(), (size_t)nb * 2, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(-3, "compact table upload failed");
+        need += nslots * 32 + (uint64_t)nb * 2;
+        for (uint32_t i = 0; i < ix->nk; ++i)
+            if (tables[t].k == ix->ks[i]) {
+                ix->wdir[i] = ix->d_wdir_t[t];
+                ix->dir_len[i] = nslots;
+                ix->wpil[i] = ix->d_wpil_t[t];
+                ix->wnb[i] = nb;
+                ix->wseed[i] = seed;
+            }
+    }
+    ix->dir_bytes = need;
+    ix->direct = true;
+    ix->mode = 5;
+    return 0;
+}
+
+// Probe structure, for ids that fit k_count3: wide tables when they fit SKQ_DIRECT_MB (default
+// 49152 MiB) and half the free device memory, else compact tables (a few % of the wide tables'
+// size); otherwise 4-B direct tables when they fit, else the bucket table alone.
+// SKQ_PROBE = wide | compact | block | dir | rank forces one kind (A/B measurements and the
+// parity tests, which run every kind).
 int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
                  const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals,
                  const std::vector<uint32_t>& lists) {
@@ -360,14 +481,22 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
     if (need == 0) return 0;
     const bool ids_ok = ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull;
-    if (force && !std::strcmp(force, "block")) {
+    auto forced = [&](const char* kind) { return force && !std::strcmp(force, kind); };
+    if (forced("block")) {
         if (!ids_ok || need / 2 > budget || need / 2 > fr / 2) return 0;
         return build_block(ix, ntables, tables, dkeys, dvals, lists);
     }
-    const bool wide_ok = ix->ntx <= (1u << 22) && need * 8 <= budget && need * 8 <= fr / 2 &&
-                         ix->nlist_words < 0x80000000ull;
-    if (wide_ok && !(force && !std::strcmp(force, "dir"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
-    if (force && !std::strcmp(force, "wide")) return 0;  // forced but does not fit: bucket table
+    const bool wide_ok = ids_ok && need * 8 <= budget && need * 8 <= fr / 2;
+    if (wide_ok && (!force || forced("wide"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
+    if (forced("wide")) return 0;  // forced but does not fit: bucket table
+    if (ids_ok && (!force || forced("compact"))) {
+        const int rc = build_compact(ix, ntables, tables, dkeys, dvals, lists);
+        if (rc == 0 || rc == -3 || forced("compact")) return rc;
+        for (auto& d : ix->d_wdir_t) dev_free(d);  // (placement failed: another kind)
+        for (auto& d : ix->d_wpil_t) dev_free(d);
+        for (auto& w : ix->wdir) w = nullptr;
+        for (auto& w : ix->wpil) w = nullptr;
+    }
     if (need > budget || need > fr / 2) return 0;
     hipStream_t st = nullptr;
     uint32_t *dk = nullptr, *dv = nullptr;
@@ -562,6 +691,7 @@ int skq_index_free(skq_index* ix) {
     for (auto& d : ix->d_dir_t) dev_free(d);
     for (auto& d : ix->d_wdir_t) dev_free(d);
     for (auto& d : ix->d_wovf_t) dev_free(d);
+    for (auto& d : ix->d_wpil_t) dev_free(d);
     for (auto& d : ix->d_rank_t) dev_free(d);
     for (auto& d : ix->d_rovf_t) dev_free(d);
     dev_free(ix->d_buckets);
@@ -830,13 +960,16 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
     p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
     // wide tables: the count kernel reads the sketch's hashes and gathers the entries itself
-    p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 4 ? 2 : 0;
+    p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 4 ? 2 : ix->mode == 5 ? 3 : 0;
     if (p.wide) {
         p.lofs = const_cast<uint32_t*>(hashes);
         for (uint32_t i = 0; i < ix->nk; ++i) {
             p.wdir[i] = ix->wdir[i];
             p.wdir_len[i] = ix->dir_len[i];
             p.wovf[i] = ix->wovf[i];
+            p.wpil[i] = ix->wpil[i];
+            p.wnb[i] = ix->wnb[i];
+            p.wseed[i] = ix->wseed[i];
         }
     }
     p.stamps = s->stamps;
@@ -872,8 +1005,8 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
                       fraction, accumulate, s->probed, stream);
 }
 
-// Fused map: k_map1 (wide or block tables, one k slot, a raw capacity of 16 or 32) or k_mapk
-// (wide tables, 2..4 k slots, capacity 16); anything else takes the two-kernel path (a caller
+// Fused map: k_map1 (compact, wide or block tables, one k slot, a raw capacity of 16 or 32) or
+// k_mapk (compact or wide tables, 2..4 k slots); anything else takes the two-kernel path (a caller
 // can always ask for that path itself with skq_sketch + skq_chain)
 static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,
                         uint32_t threshold) {
@@ -881,9 +1014,9 @@ static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t f
     if (!d_offs) max_len = fixed_len;
     const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
     const uint32_t hcap = pick_hcap(Lc, ix->mink, threshold);
-    if (ix->nk == 1) return (ix->mode == 3 || ix->mode == 4) && (hcap == 16 || hcap == 32);
-    // 2..4 k slots: k_mapk (wide tables, hcap 16 or 32)
-    return ix->mode == 3 && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32);
+    if (ix->nk == 1) return ix->mode >= 3 && (hcap == 16 || hcap == 32);
+    // 2..4 k slots: k_mapk (wide or compact tables, hcap 16 or 32)
+    return (ix->mode == 3 || ix->mode == 5) && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32);
 }
 
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,

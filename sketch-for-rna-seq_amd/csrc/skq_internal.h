@@ -148,6 +148,14 @@ struct ChainParams {
     // keys of a block (by key order) have entries [n, t0..t5] (n <= 6) or [0x80000000 | list
     // offset, t0..t5]; the 3rd+ key's list offset is wovf[i][overflow base + rank - 2].
     // wdir_len = blocks.
+    // Compact tables (wide = 3): the same 8-word entries, one per key, placed by a minimal
+    // perfect hash (cmp_slot below) in wdir_len[i] slots; wpil[i] holds one 16-bit pilot per
+    // bucket of keys (wnb[i] buckets, hash seed wseed[i]). Entry: [key, t0 | F << 22, t1 .. t6],
+    // F = n (1..7), 8 for a longer list (t0..t6 inline, the list at lists[offset]: offset bits
+    // 0-31 in bits 22-31 of words 4, 5, 6 and 22-23 of word 7), 0 for an empty slot.
+    const uint16_t* wpil[SKQ_MAX_K];
+    uint32_t wnb[SKQ_MAX_K];
+    uint32_t wseed[SKQ_MAX_K];
     int wide;
     const uint32_t* wdir[SKQ_MAX_K];
     uint64_t wdir_len[SKQ_MAX_K];
@@ -199,6 +207,23 @@ int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* va
 SKQ_HD inline uint32_t home_bucket(uint32_t key, uint32_t nbuckets) {
     return (uint32_t)(((uint64_t)(uint32_t)(key * HASH_MUL) * nbuckets) >> 32);
 }
+
+// Compact tables: key -> bucket (a 16-bit pilot each) -> slot. mix is murmur3's 32-bit finaliser
+// (a bijection); scale maps a 32-bit hash onto [0, n) by its high bits.
+SKQ_HD inline uint32_t cmp_mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+SKQ_HD inline uint32_t cmp_scale(uint32_t h, uint64_t n) { return (uint32_t)(((uint64_t)h * n) >> 32); }
+SKQ_HD inline uint32_t cmp_key_hash(uint32_t key, uint32_t seed) { return cmp_mix(key ^ seed); }
+SKQ_HD inline uint32_t cmp_slot(uint32_t kh, uint32_t pilot, uint64_t nslots) {
+    return cmp_scale(cmp_mix(kh ^ (pilot * 0x9E3779B1u)), nslots);
+}
+constexpr uint32_t CMP_LONG = 8;  // F of an entry whose list continues at lists[offset]
 size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap, bool nthash);
 
 // 33-bit ntHash lane (bits 0..32 of ntHash's split rotate evolve on their own)

@@ -1239,13 +1239,21 @@ struct Counter {
     }
 };
 
-// Up to 8 retained hashes of k slot i against a wide table: dl[u] = h << 3 (the entry's word
-// offset) or ~0u. Entries are gathered by lane pairs (each lane loads one 16-B half of both
-// lanes' entries, so a pair fetches whole 32-B entries; then the two swap the half that
-// belongs to the other), 4 per lane in flight; both lanes of every pair must run this.
-template <int NK, int PS, int B = 4>
+// Compact tables (ChainParams::wpil): the list offset of a long entry, from bits 22-31 of its
+// words 4-7 (the odd lane's half)
+__device__ __forceinline__ uint32_t cmp_long_off(const uint4& hi) {
+    return (hi.x >> 22) | ((hi.y >> 22) << 10) | ((hi.z >> 22) << 20) | ((hi.w >> 22) << 30);
+}
+constexpr uint32_t TID_MASK = 0x3FFFFFu;
+
+// Up to 8 retained hashes of k slot i against a wide or compact (CMP) table: dl[u] = the entry's
+// word offset or ~0u, hk[u] the hash (compact entries hold their key). Entries are gathered by
+// lane pairs (each lane loads one 16-B half of both lanes' entries, so a pair fetches whole 32-B
+// entries; then the two swap the half that belongs to the other), 4 per lane in flight; both
+// lanes of every pair must run this.
+template <int NK, int PS, bool CMP = false, int B = 4>
 __device__ __forceinline__ void wide_chunk(Counter<NK, PS>& c, const ChainParams& p, const uint32_t* wd,
-                                           const uint32_t (&dl)[8], bool odd, int i) {
+                                           const uint32_t (&dl)[8], const uint32_t (&hk)[8], bool odd, int i) {
     static_assert(B == 4 || B == 8, "batch of 4 or 8 entries per lane");
 #pragma unroll
     for (int u0 = 0; u0 < 8; u0 += B) {
@@ -1262,35 +1270,40 @@ __device__ __forceinline__ void wide_chunk(Counter<NK, PS>& c, const ChainParams
             la[u] = *reinterpret_cast<const uint4*>(wd + (ea != ~0u ? (uint64_t)ea : 0ull) + part);
             lb[u] = *reinterpret_cast<const uint4*>(wd + (eb != ~0u ? (uint64_t)eb : 0ull) + part);
         }
+        uint32_t nn[B];  // tids in the entry (> 7: the list continues at lists[offset])
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             const uint4 rcv = pair_swap(odd ? la[u] : lb[u]);
             const uint4 h = odd ? rcv : la[u], m = odd ? lb[u] : rcv;
-            head[u] = dl[u0 + u] != ~0u ? h : make_uint4(0, 0, 0, 0);
+            const bool v = dl[u0 + u] != ~0u;
+            head[u] = v ? h : make_uint4(0, 0, 0, 0);
             more[u] = m;
+            if (CMP) nn[u] = head[u].x == hk[u0 + u] ? head[u].y >> 22 : 0u;
+            else nn[u] = head[u].x;
         }
         bool lng = false;
 #pragma unroll
-        for (int u = 0; u < B; ++u) lng |= head[u].x > 3;
+        for (int u = 0; u < B; ++u) lng |= nn[u] > 3;
         const bool any_long = __any(lng);
+        constexpr uint32_t TM = CMP ? TID_MASK : 0xFFFFFFFFu;
 #pragma unroll
         for (int u = 0; u < B; ++u) {
-            const uint32_t n = head[u].x;  // [0x80000000 | offset] for lists longer than 7
-            c.insert(head[u].y, 1, i, n > 0);
-            c.insert(head[u].z, 1, i, n > 1);
-            c.insert(head[u].w, 1, i, n > 2);
+            const uint32_t n = nn[u];  // wide: [0x80000000 | offset] for lists longer than 7
+            c.insert(head[u].y & TM, 1, i, n > 0);
+            c.insert(head[u].z & TM, 1, i, n > 1);
+            c.insert(head[u].w & TM, 1, i, n > 2);
             if (any_long) {
-                c.insert(more[u].x, 1, i, n > 3);
-                c.insert(more[u].y, 1, i, n > 4);
-                c.insert(more[u].z, 1, i, n > 5);
-                c.insert(more[u].w, 1, i, n > 6);
+                c.insert(more[u].x & TM, 1, i, n > 3);
+                c.insert(more[u].y & TM, 1, i, n > 4);
+                c.insert(more[u].z & TM, 1, i, n > 5);
+                c.insert(more[u].w & TM, 1, i, n > 6);
             }
         }
         // lists longer than 7 (rare): the rest from the postings list, one at a time
 #pragma unroll
         for (int u = 0; u < B; ++u)
-            if (__any(head[u].x > 7) && head[u].x > 7) {
-                const uint32_t lo = head[u].x & 0x7FFFFFFFu;
+            if (__any(nn[u] > 7) && nn[u] > 7) {
+                const uint32_t lo = CMP ? cmp_long_off(more[u]) : nn[u] & 0x7FFFFFFFu;
                 const uint32_t len = p.lists[lo];
                 for (uint32_t q = 7; q < len; ++q) c.insert(p.lists[lo + 1 + q], 1, i, true);
             }
@@ -1299,13 +1312,14 @@ __device__ __forceinline__ void wide_chunk(Counter<NK, PS>& c, const ChainParams
 
 // one read of k_count3: writes its candidates (and cand_cnt) and returns their number, the
 // first nc of key[] holding them in output order. MODE: 0 = lofs hold list offsets (k_probe or
-// the fused dir/rank probe), 1 = wide tables, 2 = block tables (lofs hold the hashes).
+// the fused dir/rank probe), 1 = wide tables, 2 = block tables, 3 = compact tables (lofs hold
+// the hashes).
 // Wide tables are gathered by lane pairs (wide_chunk), so in MODE 1 every lane of the wave runs
 // the gather loops, reads past n and inactive reads with no hashes.
 template <int NK, int MODE>
 __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r, uint32_t t, uint32_t (*s_tab)[WG],
                                                uint32_t (*s_pend)[WG], uint32_t (&key)[TS]) {
-    constexpr bool COOP = MODE == 1;
+    constexpr bool COOP = MODE == 1 || MODE == 3;
     const bool inb = r < p.n;
     const uint64_t rr = inb ? r : p.n - 1;  // (p.n > 0)
     // one round trip for everything the read needs first: offsets past the read's count are
@@ -1363,10 +1377,23 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
             uint32_t dl[8];
             if (COOP) {
                 // lofs holds the read's distinct retained hashes, front-packed: each is one
-                // entry; a hash past the table is a miss
+                // entry; wide: a hash past the table is a miss; compact: the slot from the
+                // bucket's pilot (the entry's key decides the hit)
+                if (MODE == 3) {
+                    uint32_t kh[8], pv[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) dl[u] = (j0 + u < cnt && xs[u] < wlen) ? xs[u] << 3 : ~0u;
-                wide_chunk(c, p, wd, dl, t & 1u, i);
+                    for (int u = 0; u < 8; ++u) {
+                        kh[u] = cmp_key_hash(xs[u], p.wseed[i]);
+                        pv[u] = j0 + u < cnt ? p.wpil[i][cmp_scale(kh[u], p.wnb[i])] : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) dl[u] = j0 + u < cnt ? cmp_slot(kh[u], pv[u], wlen) << 3 : ~0u;
+                    wide_chunk<NK, WG, true>(c, p, wd, dl, xs, t & 1u, i);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) dl[u] = (j0 + u < cnt && xs[u] < wlen) ? xs[u] << 3 : ~0u;
+                    wide_chunk<NK, WG, false>(c, p, wd, dl, xs, t & 1u, i);
+                }
                 continue;
             }
             if (blocks) {
@@ -1569,7 +1596,7 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
     }
     uint32_t key[TS];
     uint32_t nc = 0;
-    if (MODE == 1 || r < p.n) nc = count_read<NK, MODE>(p, r, t, s_tab, s_pend, key);
+    if (MODE == 1 || MODE == 3 || r < p.n) nc = count_read<NK, MODE>(p, r, t, s_tab, s_pend, key);
     if (bin) bin_candidates(p, t, w, nc, key, s_bc, s_mem);
 }
 
@@ -1588,11 +1615,11 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
 // count words 0 on entry); flagw (the wave's 64 words, zeroed) marks reads with more than TS
 // transcripts. Writes each counted read's candidates, or lists it for the slow chain path;
 // returns the candidate count, key[] holding them in output order. Every lane must call it.
-template <int NK>
+template <int NK, bool CMP = false>
 __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64_t r, uint64_t rr, bool act,
                                                     uint32_t (&cnts)[NK], uint32_t* colbase, uint32_t* hl,
-                                                    uint8_t* ow, uint32_t cap, uint32_t* flagw, uint32_t lane,
-                                                    uint32_t (&key)[TS]) {
+                                                    uint8_t* ow, uint32_t* sll, uint32_t cap, uint32_t* flagw,
+                                                    uint32_t lane, uint32_t (&key)[TS]) {
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
     uint32_t m = 0;
 #pragma unroll
@@ -1615,6 +1642,24 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
 #pragma unroll
         for (int q = 1; q < NK; ++q) w = i == (uint32_t)q ? p.wdir_len[q] : w;
         return w;
+    };
+    // compact tables: k slot i's hash seed, and the pilot of hash h's bucket (constant i: the
+    // selects fold away)
+    auto seed_of = [&](uint32_t i) -> uint32_t {
+        uint32_t sd = p.wseed[0];
+#pragma unroll
+        for (int q = 1; q < NK; ++q) sd = i == (uint32_t)q ? p.wseed[q] : sd;
+        return sd;
+    };
+    auto pilot_of = [&](uint32_t i, uint32_t kh) -> uint32_t {
+        const uint16_t* pl = p.wpil[0];
+        uint32_t nb = p.wnb[0];
+#pragma unroll
+        for (int q = 1; q < NK; ++q) {
+            pl = i == (uint32_t)q ? p.wpil[q] : pl;
+            nb = i == (uint32_t)q ? p.wnb[q] : nb;
+        }
+        return pl[cmp_scale(kh, nb)];
     };
     // an insert whose home slot holds another transcript probes on (rare: not unrolled)
     auto ins_probe = [&](uint32_t x, uint32_t o, uint32_t inc) {
@@ -1644,6 +1689,7 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
 #pragma unroll
         for (int u = 0; u < 8; ++u) hx[i][u] = (uint32_t)u < cnts[i] ? src[(uint64_t)u * p.n] : 0u;
     }
+
     for (uint32_t pb = 0; pb < M; pb += cap) {  // wave-uniform
         // this lane's entries that fall in the pass, straight from the sketch's hash rows: the
         // first 8 of every k slot in one round trip (all loads issued before any store), the
@@ -1690,35 +1736,76 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t ne = min(M - pb, cap);
+        if constexpr (CMP) {
+            // compact tables: every listed hash's slot, one lane per entry (all of the lane's
+            // pilot loads in flight together), so the lane pairs gather without a dependent load
+            constexpr int SB = 4;  // (8 raises k_mapk's VGPRs past 128)
+            for (uint32_t e0 = 0; e0 < ne; e0 += 64 * SB) {
+                uint32_t kh[SB], pv[SB];
+#pragma unroll
+                for (int q = 0; q < SB; ++q) {
+                    const uint32_t e = e0 + lane + 64 * q;
+                    const uint32_t ee = e < ne ? e : 0;
+                    const uint32_t i = ow[ee] >> 6;
+                    kh[q] = cmp_key_hash(hl[ee], seed_of(i));
+                    pv[q] = e < ne ? pilot_of(i, kh[q]) : 0u;
+                }
+#pragma unroll
+                for (int q = 0; q < SB; ++q) {
+                    const uint32_t e = e0 + lane + 64 * q;
+                    if (e < ne) sll[e] = cmp_slot(kh[q], pv[q], wlen_of(ow[e] >> 6));
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         constexpr int R = 4;  // rounds of 32 entries in flight together
         for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
             uint4 w[R];
-            uint32_t own[R];
+            uint32_t own[R], hk[R];
             bool okk[R];
+            if constexpr (CMP) {
+                // one entry each, at the slot listed with the hash
 #pragma unroll
-            for (int u = 0; u < R; ++u) {
-                const uint32_t ee = e0 + 32 * u + (lane >> 1);
-                const bool in = ee < ne;
-                const uint32_t h = hl[in ? ee : 0];
-                own[u] = ow[in ? ee : 0];
-                const uint32_t i = own[u] >> 6;
-                okk[u] = in && h < wlen_of(i);
-                w[u] = *reinterpret_cast<const uint4*>(wd_of(i) + (okk[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
+                for (int u = 0; u < R; ++u) {
+                    const uint32_t e = e0 + 32 * u + (lane >> 1);
+                    okk[u] = e < ne;
+                    const uint32_t ee = okk[u] ? e : 0;
+                    hk[u] = hl[ee];
+                    own[u] = ow[ee];
+                    w[u] = *reinterpret_cast<const uint4*>(wd_of(own[u] >> 6) + (uint64_t)sll[ee] * 8 + (odd ? 4u : 0u));
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    const uint32_t ee = e0 + 32 * u + (lane >> 1);
+                    const bool in = ee < ne;
+                    hk[u] = hl[in ? ee : 0];
+                    own[u] = ow[in ? ee : 0];
+                    const uint32_t i = own[u] >> 6;
+                    okk[u] = in && hk[u] < wlen_of(i);
+                    w[u] = *reinterpret_cast<const uint4*>(wd_of(i) + (okk[u] ? (uint64_t)hk[u] << 3 : 0ull) + (odd ? 4u : 0u));
+                }
             }
+            constexpr uint32_t TM = CMP ? TID_MASK : 0xFFFFFFFFu;
 #pragma unroll
             for (int u = 0; u < R; ++u) {
-                const uint32_t sw = pair_swap(w[u].x);
-                const uint32_t n = okk[u] ? (odd ? sw : w[u].x) : 0u;  // [0x80000000 | offset] when long
+                // tids in the entry, pair-uniform (> 7: the list continues at lists[offset];
+                // wide: [0x80000000 | offset]); compact: the even lane's half holds key and F
+                const uint32_t mine = CMP ? (w[u].x == hk[u] ? w[u].y >> 22 : 0u) : w[u].x;
+                const uint32_t sw = pair_swap(mine);
+                const uint32_t n = okk[u] ? (odd ? sw : mine) : 0u;
                 const uint32_t qb = odd ? 3u : 0u;
                 const uint32_t o = own[u] & 63u, inc = 1u << (8 * (own[u] >> 6));
                 // the first attempts (a CAS at each tid's home slot) issue before any result is
                 // looked at; a tid found there gets a non-returning add of its k slot's count
                 uint32_t xs[4], olds[4];
                 bool vs[4];
-                xs[0] = odd ? w[u].x : w[u].y;
-                xs[1] = odd ? w[u].y : w[u].z;
-                xs[2] = odd ? w[u].z : w[u].w;
-                xs[3] = w[u].w;
+                xs[0] = (odd ? w[u].x : w[u].y) & TM;
+                xs[1] = (odd ? w[u].y : w[u].z) & TM;
+                xs[2] = (odd ? w[u].z : w[u].w) & TM;
+                xs[3] = w[u].w & TM;
                 vs[0] = n > qb;
                 vs[1] = n > qb + 1;
                 vs[2] = n > qb + 2;
@@ -1735,9 +1822,11 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
                     if (olds[q] == EMPTY || olds[q] == xs[q]) atomicAdd(colbase + (2 * sl + 1) * WG + ((o + sl) & 63u), inc);
                     else ins_probe(xs[q], o, inc);
                 }
-                // lists longer than 7 (rare): the even lane inserts the rest of the list
-                if (__any(!odd && n > 7) && !odd && n > 7) {
-                    const uint32_t lo = n & 0x7FFFFFFFu;
+                // lists longer than 7 (rare): the lane holding the offset (wide: even, compact:
+                // odd) inserts the rest of the list
+                const bool tl = n > 7 && (CMP ? odd : !odd);
+                if (__any(tl) && tl) {
+                    const uint32_t lo = CMP ? cmp_long_off(w[u]) : n & 0x7FFFFFFFu;
                     const uint32_t len = p.lists[lo];
                     for (uint32_t q = 7; q < len; ++q) ins(p.lists[lo + 1 + q], o, inc);
                 }
@@ -1802,13 +1891,14 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
 }
 
 constexpr uint32_t CW_P = 512;
-template <int NK>
+template <int NK, bool CMP>
 __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
     static_assert(NK >= 2 && NK <= NK_FAST, "2..4 k slots (8-bit counts packed per k)");
     static_assert(2 * TS >= CCAP, "the binned region reuses the count tables");
     __shared__ __attribute__((aligned(16))) uint32_t s_tabs[2 * TS * WG];
     __shared__ uint32_t s_hl[WG / 64][CW_P];
     __shared__ uint8_t s_ow[WG / 64][CW_P];
+    __shared__ uint32_t s_sl[CMP ? WG / 64 : 1][CMP ? CW_P : 1];
     __shared__ uint32_t s_flag[WG];
     __shared__ uint32_t s_bc[WG + 1];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -1835,7 +1925,8 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
     if (inb && !act) p.cand_cnt[r] = 0;
     uint32_t key[TS];
     __syncthreads();  // (the tables, flags and binning counts above are set)
-    const uint32_t nc = wide_count_wave<NK>(p, r, rr, act, cnts, s_tabs + wv * 64, s_hl[wv], s_ow[wv], CW_P,
+    const uint32_t nc = wide_count_wave<NK, CMP>(p, r, rr, act, cnts, s_tabs + wv * 64, s_hl[wv], s_ow[wv],
+                                                 CMP ? s_sl[wv] : nullptr, CW_P,
                                             s_flag + wv * 64, lane, key);
     // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
     if (bin) bin_candidates(p, t, blockIdx.x, nc, key, s_bc, s_tabs);
@@ -1849,7 +1940,9 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 constexpr uint32_t MAP_P = 384;
 __host__ __device__ inline size_t map1_wave_bytes(uint32_t wc) {
     const size_t a = sketch_codes_bytes(wc);
-    const size_t b = (size_t)MAP_P * 5 + 64 * 4;  // the list, then the per-read overflow flags
+    // the list: hashes, then owning lanes (u8; compact tables: u32 slot | lane << 26), then the
+    // per-read overflow flags
+    const size_t b = (size_t)MAP_P * 8 + 64 * 4;
     const size_t c = (size_t)(WG + 1) * 4;
     const size_t m = a > b ? a : b;
     return ((m > c ? m : c) + 15) & ~(size_t)15;
@@ -1874,8 +1967,10 @@ size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
             cp.stamps[((uint64_t)blockIdx.x * (WG / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-template <int HCAP, int MB, bool BLK, bool NT = true>
+// TAB: 0 = wide tables, 1 = block tables, 2 = compact tables
+template <int HCAP, int MB, int TAB>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
+    constexpr bool BLK = TAB == 1, CMP = TAB == 2;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
@@ -1916,14 +2011,12 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
             uint4 vv[SU];
 #pragma unroll
-            for (uint32_t u = 0; u < SU; ++u)
-                if (NT) {  // (non-temporal: the streamed bases do not evict the entries' lines; +2 %)
-                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + min(cb + u * 64, nch - 1)));
-                    vv[u] = make_uint4(x.x, x.y, x.z, x.w);
-                } else {
-                    vv[u] = src[min(cb + u * 64, nch - 1)];
-                }
+            for (uint32_t u = 0; u < SU; ++u) {
+                // (non-temporal: the streamed bases do not evict the entries' lines; +2 %)
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + min(cb + u * 64, nch - 1)));
+                vv[u] = make_uint4(x.x, x.y, x.z, x.w);
+            }
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u) {
                 const uint32_t c = cb + u * 64;
@@ -2072,13 +2165,16 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
-    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 5);  // per read: > TS transcripts
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 8);  // per read: > TS transcripts
     s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
+    uint32_t* s_x = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 4);  // compact: slot | lane << 26
     uint32_t* colbase = s_raw + wv * 64;
     const uint32_t* wd = cp.wdir[0];
     const uint64_t wlen = cp.wdir_len[0];
+    const uint16_t* cpil = cp.wpil[0];
+    const uint32_t cnb = cp.wnb[0], cseed = cp.wseed[0];
     const bool odd = lane & 1u;
     // slot sl of read (lane) o sits in column (o + sl) & 63 of row sl: the slots of one read
     // fall in distinct LDS banks (the lane pairs of one round mostly insert into the same read)
@@ -2115,7 +2211,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             const uint32_t e = off + rank;
             if (kj && e < MAP_P) {
                 s_h[e] = v[j];
-                s_own[e] = (uint8_t)lane;
+                if (CMP) s_x[e] = lane << 26;
+                else s_own[e] = (uint8_t)lane;
             }
             rank += kj ? 1u : 0u;
         }
@@ -2130,7 +2227,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 const uint32_t e = off + d;
                 if (e >= pb && e < pb + MAP_P) {
                     s_h[e - pb] = p.hashes[(uint64_t)d * p.n + r];
-                    s_own[e - pb] = (uint8_t)lane;
+                    if (CMP) s_x[e - pb] = lane << 26;
+                    else s_own[e - pb] = (uint8_t)lane;
                 }
             }
         }
@@ -2138,6 +2236,27 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t ne = min(M - pb, (uint32_t)MAP_P);
+        if constexpr (CMP) {
+            // compact tables: every listed hash's slot, one lane per entry: the bucket's pilot
+            // (an L2-resident array; all of the lane's pilot loads in flight together), then the
+            // slot, so the lane pairs below gather without a dependent load or any hashing
+            constexpr int SB = (MAP_P + 63) / 64;
+            uint32_t kh[SB], pv[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                const uint32_t e = lane + 64 * q;
+                kh[q] = cmp_key_hash(s_h[e < ne ? e : 0], cseed);
+                pv[q] = e < ne ? cpil[cmp_scale(kh[q], cnb)] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                const uint32_t e = lane + 64 * q;
+                if (e < ne) s_x[e] |= cmp_slot(kh[q], pv[q], wlen);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         constexpr int R = MB;  // rounds of 32 entries in flight together
         if constexpr (BLK) {
             // block tables (DESIGN.md "Index"): one 64-B block per hash, the even lane loading
@@ -2206,32 +2325,50 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         }
         for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
             uint4 w[R];
-            uint32_t own[R];
+            uint32_t own[R], hk[R];
             bool ok[R];
+            if constexpr (CMP) {
+                // one entry each, at the slot listed with the hash
 #pragma unroll
-            for (int u = 0; u < R; ++u) {
-                const uint32_t e = e0 + 32 * u + (lane >> 1);
-                const bool in = e < ne;
-                const uint32_t h = s_h[in ? e : 0];
-                own[u] = s_own[in ? e : 0];
-                ok[u] = in && h < wlen;
-                w[u] = *reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)h << 3 : 0ull) + (odd ? 4u : 0u));
+                for (int u = 0; u < R; ++u) {
+                    const uint32_t e = e0 + 32 * u + (lane >> 1);
+                    ok[u] = e < ne;
+                    const uint32_t ee = ok[u] ? e : 0;
+                    hk[u] = s_h[ee];
+                    const uint32_t x = s_x[ee];
+                    own[u] = x >> 26;
+                    w[u] = *reinterpret_cast<const uint4*>(wd + (uint64_t)(x & 0x3FFFFFFu) * 8 + (odd ? 4u : 0u));
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    const uint32_t e = e0 + 32 * u + (lane >> 1);
+                    const bool in = e < ne;
+                    hk[u] = s_h[in ? e : 0];
+                    own[u] = s_own[in ? e : 0];
+                    ok[u] = in && hk[u] < wlen;
+                    w[u] = *reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)hk[u] << 3 : 0ull) + (odd ? 4u : 0u));
+                }
             }
+            constexpr uint32_t TM = CMP ? TID_MASK : 0xFFFFFFFFu;
             // the inserts of each entry: the four first attempts (a CAS at each tid's home slot)
             // are issued before any result is looked at, one LDS round trip; a tid already there
             // gets a non-returning add, and only a slot held by another tid sends the insert on
             // to the probing loop
 #pragma unroll
             for (int u = 0; u < R; ++u) {
-                const uint32_t sw = pair_swap(w[u].x);
-                const uint32_t n = ok[u] ? (odd ? sw : w[u].x) : 0u;  // [0x80000000 | offset] when long
+                // tids in the entry, pair-uniform (> 7: the list continues at lists[offset];
+                // wide: [0x80000000 | offset]); compact: the even lane's half holds key and F
+                const uint32_t mine = CMP ? (w[u].x == hk[u] ? w[u].y >> 22 : 0u) : w[u].x;
+                const uint32_t sw = pair_swap(mine);
+                const uint32_t n = ok[u] ? (odd ? sw : mine) : 0u;
                 const uint32_t qb = odd ? 3u : 0u;
                 uint32_t xs[4], olds[4];
                 bool vs[4];
-                xs[0] = odd ? w[u].x : w[u].y;
-                xs[1] = odd ? w[u].y : w[u].z;
-                xs[2] = odd ? w[u].z : w[u].w;
-                xs[3] = w[u].w;
+                xs[0] = (odd ? w[u].x : w[u].y) & TM;
+                xs[1] = (odd ? w[u].y : w[u].z) & TM;
+                xs[2] = (odd ? w[u].z : w[u].w) & TM;
+                xs[3] = w[u].w & TM;
                 vs[0] = n > qb;
                 vs[1] = n > qb + 1;
                 vs[2] = n > qb + 2;
@@ -2249,9 +2386,11 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     if ((o >> 8) == x) atomicAdd(colbase + sl * WG + ((own[u] + sl) & 63u), 1u);
                     else ains_probe(x, own[u]);
                 }
-                // lists longer than 7 (rare): the even lane inserts the rest of the list
-                if (__any(!odd && n > 7) && !odd && n > 7) {
-                    const uint32_t lo = n & 0x7FFFFFFFu;
+                // lists longer than 7 (rare): the lane holding the offset (wide: even, compact:
+                // odd) inserts the rest of the list
+                const bool tl = n > 7 && (CMP ? odd : !odd);
+                if (__any(tl) && tl) {
+                    const uint32_t lo = CMP ? cmp_long_off(w[u]) : n & 0x7FFFFFFFu;
                     const uint32_t len = cp.lists[lo];
                     for (uint32_t q = 7; q < len; ++q) ains(cp.lists[lo + 1 + q], own[u]);
                 }
@@ -2327,7 +2466,7 @@ size_t mapk_lds_bytes(uint32_t nk, uint32_t wave_chunks, uint32_t hcap) {
            (size_t)WG * 4 + (size_t)(WG + 1) * 4;
 }
 
-template <int NK, int HCAP>
+template <int NK, int HCAP, bool CMP>
 __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
@@ -2520,10 +2659,13 @@ __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t cap = (uint32_t)(wave_bytes / 5) & ~31u;  // list entries a pass: hashes, then owners
+    // list entries a pass: hashes, then owners (then, compact tables, the hashes' slots)
+    const uint32_t cap = (uint32_t)(wave_bytes / (CMP ? 9 : 5)) & ~31u;
     uint32_t key[TS];
-    const uint32_t nc = wide_count_wave<NK>(cp, r, r, act, cnts, s_rows + wv * 64, reinterpret_cast<uint32_t*>(s_wave),
-                                            s_wave + (size_t)cap * 4, cap, s_flag + wv * 64, lane, key);
+    const uint32_t nc = wide_count_wave<NK, CMP>(cp, r, r, act, cnts, s_rows + wv * 64, reinterpret_cast<uint32_t*>(s_wave),
+                                                 s_wave + (size_t)cap * 4,
+                                                 reinterpret_cast<uint32_t*>(s_wave + (size_t)cap * 5), cap,
+                                                 s_flag + wv * 64, lane, key);
     // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
     if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_rows);
 }
@@ -2901,16 +3043,28 @@ int launch_count(const ChainParams& p, void* stream) {
             }
         };
         // wide tables, 2..4 k slots: the entry-parallel count
-        if (p.wide == 1 && p.nk >= 2 && p.nk <= (uint32_t)NK_FAST && p.status && !p.present && !p.hash_offs) {
+        if ((p.wide == 1 || p.wide == 3) && p.nk >= 2 && p.nk <= (uint32_t)NK_FAST && p.status && !p.present &&
+            !p.hash_offs) {
+            const bool cmp = p.wide == 3;
             switch (p.nk) {
-            case 2: hipLaunchKernelGGL((k_countw<2>), grid, dim3(WG), 0, st, p); break;
-            case 3: hipLaunchKernelGGL((k_countw<3>), grid, dim3(WG), 0, st, p); break;
-            default: hipLaunchKernelGGL((k_countw<4>), grid, dim3(WG), 0, st, p); break;
+            case 2:
+                if (cmp) hipLaunchKernelGGL((k_countw<2, true>), grid, dim3(WG), 0, st, p);
+                else hipLaunchKernelGGL((k_countw<2, false>), grid, dim3(WG), 0, st, p);
+                break;
+            case 3:
+                if (cmp) hipLaunchKernelGGL((k_countw<3, true>), grid, dim3(WG), 0, st, p);
+                else hipLaunchKernelGGL((k_countw<3, false>), grid, dim3(WG), 0, st, p);
+                break;
+            default:
+                if (cmp) hipLaunchKernelGGL((k_countw<4, true>), grid, dim3(WG), 0, st, p);
+                else hipLaunchKernelGGL((k_countw<4, false>), grid, dim3(WG), 0, st, p);
+                break;
             }
             return hipGetLastError() == hipSuccess ? 0 : -2;
         }
         if (p.wide == 1) go(std::integral_constant<int, 1>{});
         else if (p.wide == 2) go(std::integral_constant<int, 2>{});
+        else if (p.wide == 3) go(std::integral_constant<int, 3>{});
         else go(std::integral_constant<int, 0>{});
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
@@ -2979,16 +3133,14 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
     const size_t lds = map1_lds_bytes(p.tile_chunks, p.hcap);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    switch (p.hcap) {
-    case 16:
-        // (MB: gather rounds in flight)
-        if (cp.wide == 2) hipLaunchKernelGGL((k_map1<16, 4, true>), grid, dim3(WG), lds, st, p, cp);
-        else hipLaunchKernelGGL((k_map1<16, 4, false>), grid, dim3(WG), lds, st, p, cp);
-        break;
-    case 32:
-        if (cp.wide == 2) hipLaunchKernelGGL((k_map1<32, 4, true>), grid, dim3(WG), lds, st, p, cp);
-        else hipLaunchKernelGGL((k_map1<32, 4, false>), grid, dim3(WG), lds, st, p, cp);
-        break;
+    // (MB: gather rounds in flight)
+    switch (p.hcap * 4 + (cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
+    case 64: hipLaunchKernelGGL((k_map1<16, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
+    case 65: hipLaunchKernelGGL((k_map1<16, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
+    case 66: hipLaunchKernelGGL((k_map1<16, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;
+    case 128: hipLaunchKernelGGL((k_map1<32, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
+    case 129: hipLaunchKernelGGL((k_map1<32, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
+    case 130: hipLaunchKernelGGL((k_map1<32, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -3007,13 +3159,15 @@ int launch_mapk(const SketchParams& p, const ChainParams& cp, void* stream) {
                                       (int)lds);
         hipLaunchKernelGGL(kern, grid, dim3(WG), lds, st, p, cp);
     };
+    if (cp.wide != 1 && cp.wide != 3) return -4;
+    const bool cmp = cp.wide == 3;
     switch (p.nk * 100 + p.hcap) {
-    case 216: go(k_mapk<2, 16>); break;
-    case 316: go(k_mapk<3, 16>); break;
-    case 416: go(k_mapk<4, 16>); break;
-    case 232: go(k_mapk<2, 32>); break;
-    case 332: go(k_mapk<3, 32>); break;
-    case 432: go(k_mapk<4, 32>); break;
+    case 216: cmp ? go(k_mapk<2, 16, true>) : go(k_mapk<2, 16, false>); break;
+    case 316: cmp ? go(k_mapk<3, 16, true>) : go(k_mapk<3, 16, false>); break;
+    case 416: cmp ? go(k_mapk<4, 16, true>) : go(k_mapk<4, 16, false>); break;
+    case 232: cmp ? go(k_mapk<2, 32, true>) : go(k_mapk<2, 32, false>); break;
+    case 332: cmp ? go(k_mapk<3, 32, true>) : go(k_mapk<3, 32, false>); break;
+    case 432: cmp ? go(k_mapk<4, 32, true>) : go(k_mapk<4, 32, false>); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

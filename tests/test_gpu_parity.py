@@ -17,16 +17,18 @@ pytestmark = pytest.mark.gpu
 SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the wide-split mode)
 
 
-@pytest.fixture(autouse=True, params=["block", "wide", "wide-split", "dir", "rank", "bucket"])
+@pytest.fixture(autouse=True, params=["compact", "compact-split", "block", "wide", "wide-split", "dir", "rank",
+                                      "bucket"])
 def probe_mode(request, monkeypatch):
-    """Every test runs with each index probe structure: block tables and wide direct tables
-    gathered by the count kernel, 4-B direct tables probed inside the sketch kernel, and the bucket table probed by
-    k_probe (SKQ_DIRECT_MB=0)."""
+    """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables,
+    block tables and wide direct tables gathered by the map or count kernel, 4-B direct and rank
+    tables probed inside the sketch kernel, and the bucket table probed by k_probe
+    (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map)."""
     if request.param == "bucket":
         monkeypatch.setenv("SKQ_DIRECT_MB", "0")
-    elif request.param == "wide-split":  # wide tables through skq_sketch + skq_chain (no fused map)
+    elif request.param.endswith("-split"):
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
-        monkeypatch.setenv("SKQ_PROBE", "wide")
+        monkeypatch.setenv("SKQ_PROBE", request.param.split("-")[0])
         monkeypatch.setattr(sys.modules[__name__], "SPLIT", True)
     else:
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
@@ -441,7 +443,7 @@ def test_very_long_reads_and_large_postings():
 
 @pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
 def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
-    """With wide tables, 2-4 k slots map through the fused k_mapk (no separate count launch);
+    """With wide or compact tables, 2-4 k slots map through the fused k_mapk (no separate count launch);
     every other probe structure through k_sketch + a count kernel. Both bit-exact."""
     gi, oi = build(ks, tx=tx300)
     bases, _, _ = synth.reads(tx300, 2000, read_len, seed=77, err=0.002)
@@ -458,7 +460,7 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     s.check()
     s.enable_timing(False)
     count_launches = s.kernel_time(2)[1]
-    if probe_mode == "wide":
+    if probe_mode in ("wide", "compact"):
         assert count_launches == 0 and s.kernel_time(0)[1] == 1
     else:
         assert count_launches == 1
