@@ -106,6 +106,8 @@ struct skq_session {
     uint64_t hash_ext_cap = 0;
     uint32_t* ovf1 = nullptr;
     uint32_t* ovf2 = nullptr;
+    uint32_t* ovf3 = nullptr;  // second-level lists behind k_slow_wave
+    uint32_t* ovf4 = nullptr;
     uint32_t ovf_cap = 0;
     uint32_t* cand_cnt = nullptr;
     uint32_t* cand_tid = nullptr;
@@ -114,11 +116,13 @@ struct skq_session {
     uint64_t cand_ext_cap = 0;
     uint64_t* scratch = nullptr;
     uint64_t scratch_cap = 0;
-    uint64_t* tx_acc = nullptr;
     // per-transcript totals by buckets of 2^bin_bits ids (k_bin / k_bin_sum); bin_nb = 0: direct
     uint32_t bin_bits = 13, bin_nb = 0;
-    uint32_t* bin_hdr = nullptr;
-    uint32_t* bin_region = nullptr;
+    // double-buffered by batch parity: a batch's k_bin_sum (side stream) reads its bins while
+    // the next batch's map kernel writes the other set
+    uint32_t* bin_hdr[2] = {};
+    uint32_t* bin_region[2] = {};
+    uint32_t bin_par = 0;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     uint32_t* ctrl = nullptr;
@@ -130,7 +134,8 @@ struct skq_session {
     uint64_t* stamps = nullptr;  // development: k_map1 phase clocks (skq_session_set_stamps)
     // side stream for the totals (k_bin_sum runs beside the slow paths), created on first use
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork{}, ev_join{};
+    hipEvent_t ev_fork{}, ev_join[2]{};  // ev_join[b]: k_bin_sum of the last batch of parity b
+    bool join_rec[2] = {false, false};
 };
 
 int skq::session_device(const skq_session* s) { return s->idx->device; }
@@ -413,6 +418,8 @@ int build_compact(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
         const uint64_t m = dkeys[t].size();
         if (m == 0) continue;
         const uint64_t nslots = std::max<uint64_t>(m + 1, (uint64_t)std::ceil((double)m / 0.95));
+        // (5 keys per bucket: larger buckets, for a smaller pilot array, fail to place at 0.8-0.9
+        // load within 16-bit pilots; 2.7 s of host time at 4.24M keys)
         const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (m + 4) / 5);
         // (slots are listed as slot | lane << 26 in k_map1)
         if (nslots > (1ull << 26)) return fail(-1, "index too large for compact tables");
@@ -740,13 +747,13 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     int rc = 0;
     if ((rc = dev_alloc(&s->status, max_reads)) || (rc = dev_alloc(&s->hash_cnt, max_reads * ix->nk)) ||
         (rc = dev_alloc(&s->hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&s->ovf1, s->ovf_cap)) ||
-        (rc = dev_alloc(&s->ovf2, s->ovf_cap)) || (rc = dev_alloc(&s->cand_cnt, max_reads)) ||
+        (rc = dev_alloc(&s->ovf2, s->ovf_cap)) || (rc = dev_alloc(&s->ovf3, s->ovf_cap)) ||
+        (rc = dev_alloc(&s->ovf4, s->ovf_cap)) || (rc = dev_alloc(&s->cand_cnt, max_reads)) ||
         (rc = dev_alloc(&s->pflag, max_reads)) ||
         (rc = dev_alloc(&s->cand_tid, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
         (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
-        (rc = dev_alloc(&s->tx_acc, ix->ntx)) ||
         (rc = dev_alloc(&s->ctrl, skq::C_WORDS)) || (rc = ensure_hashes(s, hcap0))) {
         skq_session_free(s);
         return rc;
@@ -755,13 +762,13 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
     s->bin_nb = s->bin_bits <= 14 ? (uint32_t)(((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits) : 0u;
     const uint64_t nW = (max_reads + skq::WG - 1) / skq::WG;
-    if (s->bin_nb && ((rc = dev_alloc(&s->bin_hdr, (uint64_t)(s->bin_nb + 1) * nW)) ||
-                      (rc = dev_alloc(&s->bin_region, nW * skq::WG * skq::CCAP)))) {
-        skq_session_free(s);
-        return rc;
-    }
+    for (int b = 0; b < 2 && s->bin_nb; ++b)
+        if ((rc = dev_alloc(&s->bin_hdr[b], (uint64_t)(s->bin_nb + 1) * nW)) ||
+            (rc = dev_alloc(&s->bin_region[b], nW * skq::WG * skq::CCAP))) {
+            skq_session_free(s);
+            return rc;
+        }
     if (hipMemset(s->tx_reads, 0, ix->ntx * 8ull) != hipSuccess ||
-        hipMemset(s->tx_acc, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->ctrl, 0, skq::C_WORDS * 4) != hipSuccess) {
         skq_session_free(s);
@@ -782,7 +789,8 @@ int skq_session_free(skq_session* s) {
         (void)hipStreamSynchronize(s->side);
         (void)hipStreamDestroy(s->side);
         (void)hipEventDestroy(s->ev_fork);
-        (void)hipEventDestroy(s->ev_join);
+        (void)hipEventDestroy(s->ev_join[0]);
+        (void)hipEventDestroy(s->ev_join[1]);
     }
     dev_free(s->status);
     dev_free(s->hash_cnt);
@@ -792,14 +800,17 @@ int skq_session_free(skq_session* s) {
     dev_free(s->hash_ext);
     dev_free(s->ovf1);
     dev_free(s->ovf2);
+    dev_free(s->ovf3);
+    dev_free(s->ovf4);
     dev_free(s->cand_cnt);
     dev_free(s->cand_tid);
     dev_free(s->cand_score);
     dev_free(s->cand_ext);
     dev_free(s->scratch);
-    dev_free(s->tx_acc);
-    dev_free(s->bin_hdr);
-    dev_free(s->bin_region);
+    for (int b = 0; b < 2; ++b) {
+        dev_free(s->bin_hdr[b]);
+        dev_free(s->bin_region[b]);
+    }
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -841,6 +852,7 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     p.hash_ext_cap = s->hash_ext_cap;
     p.ctrl = s->ctrl;
     p.ovf1 = s->ovf1;
+    p.ovf_word = skq::C_OVF1;
     p.fuse = ix->mode;
     for (uint32_t i = 0; i < ix->nk; ++i) {
         p.dir[i] = ix->dir[i];
@@ -881,10 +893,25 @@ int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_off
     return sketch_impl(s, d_seqs, d_offs, fixed_len, n_seqs, max_len, threshold, 1, stream);
 }
 
-// The tail of a chain: the slow chain path (after the slow sketch path, when given) and the
-// per-transcript totals. When the count kernel binned the fast reads' candidates, k_bin_sum only
-// reads those bins and adds into tx_acc, as k_chain_slow does for its reads: it runs on the
-// session's side stream beside the slow paths, and the fold waits for both.
+// Totals on the side stream: a batch's k_bin_sum may still run when the next batch starts. The
+// kernel that next bins into the same buffer (two batches on) waits for it; every reader of the
+// running totals waits for both.
+static int wait_bins(skq_session* s, hipStream_t st) {
+    if (s->side && s->join_rec[s->bin_par]) HIP_TRY(hipStreamWaitEvent(st, s->ev_join[s->bin_par], 0));
+    return 0;
+}
+
+static int wait_totals(skq_session* s, hipStream_t st) {
+    for (int b = 0; b < 2; ++b)
+        if (s->side && s->join_rec[b]) HIP_TRY(hipStreamWaitEvent(st, s->ev_join[b], 0));
+    return 0;
+}
+
+// The tail of a chain: the slow paths and the per-transcript totals. When the count kernel binned
+// the fast reads' candidates, k_bin_sum only reads those bins and adds into the running totals
+// with atomics (commuting with the slow paths' direct adds). For batches of 4M+ reads it runs on
+// the session's side stream and nothing on the launch stream waits for it: it overlaps the slow
+// paths and the next batch's map kernel, which bins into the other buffer (wait_bins).
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
                       hipStream_t st) {
     // (small batches: the extra stream hand-offs cost more than the overlap gains: 1M reads ran
@@ -895,28 +922,39 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         if (!s->side) {
             HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_join[0], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_join[1], hipEventDisableTiming));
         }
         HIP_TRY(hipEventRecord(s->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
         record(s, 3, &t0, s->side);
         if (skq::launch_bin(p, 1, s->side)) return fail(-3, "totals launch failed");
         record_stop(s, 3, t0, s->side);
-        HIP_TRY(hipEventRecord(s->ev_join, s->side));
+        HIP_TRY(hipEventRecord(s->ev_join[s->bin_par], s->side));
+        s->join_rec[s->bin_par] = true;
     }
-    if (sp && skq::launch_sketch_slow(*sp, st)) return fail(-3, "sketch slow-path launch failed");
-    if (skq::launch_chain_slow(p, st)) return fail(-3, "chain slow-path launch failed");
-    if (accumulate) {
-        if (fork) {
-            HIP_TRY(hipStreamWaitEvent(st, s->ev_join, 0));
-        } else {
-            record(s, 3, &t0, st);
-            if (skq::launch_bin(p, p.slow_totals, st)) return fail(-3, "totals launch failed");
-            record_stop(s, 3, t0, st);
-        }
-        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, st))
-            return fail(-3, "totals fold launch failed");
+    if (sp && (p.wide == 1 || p.wide == 3) && p.nk <= (uint32_t)skq::NK_FAST) {
+        // the fused map's slow reads: the wave path first, the general paths for what it leaves
+        if (int rc = skq::launch_slow_wave(*sp, p, s->ovf3, s->ovf4, st))
+            return fail(-3, rc == -4 ? "slow path: unsupported tables" : "slow-path launch failed");
+        skq::SketchParams sp2 = *sp;
+        sp2.ovf1 = s->ovf3;
+        sp2.ovf_word = skq::C_OVF3;
+        skq::ChainParams p2 = p;
+        p2.ovf2 = s->ovf4;
+        p2.ovf_word = skq::C_OVF4;
+        if (skq::launch_sketch_slow(sp2, st, 256)) return fail(-3, "sketch slow-path launch failed");
+        if (skq::launch_chain_slow(p2, st, 256)) return fail(-3, "chain slow-path launch failed");
+    } else {
+        if (sp && skq::launch_sketch_slow(*sp, st)) return fail(-3, "sketch slow-path launch failed");
+        if (skq::launch_chain_slow(p, st)) return fail(-3, "chain slow-path launch failed");
     }
+    if (accumulate && !fork) {
+        record(s, 3, &t0, st);
+        if (skq::launch_bin(p, p.slow_totals, st)) return fail(-3, "totals launch failed");
+        record_stop(s, 3, t0, st);
+    }
+    if (accumulate && p.bin_nb) s->bin_par ^= 1;  // this batch's bins were written
     return 0;
 }
 
@@ -950,11 +988,11 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.cand_ext_cap = s->cand_ext_cap;
     p.scratch = s->scratch;
     p.scratch_cap = s->scratch_cap;
-    p.tx_acc = s->tx_acc;
     p.tx_reads = s->tx_reads;
     p.tx_score = s->tx_score;
     p.ctrl = s->ctrl;
     p.ovf2 = s->ovf2;
+    p.ovf_word = skq::C_OVF2;
     p.lofs = s->lofs;
     p.pflag = s->pflag;
     // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
@@ -976,14 +1014,15 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
     p.bin_nb = s->bin_nb;
-    p.bin_hdr = s->bin_hdr;
-    p.bin_region = s->bin_region;
+    p.bin_hdr = s->bin_hdr[s->bin_par];
+    p.bin_region = s->bin_region[s->bin_par];
     p.slow_totals = accumulate && skq::count_bins(p);
     if (prep) {
         *prep = p;
         return 0;
     }
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
+    if (int rc = wait_bins(s, st)) return rc;
     hipEvent_t t0{};
     if (!probed) {
         record(s, 1, &t0, st);
@@ -1031,6 +1070,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
+    if (int rc = wait_bins(s, st)) return rc;
     hipEvent_t t0{};
     record(s, 0, &t0, st);
     const int rc = s->idx->nk == 1 ? skq::launch_map1(sp, cp, stream) : skq::launch_mapk(sp, cp, stream);
@@ -1112,8 +1152,8 @@ int skq_session_reset_totals(skq_session* s, void* stream) {
     if (!s) return fail(-1, "null session");
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (int rc = wait_totals(s, st)) return rc;
     HIP_TRY(hipMemsetAsync(s->tx_reads, 0, s->idx->ntx * 8ull, st));
-    HIP_TRY(hipMemsetAsync(s->tx_acc, 0, s->idx->ntx * 8ull, st));
     HIP_TRY(hipMemsetAsync(s->tx_score, 0, s->idx->ntx * 8ull, st));
     return 0;
 }
@@ -1206,6 +1246,7 @@ int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, i
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const size_t bytes = s->idx->ntx * 8ull;
     const hipMemcpyKind kind = to_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (int rc = wait_totals(s, st)) return rc;
     if (tx_reads) HIP_TRY(hipMemcpyAsync(tx_reads, s->tx_reads, bytes, kind, st));
     if (tx_score) HIP_TRY(hipMemcpyAsync(tx_score, s->tx_score, bytes, kind, st));
     if (!to_device) HIP_TRY(hipStreamSynchronize(st));

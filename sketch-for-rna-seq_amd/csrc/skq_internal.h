@@ -28,10 +28,12 @@ enum Ctrl : int {
     C_OVF1 = 0,     // sketch overflow list length
     C_ERR1 = 1,     // sketch error bits
     C_BUMP_H = 2,   // u64 (words 2-3): hash_ext words used
+    C_OVF3 = 4,     // second-level sketch list (k_slow_wave -> k_sketch_slow)
     C_OVF2 = 8,     // chain overflow list length
     C_ERR2 = 9,     // chain error bits
     C_BUMP_S = 10,  // u64 (words 10-11): chain scratch u64 words used
     C_BUMP_C = 12,  // u64 (words 12-13): cand_ext pairs used
+    C_OVF4 = 14,    // second-level chain list (k_slow_wave -> k_chain_slow)
     C_WORDS = 16
 };
 enum Err : uint32_t {
@@ -81,6 +83,7 @@ struct SketchParams {
     uint64_t hash_ext_cap;
     uint32_t* ctrl;
     uint32_t* ovf1;
+    uint32_t ovf_word;  // the control word counting ovf1 (k_sketch_slow: C_OVF1, or C_OVF3 behind k_slow_wave)
     // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
@@ -122,11 +125,11 @@ struct ChainParams {
     uint64_t cand_ext_cap;     // pairs
     uint64_t* scratch;
     uint64_t scratch_cap;      // u64 words
-    uint64_t* tx_acc;          // per batch: (reads << 40) | score, one atomic per candidate
     uint64_t* tx_reads;
     uint64_t* tx_score;
     uint32_t* ctrl;
     uint32_t* ovf2;
+    uint32_t ovf_word;         // the control word counting ovf2 (k_chain_slow: C_OVF2, or C_OVF4)
     uint32_t* lofs;            // k_probe or fused k_sketch -> k_count: list offset per probe,
                                // [(i*lcap + j)*n + r], ~0u = miss
     uint8_t* pflag;            // -> k_count: 1 = read goes to the slow chain path
@@ -178,16 +181,20 @@ int tables_from_csr(uint32_t ntables, const uint32_t* ks, std::vector<uint32_t>*
 
 // launchers (skq_kernels.hip)
 int launch_sketch(const SketchParams& p, void* stream);
-int launch_sketch_slow(const SketchParams& p, void* stream);
+// (grid: workgroups walking the list; the list length is on the device)
+int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid = 2048);
 // fused sketch + chain (k_map1: quant mode, one k slot, wide tables, hcap 16 or 32; -4 otherwise)
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
 // fused sketch + chain for 2..4 k slots (k_mapk: wide tables, hcap 16 or 32; -4 otherwise)
 int launch_mapk(const SketchParams& p, const ChainParams& cp, void* stream);
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
-int launch_chain_slow(const ChainParams& p, void* stream);
-int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
-// per-transcript totals of the batch's final candidates into p.tx_acc (k_bin + k_bin_sum)
+int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
+// the wave slow path behind k_map1 / k_mapk (wide or compact tables, <= 4 k slots; -4 otherwise):
+// the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
+int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);
+// per-transcript totals of the batch's final candidates into p.tx_reads / p.tx_score (k_bin +
+// k_bin_sum; atomics, so they commute with the slow paths' direct adds)
 // (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs)
 int launch_bin(const ChainParams& p, int binned, void* stream);
 // whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)

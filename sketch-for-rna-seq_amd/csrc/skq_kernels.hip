@@ -514,7 +514,7 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
     __shared__ uint32_t s_cnt, s_bad;
     __shared__ unsigned long long s_at;
     const uint32_t t = threadIdx.x;
-    const uint32_t cnt = min(p.ctrl[C_OVF1], p.ovf_cap);
+    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
     unsigned long long* bump = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
     const uint64_t* seed = p.rolltab + p.nk * 16;
     for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
@@ -2678,7 +2678,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
     __shared__ uint32_t s_cnt, s_nc;
     __shared__ unsigned long long s_at;
     const uint32_t t = threadIdx.x;
-    const uint32_t cnt = min(p.ctrl[C_OVF2], p.ovf_cap);
+    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
     unsigned long long* bump_s = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_S);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_C);
     for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
@@ -2825,7 +2825,344 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
     }
 }
 
-// per-batch packed totals -> running (reads, score) totals
+// Wave slow path (fused map, wide or compact tables, 1..4 k slots): one 64-lane workgroup per
+// read the map kernel listed (ovf2; the ones with status ST_SLOW1 also need their sketch), so the
+// common slow reads (17-255 retained hashes per k, or 17-256 distinct transcripts) cost a few
+// microseconds in one launch instead of a workgroup-wide sort each. Sketch: the windows in one
+// contiguous run per lane (rebuilt from k bases, then rolled), retained values compacted into LDS,
+// a bitonic sort and de-duplication, written exactly as k_sketch_slow writes them. Chain: one
+// entry gather per retained hash per lane, its transcripts counted per k slot in an LDS table of
+// SW_T slots (tid; 8-bit count per k), the filter of src/sparse_chaining.cpp:76-101, a bitonic
+// sort of (score desc, tid asc) keys, the candidates and totals written as k_chain_slow writes
+// them. Reads beyond these limits go on to the general paths (k_sketch_slow, k_chain_slow) through
+// the second-level lists ovf3 (sketch and chain) and ovf4 (chain).
+constexpr uint32_t SW_NW = 512;  // windows per (read, k)
+constexpr uint32_t SW_H = 255;   // retained hashes per (read, k) (8-bit counts)
+constexpr uint32_t SW_T = 256;   // distinct transcripts per read
+
+// ascending bitonic sort of a[0..n2) in LDS (n2 a power of two), by one wave
+template <typename T>
+__device__ __forceinline__ void wave_lds_sort(T* a, uint32_t n2, uint32_t lane) {
+    for (uint32_t k2 = 2; k2 <= n2; k2 <<= 1)
+        for (uint32_t j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
+            for (uint32_t x = lane; x < n2; x += 64) {
+                const uint32_t y = x ^ j2;
+                if (y > x) {
+                    const T u = a[x], v = a[y];
+                    const bool up = (x & k2) == 0;
+                    if (up ? (u > v) : (u < v)) {
+                        a[x] = v;
+                        a[y] = u;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int NK, bool CMP>
+__global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp, uint32_t* ovf3, uint32_t* ovf4) {
+    __shared__ uint32_t s_h[NK][SW_H + 1];
+    __shared__ uint32_t s_tid[SW_T], s_c[SW_T];
+    __shared__ uint64_t s_key[SW_T];
+    __shared__ uint32_t s_m[NK], s_flag, s_nc;
+    __shared__ unsigned long long s_at;
+    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t cnt = min(cp.ctrl[C_OVF2], cp.ovf_cap);
+    unsigned long long* bump_h = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
+    unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(cp.ctrl + C_BUMP_C);
+    const uint64_t* seed = p.rolltab + p.nk * 16;
+    const uint64_t n = cp.n;
+    for (uint32_t jr = blockIdx.x; jr < cnt; jr += gridDim.x) {
+        const uint32_t r = cp.ovf2[jr];
+        const uint8_t st0 = p.status[r];
+        bool hashed = false;  // (uniform) the read's retained sets are in s_h / s_m
+        uint8_t st = st0 & SKQ_STATUS_MASK;
+        if (st0 & ST_SLOW1) {
+            // ---- sketch (k_sketch_slow's contract)
+            uint64_t start, len;
+            read_extent(p.offs, p.fixed_len, r, start, len);
+            uint32_t mink = p.ks[0];
+#pragma unroll
+            for (int i = 1; i < NK; ++i) mink = min(mink, p.ks[i]);
+            if (len > (uint64_t)SW_NW + mink - 1) {
+                if (lane == 0) {
+                    list_push(p.ctrl, C_OVF3, C_ERR1, ovf3, p.ovf_cap, r, E_OVF1_FULL);
+                    list_push(cp.ctrl, C_OVF4, C_ERR2, ovf4, cp.ovf_cap, r, E_OVF2_FULL);
+                }
+                continue;
+            }
+            const uint8_t* sb = p.reads + start;
+            bool bad = false;
+            for (uint32_t q = lane; q < len; q += 64) {
+                const uint8_t c = sb[q];
+                bad |= !(c == 'A' || c == 'C' || c == 'G' || c == 'T');
+            }
+            bad = __any(bad);
+            st = bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
+            for (uint32_t i = lane; i < p.nk; i += 64) p.hash_cnt[(uint64_t)i * n + r] = 0;
+            bool fits = true;
+            if (st == SKQ_READ_OK) {
+#pragma unroll
+                for (int i = 0; i < NK; ++i) {
+                    const uint32_t k = p.ks[i];
+                    const uint32_t nw = (uint32_t)len - k + 1;
+                    const uint32_t seg = (nw + 63) / 64;  // <= 8
+                    const uint32_t wa = min(nw, lane * seg), wb = min(nw, wa + seg);
+                    uint32_t got[SW_NW / 64];
+                    uint32_t keepb = 0;  // bit u: window wa + u is retained
+                    if (wa < wb) {
+                        const uint64_t* tab = p.rolltab + i * 16;
+                        uint32_t hlo = 0, hhi = 0;
+                        for (uint32_t q = 0; q < k; ++q) roll33(hlo, hhi, seed[(sb[wa + q] >> 1) & 3u]);
+#pragma unroll
+                        for (uint32_t u = 0; u < SW_NW / 64; ++u) {
+                            const uint32_t w = wa + u;
+                            if (w < wb) {
+                                if (u) roll33(hlo, hhi, tab[((sb[w + k - 1] >> 1) & 3u) * 4 + ((sb[w - 1] >> 1) & 3u)]);
+                                got[u] = hlo;
+                                keepb |= (hlo <= p.threshold ? 1u : 0u) << u;  // src/sketch.cpp:33-35
+                            }
+                        }
+                    }
+                    const uint32_t m = __builtin_popcount(keepb);
+                    const uint32_t incl = wave_incl_scan(m, lane);
+                    const uint32_t tot = __shfl(incl, 63, 64);
+                    if (tot > SW_H) {  // uniform: the general path
+                        fits = false;
+                        break;
+                    }
+                    {
+                        uint32_t at = incl - m;
+#pragma unroll
+                        for (uint32_t u = 0; u < SW_NW / 64; ++u)
+                            if ((keepb >> u) & 1u) s_h[i][at++] = got[u];
+                    }
+                    const uint32_t n2 = pow2_at_least(max(tot, 1u));
+                    for (uint32_t x = tot + lane; x < n2; x += 64) s_h[i][x] = EMPTY;
+                    wave_sync();
+                    wave_lds_sort(s_h[i], n2, lane);
+                    // de-duplicate in place: each chunk of 64 read (with its predecessor) before
+                    // any of its compacted values are written
+                    uint32_t u_all = 0, prev = EMPTY;
+                    for (uint32_t x0 = 0; x0 < tot; x0 += 64) {
+                        const uint32_t x = x0 + lane;
+                        const uint32_t v = x < tot ? s_h[i][x] : EMPTY;
+                        // (the shuffle runs on every lane: a lane it reads from must be active)
+                        const uint32_t up = __shfl_up(v, 1, 64);
+                        const uint32_t pv = lane ? up : prev;
+                        const bool keep = x < tot && (x == 0 || v != pv);
+                        prev = __shfl(v, 63, 64);
+                        const uint64_t bm = __ballot(keep);
+                        const uint32_t at = u_all + __builtin_popcountll(bm & ((1ull << lane) - 1ull));
+                        wave_sync();
+                        if (keep) s_h[i][at] = v;
+                        u_all += __builtin_popcountll(bm);
+                        wave_sync();
+                    }
+                    if (lane == 0) s_m[i] = 0;
+                    // out: <= hcap in the padded slots, else a bump-allocated run in hash_ext
+                    uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * n + r;
+                    uint32_t* dst = slot;
+                    uint64_t dstride = n;
+                    if (u_all > p.hcap) {
+                        if (lane == 0) {
+                            const unsigned long long at = atomicAdd(bump_h, (unsigned long long)u_all);
+                            s_at = at + u_all <= p.hash_ext_cap ? at : ~0ull;
+                            if (s_at == ~0ull) atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
+                        }
+                        wave_sync();
+                        if (s_at == ~0ull) continue;  // (error recorded; hash_cnt stays 0)
+                        dst = p.hash_ext + s_at;
+                        dstride = 1;
+                        if (lane == 0) slot[0] = (uint32_t)s_at;
+                    }
+                    for (uint32_t x = lane; x < u_all; x += 64) dst[(uint64_t)x * dstride] = s_h[i][x];
+                    if (lane == 0) {
+                        p.hash_cnt[(uint64_t)i * n + r] = u_all;
+                        s_m[i] = u_all;
+                    }
+                }
+            }
+            if (!fits) {  // hashing starts over in k_sketch_slow (status and hash_cnt rewritten there)
+                if (lane == 0) {
+                    list_push(p.ctrl, C_OVF3, C_ERR1, ovf3, p.ovf_cap, r, E_OVF1_FULL);
+                    list_push(cp.ctrl, C_OVF4, C_ERR2, ovf4, cp.ovf_cap, r, E_OVF2_FULL);
+                }
+                continue;
+            }
+            if (lane == 0) p.status[r] = st;
+            hashed = true;
+        }
+        if (st != SKQ_READ_OK) {
+            if (lane == 0) cp.cand_cnt[r] = 0;
+            continue;
+        }
+        // ---- chain (k_chain_slow's contract)
+        if (!hashed) {  // a read the map kernel sketched: its sets are in the padded slots
+            bool fits = true;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const uint32_t hc = hash_count(cp, r, i);
+                if (hc > SW_H) fits = false;
+                uint64_t hs;
+                const uint32_t* hp = hash_list(cp, r, i, hc, hs);
+                for (uint32_t x = lane; x < hc && x < SW_H; x += 64) s_h[i][x] = hp[x * hs];
+                if (lane == 0) s_m[i] = hc;
+            }
+            if (!fits) {
+                if (lane == 0) list_push(cp.ctrl, C_OVF4, C_ERR2, ovf4, cp.ovf_cap, r, E_OVF2_FULL);
+                continue;
+            }
+        }
+        for (uint32_t x = lane; x < SW_T; x += 64) {
+            s_tid[x] = EMPTY;
+            s_c[x] = 0;
+        }
+        if (lane == 0) s_flag = 0;
+        wave_sync();
+        auto ins = [&](uint32_t tid, uint32_t inc) {
+            uint32_t sl = (tid * 0x9E3779B1u) >> 24;
+            for (uint32_t z = 0; z < SW_T; ++z) {
+                const uint32_t old = atomicCAS(&s_tid[sl], EMPTY, tid);
+                if (old == EMPTY || old == tid) {
+                    atomicAdd(&s_c[sl], inc);
+                    return;
+                }
+                sl = (sl + 1) & (SW_T - 1);
+            }
+            s_flag = 1;  // more than SW_T transcripts
+        };
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            if (!cp.tabs[i].present) continue;
+            const uint32_t m = s_m[i], inc = 1u << (8 * i);
+            const uint32_t* wd = cp.wdir[i];
+            const uint64_t wlen = cp.wdir_len[i];
+            for (uint32_t x = lane; x < m; x += 64) {
+                const uint32_t h = s_h[i][x];
+                uint64_t at;
+                bool ok;
+                if (CMP) {
+                    const uint32_t kh = cmp_key_hash(h, cp.wseed[i]);
+                    at = (uint64_t)cmp_slot(kh, cp.wpil[i][cmp_scale(kh, cp.wnb[i])], wlen) * 8;
+                    ok = true;
+                } else {
+                    ok = h < wlen;
+                    at = ok ? (uint64_t)h * 8 : 0;
+                }
+                const uint4 a = *reinterpret_cast<const uint4*>(wd + at);
+                const uint4 b = *reinterpret_cast<const uint4*>(wd + at + 4);
+                uint32_t nn;
+                if (CMP) nn = ok && a.x == h ? a.y >> 22 : 0u;
+                else nn = ok ? a.x : 0u;
+                constexpr uint32_t TM = CMP ? TID_MASK : 0xFFFFFFFFu;
+                const uint32_t t7[7] = {a.y & TM, a.z & TM, a.w & TM, b.x & TM, b.y & TM, b.z & TM, b.w & TM};
+#pragma unroll
+                for (uint32_t q = 0; q < 7; ++q)
+                    if (q < nn) ins(t7[q], inc);
+                if (nn > 7) {  // the rest of a longer list
+                    const uint32_t lo = CMP ? cmp_long_off(b) : nn & 0x7FFFFFFFu;
+                    const uint32_t L = cp.lists[lo];
+                    for (uint32_t q = 7; q < L; ++q) ins(cp.lists[lo + 1 + q], inc);
+                }
+            }
+        }
+        wave_sync();
+        if (s_flag) {
+            if (lane == 0) list_push(cp.ctrl, C_OVF4, C_ERR2, ovf4, cp.ovf_cap, r, E_OVF2_FULL);
+            continue;
+        }
+        // per-k maxima (src/sparse_chaining.cpp:76-82), then the filter (:84-101) as the fast path
+        uint32_t mx[NK] = {};
+        for (uint32_t x = lane; x < SW_T; x += 64)
+            if (s_tid[x] != EMPTY) {
+#pragma unroll
+                for (int i = 0; i < NK; ++i) mx[i] = max(mx[i], (s_c[x] >> (8 * i)) & 0xFFu);
+            }
+        uint32_t need[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) mx[i] = max(mx[i], (uint32_t)__shfl_xor(mx[i], d, 64));
+            const double thr = cp.fraction * (double)mx[i];
+            uint32_t ti = 0;
+            if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+            need[i] = ti;
+        }
+        if (lane == 0) s_nc = 0;
+        wave_sync();
+        for (uint32_t x0 = 0; x0 < SW_T; x0 += 64) {
+            const uint32_t x = x0 + lane;
+            const uint32_t tid = s_tid[x], c = s_c[x];
+            bool keep = tid != EMPTY;
+            uint32_t score = 0;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const uint32_t ci = (c >> (8 * i)) & 0xFFu;
+                keep &= ci >= need[i];
+                score += ci;
+            }
+            const uint64_t bm = __ballot(keep);
+            const uint32_t at = s_nc + __builtin_popcountll(bm & ((1ull << lane) - 1ull));
+            // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
+            const uint64_t key = ((uint64_t)(0xFFFFFFFFu - score) << 32) | tid;
+            wave_sync();
+            if (keep) s_key[at] = key;
+            if (lane == 0) s_nc += __builtin_popcountll(bm);
+            wave_sync();
+        }
+        const uint32_t nc = s_nc;
+        const uint32_t n2 = pow2_at_least(max(nc, 1u));
+        for (uint32_t x = nc + lane; x < n2; x += 64) s_key[x] = ~0ull;
+        wave_sync();
+        wave_lds_sort(s_key, n2, lane);
+        uint32_t* ct = cp.cand_tid + r;
+        uint32_t* cs = cp.cand_score + r;
+        uint64_t stride = n;
+        if (nc > (uint32_t)CCAP) {
+            if (lane == 0) {
+                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)nc);
+                if (at + nc <= cp.cand_ext_cap) {
+                    s_at = at;
+                    cp.cand_tid[r] = (uint32_t)at;
+                } else {
+                    atomicOr(&cp.ctrl[C_ERR2], (uint32_t)E_CAND_EXT);
+                    s_at = ~0ull;
+                }
+            }
+            wave_sync();
+            if (s_at == ~0ull) {
+                if (lane == 0) cp.cand_cnt[r] = 0;
+                continue;
+            }
+            ct = cp.cand_ext + 2 * s_at;
+            cs = ct + 1;
+            stride = 2;
+        }
+        for (uint32_t a = lane; a < nc; a += 64) {
+            const uint32_t tid = (uint32_t)s_key[a];
+            const uint32_t score = 0xFFFFFFFFu - (uint32_t)(s_key[a] >> 32);
+            ct[a * stride] = tid;
+            cs[a * stride] = score;
+            if (cp.accumulate && cp.slow_totals) {  // the map kernel binned the fast reads' totals
+                atomicAdd(reinterpret_cast<unsigned long long*>(&cp.tx_reads[tid]), 1ull);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&cp.tx_score[tid]), (unsigned long long)score);
+            }
+        }
+        if (lane == 0) cp.cand_cnt[r] = nc;
+    }
+}
+
 // Per-transcript totals without one scattered atomic per candidate (those run at the fabric's
 // random-request rate). Pass 1, one workgroup per 256 reads: the workgroup's candidates are
 // grouped by transcript bucket (2^bits ids) with LDS counters and a scan and written, packed as
@@ -2833,7 +3170,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
 // where bucket b starts in region w (b = nb: the region's total). Candidates that do not pack
 // (overflow lists, huge scores) are added directly. Pass 2, one workgroup per (chunk of
 // regions, bucket): an LDS histogram of the bucket, flushed with one coalesced atomic per
-// non-empty bin into tx_acc ((reads << 40) | score).
+// non-empty bin into the running totals (two atomics: reads, score).
 __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW, uint32_t* hdr,
                                            uint32_t* region) {
     __shared__ uint32_t s_cnt[WG + 1], s_fill[WG + 1];
@@ -2925,7 +3262,8 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
     for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
-__global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nb, uint32_t nW,
+__global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_reads, uint64_t* tx_score, uint32_t ntx, uint32_t bits,
+                                               uint32_t nb, uint32_t nW,
                                                uint32_t chunk, const uint32_t* hdr, const uint32_t* region) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
@@ -2967,20 +3305,14 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
     for (uint32_t i = t; i < bs; i += WG) {
         const unsigned long long a = s_bins[i];
         const uint32_t tx = b * bs + i;
-        if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
-    }
-}
-
-__global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx) {
-    for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < ntx; t += gridDim.x * WG) {
-        const uint64_t a = acc[t];
-        if (a) {
-            reads[t] += a >> 40;
-            score[t] += a & ((1ull << 40) - 1);
-            acc[t] = 0;
+        // (a bin packs (reads << 40) | score: a batch holds < 2^24 reads of score <= 2^10)
+        if (a && tx < ntx) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&tx_reads[tx]), a >> 40);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&tx_score[tx]), a & ((1ull << 40) - 1));
         }
     }
 }
+
 
 // ---------------------------------------------------------------------------------------------
 // launchers
@@ -3013,9 +3345,9 @@ int launch_sketch(const SketchParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_sketch_slow(const SketchParams& p, void* stream) {
+int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_sketch_slow, dim3(2048), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_sketch_slow, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -3078,9 +3410,38 @@ int launch_count(const ChainParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_chain_slow(const ChainParams& p, void* stream) {
+int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream) {
+    if (cp.n == 0) return 0;
+    if (cp.wide != 1 && cp.wide != 3) return -4;
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // a 64-lane workgroup per listed read, grid-stride (the list length is on the device)
+    const dim3 grid(2048), blk(64);
+    const bool cmp = cp.wide == 3;
+    switch (cp.nk) {
+    case 1:
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<1, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<1, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        break;
+    case 2:
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<2, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<2, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        break;
+    case 3:
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<3, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<3, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        break;
+    case 4:
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<4, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<4, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        break;
+    default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_chain_slow, dim3(2048), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(k_chain_slow, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -3202,17 +3563,10 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     if (lds > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-    hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits, nb,
+    hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_reads, p.tx_score, p.ntx, bits, nb,
                        nW, chunk, hdr, region);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream) {
-    if (ntx == 0) return 0;
-    const unsigned grid = (unsigned)std::min<uint32_t>((ntx + WG - 1) / WG, 1024);
-    hipLaunchKernelGGL(k_fold_totals, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), acc, reads,
-                       score, ntx);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
 
 }  // namespace skq

@@ -262,6 +262,45 @@ def test_wide_postings_take_slow_chain_path():
         assert ref["cand_cnt"].max() > 16 or fraction != 0.0
 
 
+def test_slow_reads_past_the_wave_path():
+    """Reads the map kernel lists go to the wave slow path (k_slow_wave) first; those past its
+    limits go on to the general paths: > 255 retained hashes per k (fraction 0.9, 300 bp), > 256
+    distinct transcripts (fraction 0.3 with every hash mapping to 40 transcripts), > 512 windows
+    (600 bp). Mixed with ordinary slow reads in one batch."""
+    rng = np.random.default_rng(11)
+    ntx = 3000
+    tx = synth.transcriptome(24, seed=12)
+    seqs = [tx.seq(t) for t in range(tx.ntx)]
+    thr = orc.threshold(0.3)
+    h, t = [], []
+    for tid, s in enumerate(seqs):
+        for x in orc.sketch(s, 31, thr=orc.threshold(0.95)):
+            h.append(x)
+            t.append(tid)
+            if rng.random() < 0.5:
+                for extra in rng.choice(np.arange(24, ntx), 40, replace=False):
+                    h.append(x)
+                    t.append(int(extra))
+    pairs = [(np.array(h, np.uint32), np.array(t, np.uint32))]
+    gi, oi = build([31], pairs=pairs, ntx=ntx)
+    long = [s for s in seqs if len(s) >= 700]
+    assert long
+    reads = []
+    for i in range(300):
+        s = seqs[i % len(seqs)]
+        L = min(len(s), (150, 150, 300, 600)[i % 4])
+        p = int(rng.integers(0, len(s) - L + 1))
+        reads.append(s[p:p + L])
+    for th, fraction in ((thr, 0.9), (thr, 0.0), (orc.threshold(0.9), 0.0)):
+        out = run_gpu(gi, reads, thr=th, fraction=fraction)
+        ref = oi.map_batch(reads, thr=th, fraction=fraction)
+        compare(out, ref, len(reads), 1)
+        assert fraction > 0 or int(ref["cand_cnt"].max()) > 256
+        tr, ts = totals_from(ref, len(reads), ntx)
+        np.testing.assert_array_equal(out["totals"][0], tr)
+        np.testing.assert_array_equal(out["totals"][1], ts)
+
+
 def test_list_lengths_around_the_inline_limit():
     # hand-built index whose lists hold 1..12 transcripts: wide entries keep 7 inline and read
     # the rest from the postings list; each read stays within 16 distinct transcripts (the
