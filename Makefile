@@ -36,8 +36,10 @@ $(OUT)/libskq.so: $(LIB_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(LIB_OBJS)
 
 # the command line (index / quant), src/main.cpp's interface
+# (several GPUs: HIP streams and RCCL from the host program; the HIP headers want the platform named)
 $(OUT)/skq: $(CSRC)/skq_cli.cpp $(OUT)/libskq.so include/skq.h include/skq_host.h
-	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude $< -o $@ -L$(OUT) -lskq -Wl,-rpath,'$$ORIGIN'
+	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ $< -o $@ -L$(OUT) -lskq \
+	    -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ROCM)/lib
 
 # test driver for the C++ drop-in signatures (tests/test_dropin.py)
 $(OUT)/skq_dropin_check: tests/dropin_check.cpp $(OUT)/libskq.so $(wildcard include/dropin/*.h)

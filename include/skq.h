@@ -168,6 +168,11 @@ int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, i
  * skipped) and the batch goes through skq_map. Records are numbered in file order from 0. */
 typedef struct skq_ingest skq_ingest;
 int skq_ingest_open(skq_session* s, const char* path, uint64_t chunk_bytes, int io_threads, skq_ingest** out);
+/* The records whose header line starts in [lo, hi) of the file (line starts, e.g. from
+ * skq_fastq_split), the reader's state at lo given: one part of a file mapped on several devices.
+ * Records are numbered from 0 within the part. */
+int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_t hi, uint32_t entry_state,
+                          uint64_t chunk_bytes, int io_threads, skq_ingest** out);
 /* The next batch (at most the session's max_reads records): parse if needed, sketch + chain on
  * `stream`. Results are the session's, as after skq_map; *n = records in the batch (0 at the end
  * of the file), numbered from *first. Every record is in the batch: status marks the reads the
@@ -178,6 +183,10 @@ uint64_t skq_ingest_records(const skq_ingest* g);
 /* After the last batch: kept[r] = 1 for the record that the reference keeps for its id, the last
  * one with status SKQ_READ_OK (src/main.cpp:147); kept holds skq_ingest_records() bytes. */
 int skq_ingest_finish(skq_ingest* g, uint8_t* kept);
+/* The parts of one file, in file order, each finished with its own kept array: clears
+ * kept[p][r] where a later part keeps a record of the same id, so that across the parts only the
+ * last valid record of every id stays (src/main.cpp:147). */
+int skq_ingest_supersede(skq_ingest* const* parts, uint32_t nparts, uint8_t* const* kept);
 /* id of a record (the header line after '@'), pointing into the mapped file */
 int skq_ingest_id(const skq_ingest* g, uint64_t ordinal, const char** id, uint64_t* len);
 int skq_ingest_close(skq_ingest* g);

@@ -85,6 +85,12 @@ int skq_fastq_kept(const skq_fastq* q, uint64_t ordinal);
 uint64_t skq_fastq_records(const skq_fastq* q);
 int skq_fastq_id(const skq_fastq* q, uint64_t ordinal, const char** id, uint64_t* len);
 int skq_fastq_close(skq_fastq* q);
+/* Split a FASTQ file into `parts` byte ranges for several devices (skq_ingest_open_range):
+ * offs[0] = 0, offs[parts] = file size, the rest at line starts near equal shares; states[p] is
+ * the reader's record-machine state (0 between records, 1-3 inside one, src/main.cpp:119-129)
+ * at offs[p], exact: worked out from the lines before the split point, going back until every
+ * possible earlier state has converged (a few lines in any FASTQ; the whole prefix at worst). */
+int skq_fastq_split(const char* path, uint32_t parts, uint64_t* offs, uint32_t* states);
 
 /* ---- the legacy binary index (save_index / load_index, src/data_io.cpp:165-304) ------------ */
 typedef struct skq_legacy_index skq_legacy_index;

@@ -7,7 +7,14 @@
 // quant: legacy file -> device index; FASTQ streamed to the GPU, parsed there and mapped in
 //        batches (skq_ingest: sketch + sparse chain); the last valid record of every read id
 //        kept; EM (20 rounds, 0.01) and assignment on the GPU -> CSV. As in the reference, quant uses the index's k list.
+//        Several GPUs (SKQ_DEVICES=0,1,...): the file is split into one part per device at line
+//        starts (skq_fastq_split), each device holds the index and maps its part on a host thread
+//        of its own, duplicate ids are settled across the parts (skq_ingest_supersede), and every
+//        EM round is the devices' E-steps, one RCCL all-reduce of the posterior sums over xGMI,
+//        and the same M-step on every device (src/main.cpp:165-197, src/isoform_assignment.cpp).
 #include <getopt.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -17,6 +24,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "skq.h"
@@ -41,8 +49,9 @@ void print_help(const std::string& prog) {
               << "  " << prog << " -o index <reference_genome.fasta> <index_output>\n\n"
               << "Quant mode usage:\n"
               << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
-              << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_BATCH (reads per batch),\n"
-              << "             SKQ_CHUNK_MB (FASTQ MiB per device chunk, default 64).\n";
+              << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_DEVICES (GPU list for quant,\n"
+              << "             e.g. 0,1,2,3 or all), SKQ_BATCH (reads per batch), SKQ_CHUNK_MB (FASTQ MiB\n"
+              << "             per device chunk, default 64).\n";
 }
 
 const float kSketchSize = 0.05f;  // src/main.cpp:43
@@ -51,6 +60,127 @@ int device() {
     const char* e = std::getenv("SKQ_DEVICE");
     return e ? std::atoi(e) : 0;
 }
+
+// quant's devices: SKQ_DEVICES (a list, or "all"), else SKQ_DEVICE
+std::vector<int> devices() {
+    const char* e = std::getenv("SKQ_DEVICES");
+    if (!e || !*e) return {device()};
+    std::vector<int> d;
+    if (std::string(e) == "all") {
+        for (int i = 0; i < skq_device_count(); ++i) d.push_back(i);
+    } else {
+        std::istringstream iss(e);
+        std::string tok;
+        while (std::getline(iss, tok, ','))
+            if (!tok.empty()) d.push_back(std::stoi(tok));
+    }
+    if (d.empty()) throw std::runtime_error("SKQ_DEVICES names no device");
+    return d;
+}
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// One device's share of quant: its copy of the index, a session, the GPU ingest of its part of
+// the FASTQ file, and the candidate lists kept on the device for the EM.
+struct Part {
+    int dev = 0;
+    uint64_t lo = 0, hi = 0;
+    uint32_t state = 0;
+    skq_index* ix = nullptr;
+    skq_session* s = nullptr;
+    skq_ingest* q = nullptr;
+    skq_em_set* em = nullptr;
+    std::vector<uint8_t> kept;
+    hipStream_t st = nullptr;
+    double *d_pi = nullptr, *d_post = nullptr;
+    uint8_t* d_assigned = nullptr;
+    std::string err;
+
+    void map(const std::string& reads_path, uint32_t ntx, uint32_t nk, const uint32_t* ks, const skq_tables* tabs) {
+        check(skq_index_from_tables(dev, ntx, nk, ks, tabs, &ix), "device index");
+        uint64_t batch = 1u << 21;  // reads per batch (2M and 64-MiB chunks: tools/ingest_bench.py sweep)
+        if (const char* e = std::getenv("SKQ_BATCH")) batch = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+        check(skq_session_create(ix, batch, 256, &s), "session");
+        uint64_t chunk = 0;
+        if (const char* e = std::getenv("SKQ_CHUNK_MB")) chunk = std::strtoull(e, nullptr, 10) << 20;
+        check(skq_ingest_open_range(s, reads_path.c_str(), lo, hi, state, chunk, 8, &q), "FASTQ");
+        // every record's candidates stay on the device, appended batch by batch to the EM set
+        check(skq_em_create(dev, ntx, &em), "EM");
+        const uint32_t thr = skq_threshold((double)kSketchSize);
+        for (;;) {
+            uint64_t n = 0, first = 0;
+            check(skq_ingest_map(q, thr, 0.9, 0, nullptr, &n, &first), "sketch + sparse chain");
+            if (n == 0) break;
+            check(skq_em_add_session(em, s, nullptr), "EM reads");
+        }
+        kept.resize(skq_ingest_records(q));
+        check(skq_ingest_finish(q, kept.data()), "duplicate reads");
+    }
+
+    ~Part() {
+        if (d_pi) skq_free(d_pi);
+        if (d_post) skq_free(d_post);
+        if (d_assigned) skq_free(d_assigned);
+        if (st) (void)hipStreamDestroy(st);
+        skq_em_free(em);
+        skq_ingest_close(q);
+        skq_session_free(s);
+        skq_index_free(ix);
+    }
+};
+
+// Sum (or max) of one device array over the parts, left in every part's copy: RCCL over xGMI
+// when the devices are distinct; a host-staged sum in part order when a device repeats (several
+// parts sharing one GPU, as the tests run them).
+struct Reducer {
+    std::vector<Part*> parts;
+    std::vector<ncclComm_t> comms;
+    bool host = false;
+
+    explicit Reducer(std::vector<Part*> ps) : parts(std::move(ps)) {
+        std::vector<int> devs;
+        for (Part* p : parts) devs.push_back(p->dev);
+        std::vector<int> u = devs;
+        std::sort(u.begin(), u.end());
+        host = std::unique(u.begin(), u.end()) != u.end();
+        if (!host) {
+            comms.resize(parts.size());
+            if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess)
+                throw std::runtime_error("RCCL communicator setup failed");
+        }
+    }
+    ~Reducer() {
+        for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
+    }
+    template <typename T>
+    void all(T* (Part::*field), size_t count, ncclDataType_t type, ncclRedOp_t op) {
+        if (!host) {
+            if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("RCCL group");
+            for (size_t d = 0; d < parts.size(); ++d) {
+                T* p = parts[d]->*field;
+                if (ncclAllReduce(p, p, count, type, op, comms[d], parts[d]->st) != ncclSuccess)
+                    throw std::runtime_error("RCCL all-reduce failed");
+            }
+            if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL group");
+            return;
+        }
+        std::vector<T> acc(count), h(count);
+        for (size_t d = 0; d < parts.size(); ++d) {
+            hip_check(hipSetDevice(parts[d]->dev), "device");
+            hip_check(hipMemcpyAsync(h.data(), parts[d]->*field, count * sizeof(T), hipMemcpyDeviceToHost, parts[d]->st),
+                      "reduce copy");
+            hip_check(hipStreamSynchronize(parts[d]->st), "reduce copy");
+            for (size_t i = 0; i < count; ++i) acc[i] = d == 0 ? h[i] : (op == ncclSum ? acc[i] + h[i] : std::max(acc[i], h[i]));
+        }
+        for (Part* p : parts) {
+            hip_check(hipSetDevice(p->dev), "device");
+            hip_check(hipMemcpyAsync(p->*field, acc.data(), count * sizeof(T), hipMemcpyHostToDevice, p->st), "reduce copy");
+            hip_check(hipStreamSynchronize(p->st), "reduce copy");
+        }
+    }
+};
 
 void build_and_save_index(const std::string& fasta, const std::string& out, const std::vector<uint32_t>& ks) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -91,49 +221,99 @@ void quantification(const std::string& index_path, const std::string& reads_path
     check(skq_legacy_index_view(lx, &nk, &ks, &tx, &tabs), "index view");
     if (nk == 0) throw std::runtime_error("the index holds no k-mer lengths");
     const uint32_t ntx = (uint32_t)skq_seqs_count(tx);
-    skq_index* ix = nullptr;
-    check(skq_index_from_tables(device(), ntx, nk, ks, tabs, &ix), "device index");
 
-    uint64_t batch = 1u << 21;  // reads per batch (2M and 64-MiB chunks: tools/ingest_bench.py sweep)
-    if (const char* e = std::getenv("SKQ_BATCH")) batch = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
-    skq_session* s = nullptr;
-    check(skq_session_create(ix, batch, 256, &s), "session");
-    // FASTQ parsed on the GPU: the reader thread streams the file to HBM (skq_ingest)
-    skq_ingest* q = nullptr;
-    uint64_t chunk = 0;
-    if (const char* e = std::getenv("SKQ_CHUNK_MB")) chunk = std::strtoull(e, nullptr, 10) << 20;
-    check(skq_ingest_open(s, reads_path.c_str(), chunk, 8, &q), "FASTQ");
-
-    // every record's candidates stay on the device, appended batch by batch to the EM set
-    skq_em_set* em = nullptr;
-    check(skq_em_create(device(), ntx, &em), "EM");
-    const uint32_t thr = skq_threshold((double)kSketchSize);
-    for (;;) {
-        uint64_t n = 0, first = 0;
-        check(skq_ingest_map(q, thr, 0.9, 0, nullptr, &n, &first), "sketch + sparse chain");
-        if (n == 0) break;
-        check(skq_em_add_session(em, s, nullptr), "EM reads");
+    // one part of the file per device, mapped on a host thread each
+    const std::vector<int> devs = devices();
+    const uint32_t D = (uint32_t)devs.size();
+    std::vector<uint64_t> offs(D + 1);
+    std::vector<uint32_t> states(D);
+    check(skq_fastq_split(reads_path.c_str(), D, offs.data(), states.data()), "FASTQ split");
+    std::vector<Part> parts(D);
+    for (uint32_t d = 0; d < D; ++d) {
+        parts[d].dev = devs[d];
+        parts[d].lo = offs[d];
+        parts[d].hi = offs[d + 1];
+        parts[d].state = states[d];
     }
-    std::vector<uint8_t> kept(skq_ingest_records(q));
-    check(skq_ingest_finish(q, kept.data()), "duplicate reads");
+    {
+        std::vector<std::thread> ts;
+        for (Part& p : parts)
+            ts.emplace_back([&p, &reads_path, ntx, nk, ks, tabs] {
+                try {
+                    hip_check(hipSetDevice(p.dev), "device");
+                    p.map(reads_path, ntx, nk, ks, tabs);
+                } catch (const std::exception& e) {
+                    p.err = e.what();
+                }
+            });
+        for (auto& t : ts) t.join();
+    }
+    for (Part& p : parts)
+        if (!p.err.empty()) throw std::runtime_error(p.err);
+    std::vector<skq_ingest*> qs;
+    std::vector<uint8_t*> kp;
+    for (Part& p : parts) {
+        qs.push_back(p.q);
+        kp.push_back(p.kept.data());
+    }
+    check(skq_ingest_supersede(qs.data(), D, kp.data()), "duplicate reads");  // (one part: no-op)
     std::cout << "Loading read completed" << std::endl;
     std::cout << "Sparse chaining completed" << std::endl;
 
     // the reads sparse_chain saw: status OK, and the last such record of their id
-    check(skq_em_select(em, kept.data()), "EM reads");
+    uint64_t R = 0;
+    for (Part& p : parts) {
+        check(skq_em_select(p.em, p.kept.data()), "EM reads");
+        R += skq_em_reads(p.em);
+    }
     std::vector<double> pi(ntx), counts(ntx);
     std::vector<uint8_t> assigned(ntx);
-    int iters = 0;
-    check(skq_em_run(em, 20, 0.01, pi.data(), &iters), "EM");
-    std::cout << "EM estimation completed" << std::endl;
-    check(skq_em_assign_host(em, nullptr, counts.data(), assigned.data()), "assign");
+    if (D == 1) {
+        Part& p = parts[0];
+        int iters = 0;
+        check(skq_em_run(p.em, 20, 0.01, pi.data(), &iters), "EM");
+        std::cout << "EM estimation completed" << std::endl;
+        check(skq_em_assign_host(p.em, nullptr, counts.data(), assigned.data()), "assign");
+    } else {
+        // sharded rounds (src/isoform_assignment.cpp:9-70): every device's E-step over its reads,
+        // the posterior sums all-reduced, the same M-step (and convergence test) on every device
+        std::vector<Part*> pp;
+        for (Part& p : parts) {
+            hip_check(hipSetDevice(p.dev), "device");
+            hip_check(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking), "stream");
+            check(skq_malloc(p.dev, ntx * 8ull, reinterpret_cast<void**>(&p.d_pi)), "EM buffers");
+            check(skq_malloc(p.dev, ntx * 8ull, reinterpret_cast<void**>(&p.d_post)), "EM buffers");
+            check(skq_malloc(p.dev, ntx, reinterpret_cast<void**>(&p.d_assigned)), "EM buffers");
+            check(skq_em_init(p.em, p.d_pi, p.st), "EM");
+            pp.push_back(&p);
+        }
+        Reducer red(pp);
+        int it = 0;
+        for (; it < 20; ++it) {
+            for (Part& p : parts) check(skq_em_estep(p.em, p.d_pi, p.d_post, p.st), "EM");
+            red.all(&Part::d_post, ntx, ncclDouble, ncclSum);
+            double change = 0.0;
+            for (Part& p : parts) check(skq_em_mstep(p.em, p.d_pi, p.d_post, R, &change, p.st), "EM");
+            if (change < 0.01) {  // (:62-64; the same value on every device)
+                ++it;
+                break;
+            }
+        }
+        std::cout << "EM estimation completed" << std::endl;
+        // assignment: counts summed over the devices, assigned flags or-ed (max)
+        for (Part& p : parts) check(skq_em_assign(p.em, p.d_pi, p.d_post, p.d_assigned, p.st), "assign");
+        red.all(&Part::d_post, ntx, ncclDouble, ncclSum);
+        red.all(&Part::d_assigned, ntx, ncclUint8, ncclMax);
+        for (Part& p : parts) check(skq_stream_sync(p.st), "assign");
+        hip_check(hipSetDevice(parts[0].dev), "device");
+        check(skq_memcpy_d2h(pi.data(), parts[0].d_pi, ntx * 8ull, parts[0].st), "assign");
+        check(skq_memcpy_d2h(counts.data(), parts[0].d_post, ntx * 8ull, parts[0].st), "assign");
+        check(skq_memcpy_d2h(assigned.data(), parts[0].d_assigned, ntx, parts[0].st), "assign");
+    }
     std::cout << "Read assignment completed" << std::endl;
     check(skq_csv_write(out_path.c_str(), tx, counts.data(), assigned.data(), pi.data()), "output_to_csv");
     std::cout << "Output written to " << out_path << std::endl;
-    skq_em_free(em);
-    skq_ingest_close(q);
-    skq_session_free(s);
-    skq_index_free(ix);
+    parts.clear();
     skq_legacy_index_free(lx);
 }
 

@@ -318,6 +318,7 @@ struct skq_ingest {
     uint64_t max_reads = 0;
     int fd = -1;
     uint64_t fsize = 0;
+    uint64_t lo = 0, hi = 0;     // this ingest's records: those whose header line starts in [lo, hi)
     const char* map = nullptr;   // the file, mapped for duplicate-id comparisons
     uint64_t chunk = 0;
     int io_threads = 1;
@@ -390,13 +391,13 @@ uint64_t find_nl(const uint8_t* h, uint64_t from, uint64_t to) {
     return q ? (uint64_t)(static_cast<const uint8_t*>(q) - h) : to;
 }
 
-// Reader thread: chunk = whole lines from `off` (at least `chunk` bytes unless the file ends)
-// plus the line after them (the halo).
+// Reader thread: chunk = whole lines from `off` (at least `chunk` bytes unless the range ends)
+// plus the line after them (the halo, which may lie past the range).
 void reader_main(skq_ingest* g) {
     (void)hipSetDevice(g->device);
-    uint64_t off = 0;
+    uint64_t off = g->lo;
     std::string err;
-    for (uint64_t c = 0; off < g->fsize; ++c) {
+    for (uint64_t c = 0; off < g->hi; ++c) {
         Slot& sl = g->slot[c & 1];
         {
             std::unique_lock<std::mutex> lk(g->mu);
@@ -408,7 +409,8 @@ void reader_main(skq_ingest* g) {
             sl.consumed_pending = false;
         }
         // read until the own region ends at a newline (or EOF) and the halo line is complete
-        uint64_t have = 0, want = std::min<uint64_t>(g->fsize - off, g->chunk + (1u << 16));
+        const uint64_t lim = g->hi - off;  // bytes of the range left (hi is a line start or EOF)
+        uint64_t have = 0, want = std::min<uint64_t>(g->fsize - off, std::min(lim, g->chunk) + (1u << 16));
         uint64_t own = 0, len = 0;
         for (;;) {
             if (want > sl.host_cap) {
@@ -428,9 +430,21 @@ void reader_main(skq_ingest* g) {
                 have = want;
             }
             const bool at_eof = off + have == g->fsize;
-            if (g->fsize - off <= g->chunk) {
-                own = len = g->fsize - off;  // the rest of the file
-                break;
+            if (lim <= g->chunk) {  // the rest of the range, then the line after it
+                own = lim;
+                if (off + own == g->fsize) {
+                    len = own;
+                    break;
+                }
+                if (have > own) {
+                    const uint64_t h = find_nl(sl.host, own, have);
+                    if (h < have || at_eof) {
+                        len = h < have ? h + 1 : have;
+                        break;
+                    }
+                }
+                want = std::min<uint64_t>(g->fsize - off, std::max<uint64_t>(have * 2, own + (1u << 16)));
+                continue;
             }
             const uint64_t e = find_nl(sl.host, g->chunk - 1, have);
             if (e < have) {
@@ -564,7 +578,13 @@ int parse_chunk(skq_ingest* g, int c, hipStream_t st) {
 extern "C" {
 
 int skq_ingest_open(skq_session* s, const char* path, uint64_t chunk_bytes, int io_threads, skq_ingest** out) {
+    return skq_ingest_open_range(s, path, 0, ~0ull, 0, chunk_bytes, io_threads, out);
+}
+
+int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_t hi, uint32_t entry_state,
+                          uint64_t chunk_bytes, int io_threads, skq_ingest** out) {
     if (!s || !path || !out) return ifail(-1, "null argument");
+    if (entry_state > 3) return ifail(-1, "record-machine state must be 0..3");
     *out = nullptr;
     auto* g = new skq_ingest();
     g->s = s;
@@ -591,6 +611,12 @@ int skq_ingest_open(skq_session* s, const char* path, uint64_t chunk_bytes, int 
         }
         g->map = static_cast<const char*>(m);
     }
+    g->hi = std::min(hi, g->fsize);
+    g->lo = std::min(lo, g->hi);
+    if ((g->lo > 0 && g->map[g->lo - 1] != '\n') || (g->hi < g->fsize && g->map[g->hi - 1] != '\n')) {
+        skq_ingest_close(g);
+        return ifail(-1, "range bounds must be line starts (skq_fastq_split)");
+    }
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
@@ -598,7 +624,8 @@ int skq_ingest_open(skq_session* s, const char* path, uint64_t chunk_bytes, int 
     if (hipStreamCreateWithFlags(&g->copy, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->h_scal), 16, hipHostMallocDefault) != hipSuccess ||
         g->state.reserve(2) != hipSuccess || g->scal.reserve(2) != hipSuccess ||
-        hipMemset(g->state.p, 0, 8) != hipSuccess)
+        hipMemset(g->state.p, 0, 8) != hipSuccess ||
+        hipMemcpy(g->state.p, &entry_state, 4, hipMemcpyHostToDevice) != hipSuccess)
         rc = ifail(-3, "ingest setup failed");
     for (auto& sl : g->slot)
         if (!rc && (hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming) != hipSuccess ||
@@ -737,6 +764,67 @@ int skq_ingest_id(const skq_ingest* g, uint64_t ordinal, const char** id, uint64
     if (!ok) return ifail(-3, "id lookup failed");
     if (id) *id = g->map + pos;
     if (len) *len = l;
+    return 0;
+}
+
+int skq_ingest_supersede(skq_ingest* const* gs, uint32_t nparts, uint8_t* const* kept) {
+    if ((!gs || !kept) && nparts) return ifail(-1, "null argument");
+    // every range's kept records (id hash, range, ordinal), grouped by the hash's top bits so that
+    // threads can each sort and scan one group
+    struct E {
+        uint64_t h;
+        uint32_t d;
+        uint64_t r;
+        bool operator<(const E& o) const { return h != o.h ? h < o.h : d < o.d; }
+    };
+    constexpr int TB = 16;
+    std::vector<std::vector<E>> bk(TB);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    for (uint32_t d = 0; d < nparts; ++d) {
+        const skq_ingest* g = gs[d];
+        if (!g || !kept[d]) return ifail(-1, "null part");
+        if (!g->finished) return ifail(-1, "call skq_ingest_finish on every part first");
+        std::vector<uint64_t> h(g->records);
+        (void)hipSetDevice(g->device);
+        const bool ok = !g->records ||
+                        hipMemcpy(h.data(), g->id_hash.p, g->records * 8, hipMemcpyDeviceToHost) == hipSuccess;
+        (void)hipSetDevice(prev);
+        if (!ok) return ifail(-3, "id hash copy failed");
+        for (uint64_t r = 0; r < g->records; ++r)
+            if (kept[d][r]) bk[h[r] >> 60].push_back({h[r], d, r});
+    }
+    std::vector<int> rcs(TB, 0);
+    std::vector<std::thread> ts;
+    for (int b = 0; b < TB; ++b)
+        ts.emplace_back([&, b] {
+            auto& v = bk[b];
+            std::sort(v.begin(), v.end());
+            for (size_t i = 0; i < v.size();) {
+                size_t j = i + 1;
+                while (j < v.size() && v[j].h == v[i].h) ++j;
+                if (v[j - 1].d != v[i].d) {  // one hash kept in several ranges: compare the ids
+                    std::unordered_map<std::string_view, size_t> last;  // id -> its entry in the latest range
+                    std::vector<std::string_view> ids(j - i);
+                    for (size_t q = i; q < j; ++q) {
+                        const char* id = nullptr;
+                        uint64_t len = 0;
+                        if (skq_ingest_id(gs[v[q].d], v[q].r, &id, &len)) {
+                            rcs[b] = -3;
+                            return;
+                        }
+                        ids[q - i] = std::string_view(id, len);
+                        last[ids[q - i]] = q;  // (ranges ascending within the group)
+                    }
+                    for (size_t q = i; q < j; ++q)
+                        if (last[ids[q - i]] != q) kept[v[q].d][v[q].r] = 0;
+                }
+                i = j;
+            }
+        });
+    for (auto& t : ts) t.join();
+    for (int rc : rcs)
+        if (rc) return ifail(rc, "id lookup failed");
     return 0;
 }
 

@@ -153,6 +153,72 @@ struct skq_fastq {
 
 extern "C" {
 
+// the record machine over the lines of t[a, b) (a and b line starts) from state s
+// (src/main.cpp:119-129: between records a line starting with '@' opens one, any other line is
+// skipped; the sequence, '+' and quality lines are taken whatever they hold)
+static uint32_t fastq_run(const char* t, uint64_t a, uint64_t b, uint32_t s) {
+    while (a < b) {
+        s = s == 0 ? (t[a] == '@' ? 1u : 0u) : (s + 1) & 3u;
+        const void* nl = std::memchr(t + a, '\n', (size_t)(b - a));
+        a = nl ? (uint64_t)(static_cast<const char*>(nl) - t) + 1 : b;
+    }
+    return s;
+}
+
+int skq_fastq_split(const char* path, uint32_t parts, uint64_t* offs, uint32_t* states) {
+    if (!path || !offs || !states || parts == 0) return skq::set_error(-1, "null argument or no parts");
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return skq::set_error(-2, (std::string("Could not open FASTQ file: ") + path).c_str());
+    struct stat st {};
+    if (fstat(fd, &st) != 0) {
+        ::close(fd);
+        return skq::set_error(-2, "Could not stat FASTQ file");
+    }
+    const uint64_t n = (uint64_t)st.st_size;
+    const char* t = nullptr;
+    if (n) {
+        void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) {
+            ::close(fd);
+            return skq::set_error(-2, "FASTQ mmap failed");
+        }
+        t = static_cast<const char*>(m);
+    }
+    auto line_start_at_or_after = [&](uint64_t x) -> uint64_t {
+        if (x == 0 || x >= n) return std::min(x, n);
+        const void* nl = std::memchr(t + x - 1, '\n', (size_t)(n - x + 1));
+        return nl ? (uint64_t)(static_cast<const char*>(nl) - t) + 1 : n;
+    };
+    offs[0] = 0;
+    states[0] = 0;
+    for (uint32_t p = 1; p < parts; ++p) {
+        uint64_t b = line_start_at_or_after(n / parts * p);
+        b = std::max(b, offs[p - 1]);
+        offs[p] = b;
+        // the state at b: from a line start W bytes back, all four states run forward; when they
+        // agree at b that is the state whatever it was there; else go back further (from the file
+        // start the state is exactly 0)
+        uint32_t s = 0;
+        for (uint64_t W = 1 << 12;; W <<= 2) {
+            if (W >= b) {
+                s = fastq_run(t, 0, b, 0);
+                break;
+            }
+            const uint64_t a = line_start_at_or_after(b - W);
+            const uint32_t s0 = fastq_run(t, a, b, 0);
+            if (fastq_run(t, a, b, 1) == s0 && fastq_run(t, a, b, 2) == s0 && fastq_run(t, a, b, 3) == s0) {
+                s = s0;
+                break;
+            }
+        }
+        states[p] = s;
+    }
+    offs[parts] = n;
+    if (t) munmap(const_cast<char*>(t), n);
+    ::close(fd);
+    return 0;
+}
+
 int skq_fastq_open(const char* path, skq_fastq** out) {
     if (!path || !out) return fail(-1, "null argument");
     *out = nullptr;

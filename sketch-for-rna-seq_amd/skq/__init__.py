@@ -91,6 +91,9 @@ def lib():
             "skq_fastq_id": (i32, [vp, u64, C.POINTER(vp), C.POINTER(u64)]),
             "skq_fastq_close": (i32, [vp]),
             "skq_ingest_open": (i32, [vp, C.c_char_p, u64, i32, C.POINTER(vp)]),
+            "skq_ingest_open_range": (i32, [vp, C.c_char_p, u64, u64, C.c_uint32, u64, i32, C.POINTER(vp)]),
+            "skq_ingest_supersede": (i32, [vp, C.c_uint32, vp]),
+            "skq_fastq_split": (i32, [C.c_char_p, C.c_uint32, vp, vp]),
             "skq_ingest_map": (i32, [vp, u32, dbl, i32, vp, C.POINTER(u64), C.POINTER(u64)]),
             "skq_ingest_records": (u64, [vp]),
             "skq_ingest_finish": (i32, [vp, vp]),
@@ -470,10 +473,17 @@ class FastqReader:
 class Ingest:
     """FASTQ parsed on the GPU (skq_ingest_*): batches of records mapped through `session`."""
 
-    def __init__(self, session, path, chunk_bytes=0, io_threads=4):
+    def __init__(self, session, path, chunk_bytes=0, io_threads=4, part=None):
+        """part = (lo, hi, entry_state): only the records whose header starts in [lo, hi)
+        (fastq_split), numbered from 0."""
         self.session = session  # keeps the session alive
         self.h = C.c_void_p()
-        _check(lib().skq_ingest_open(session.h, str(path).encode(), chunk_bytes, io_threads, C.byref(self.h)))
+        if part is None:
+            _check(lib().skq_ingest_open(session.h, str(path).encode(), chunk_bytes, io_threads, C.byref(self.h)))
+        else:
+            lo, hi, state = part
+            _check(lib().skq_ingest_open_range(session.h, str(path).encode(), lo, hi, state, chunk_bytes, io_threads,
+                                               C.byref(self.h)))
 
     def map(self, thr=None, fraction=0.9, accumulate=True, stream=None):
         """(first ordinal, n) of the next batch, now in the session's results; n == 0 at the end."""
@@ -502,6 +512,22 @@ class Ingest:
 
     def __del__(self):
         self.close()
+
+
+def fastq_split(path, parts):
+    """(offs[parts + 1], states[parts]): the file's parts at line starts with the reader's exact
+    state at each (skq_fastq_split)."""
+    offs = np.zeros(parts + 1, np.uint64)
+    states = np.zeros(parts, np.uint32)
+    _check(lib().skq_fastq_split(str(path).encode(), parts, _p(offs), _p(states)))
+    return offs, states
+
+
+def ingest_supersede(ingests, kepts):
+    """Clear kept flags of records whose id a later part keeps (skq_ingest_supersede)."""
+    hs = (C.c_void_p * len(ingests))(*[g.h.value for g in ingests])
+    ks = (C.c_void_p * len(kepts))(*[k.ctypes.data for k in kepts])
+    _check(lib().skq_ingest_supersede(C.cast(hs, C.c_void_p), len(ingests), C.cast(ks, C.c_void_p)))
 
 
 def _csr(cand_offs, cand_tid, cand_score):

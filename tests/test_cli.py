@@ -64,8 +64,11 @@ def _records(path):
     return recs
 
 
-@pytest.mark.parametrize("ks", [[31], [21, 25, 31]])
-def test_synthetic_quant_matches_the_oracle_pipeline(tmp_path, ks):
+@pytest.mark.parametrize("ks,devices", [([31], None), ([21, 25, 31], None), ([31], "0,0"), ([21, 25, 31], "0,0,0")])
+def test_synthetic_quant_matches_the_oracle_pipeline(tmp_path, ks, devices):
+    """devices: SKQ_DEVICES, the file split in parts mapped by one host thread and device index
+    each (here the same GPU several times: the posterior sums reduce through the host instead of
+    RCCL), duplicate ids settled across the parts, EM rounds sharded over the parts."""
     tx = synth.transcriptome(150, seed=61)
     fa, fq = tmp_path / "t.fa", tmp_path / "r.fq"
     tx.write_fasta(fa)
@@ -85,6 +88,8 @@ def test_synthetic_quant_matches_the_oracle_pipeline(tmp_path, ks):
     idx, csv = tmp_path / "t.idx", tmp_path / "t.csv"
     run("-k", ",".join(map(str, ks)), "-o", "index", fa, idx)
     env = dict(os.environ, SKQ_BATCH="700")  # several batches
+    if devices:
+        env["SKQ_DEVICES"] = devices
     run("-o", "quant", idx, fq, csv, env=env)
 
     # oracle pipeline

@@ -118,6 +118,36 @@ def test_reader_restatement_matches_host_reader(tmp_path):
         assert list(zip(ids, seqs)) == ref_records(data)
 
 
+def _machine_states(data):
+    """The reader's record-machine state at every line start (src/main.cpp:119-129)."""
+    st, s, a = {}, 0, 0
+    while a < len(data):
+        st[a] = s
+        s = (1 if data[a:a + 1] == b"@" else 0) if s == 0 else (s + 1) & 3
+        nl = data.find(b"\n", a)
+        a = len(data) if nl < 0 else nl + 1
+    st[len(data)] = s
+    return st
+
+
+def test_fastq_split_points_and_states(tmp_path):
+    """skq_fastq_split: part bounds at line starts, and the exact reader state there, also where
+    the four possible states never converge (every line starts with '@': the whole prefix)."""
+    tx = synth.transcriptome(30, seed=2)
+    cases = [tricky_fastq(tx, 800, seed=3, long_junk=500), b"@x\n" * 20000, b"", b"@a\nAC", b"@a\n" + b"+\n" * 7000]
+    for data in cases:
+        p = tmp_path / "s.fq"
+        p.write_bytes(data)
+        st = _machine_states(data)
+        for parts in (1, 2, 3, 7):
+            offs, states = skq.fastq_split(p, parts)
+            assert offs[0] == 0 and offs[-1] == len(data) and all(np.diff(offs.astype(np.int64)) >= 0)
+            for q in range(parts):
+                o = int(offs[q])
+                assert o == 0 or data[o - 1:o] == b"\n"
+                assert states[q] == st[o], (q, o)
+
+
 @pytest.fixture(scope="module")
 def tx200():
     tx = synth.transcriptome(200, seed=77)
@@ -153,6 +183,55 @@ def test_ingest_matches_reference_reader(tmp_path, tx200, chunk, max_reads):
     p.write_bytes(data)
     res = ingest_all(index, p, max_reads, chunk_bytes=chunk)
     check_against_reference(res, data, oi)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,chunk", [(2, 0), (3, 4096), (5, 1 << 15)])
+def test_ingest_in_parts_matches_reference_reader(tmp_path, tx200, parts, chunk):
+    """The file split for several devices (here all on one): every part ingested from its bounds
+    and entry state, duplicate ids settled across parts; in file order the records, statuses,
+    sketches, candidates and kept flags equal the single reader's."""
+    tx, _, index, oi = tx200
+    data = tricky_fastq(tx, 1500, seed=5)
+    rng = random.Random(parts)
+    lines = data.split(b"\n")
+    # the same ids again near the end of the file, so duplicates cross the parts
+    extra = []
+    for _ in range(40):
+        i = rng.randrange(0, 1400)
+        seq = tx.seq(i % tx.ntx)[:150]
+        extra.append(b"@read%d tx=%d\n%s\n+\n%s\n" % (i, i % 7, seq, b"I" * len(seq)))
+    data = data + b"".join(extra)
+    p = tmp_path / "r.fq"
+    p.write_bytes(data)
+    offs, states = skq.fastq_split(p, parts)
+    res, gs, kepts = [], [], []
+    for q in range(parts):
+        s = skq.Session(index, 300, 256)
+        g = skq.Ingest(s, p, chunk_bytes=chunk, part=(int(offs[q]), int(offs[q + 1]), int(states[q])))
+        status, hashes, cands = [], [], []
+        while True:
+            first, n = g.map(fraction=0.9)
+            if n == 0:
+                break
+            s.check()
+            out = s.export()
+            status.append(out["status"].copy())
+            ho, co = out["hash_offs"], out["cand_offs"]
+            for r in range(n):
+                hashes.append(list(out["hashes"][ho[r]:ho[r + 1]]))
+                cands.append((list(out["cand_tid"][co[r]:co[r + 1]]), list(out["cand_score"][co[r]:co[r + 1]])))
+        kepts.append(g.finish())
+        gs.append(g)
+        res.append((status, hashes, cands, [g.id(r) for r in range(g.records())], s))
+    skq.ingest_supersede(gs, kepts)
+    merged = dict(status=np.concatenate([np.concatenate(r[0]) if r[0] else np.zeros(0, np.uint8) for r in res]),
+                  hashes=sum((r[1] for r in res), []), cands=sum((r[2] for r in res), []),
+                  ids=sum((r[3] for r in res), []), kept=np.concatenate(kepts))
+    assert len(set(merged["ids"])) < len(merged["ids"])  # duplicate ids present
+    check_against_reference(merged, data, oi)
+    for g in gs:
+        g.close()
 
 
 @pytest.mark.gpu
