@@ -158,8 +158,9 @@ void dev_free(T*& p) {
 }
 
 // choose the raw-retained capacity per (read, k) for a batch: the smallest of 16/32/64 holding
-// the expected count plus 4 sigma (reads beyond it are still exact, through the slow path;
-// at 150 bp, k = 31, 5 % that is ~4e-5 of reads)
+// the expected count plus 4 sigma (reads beyond it are still exact, through the wave slow path;
+// at 150 bp, 5 %: 16 at k = 31 (1.3e-4 of the reads past it), 32 at k = 21, 25, 31; 3 sigma (16
+// there) sent 18k of 10M reads to the slow path: 4 % slower at cfg5)
 uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold) {
     const uint32_t L = std::min<uint32_t>(max_len, skq::LFAST);
     const double w = L >= mink ? (double)(L - mink + 1) : 0.0;

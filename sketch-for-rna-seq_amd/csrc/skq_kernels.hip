@@ -1615,7 +1615,9 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
 // count words 0 on entry); flagw (the wave's 64 words, zeroed) marks reads with more than TS
 // transcripts. Writes each counted read's candidates, or lists it for the slow chain path;
 // returns the candidate count, key[] holding them in output order. Every lane must call it.
-template <int NK, bool CMP = false>
+// R: rounds of 32 entries in flight together (8 in k_mapk, where LDS holds the kernel at 3 waves
+// per SIMD anyway: 5 % slower at cfg5)
+template <int NK, bool CMP = false, int R = 4>
 __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64_t r, uint64_t rr, bool act,
                                                     uint32_t (&cnts)[NK], uint32_t* colbase, uint32_t* hl,
                                                     uint8_t* ow, uint32_t* sll, uint32_t cap, uint32_t* flagw,
@@ -1628,7 +1630,6 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
         m += cnts[i];
     }
     const uint32_t incl = wave_incl_scan(m, lane);
-    const uint32_t off = incl - m;
     const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes, all k slots
     const bool odd = lane & 1u;
     auto wd_of = [&](uint32_t i) -> const uint32_t* {
@@ -1691,26 +1692,34 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
     }
 
     for (uint32_t pb = 0; pb < M; pb += cap) {  // wave-uniform
-        // this lane's entries that fall in the pass, straight from the sketch's hash rows: the
-        // first 8 of every k slot in one round trip (all loads issued before any store), the
-        // rest (reads with more than 8 at a k) 8 at a time
-        {
-            uint32_t e = off;
+        // this lane's entries that fall in the pass, straight from the sketch's hash rows. The
+        // first 8 of every k slot (loaded once, before the passes) go in (k slot, rank) order
+        // across the wave's reads, so a round of 32 consecutive entries holds one hash of 32
+        // different reads: their inserts go to 32 different count tables (read-major order put
+        // most of a round into one read's table: 20x the LDS address conflicts of k_map1). The
+        // rest (reads with more than 8 at a k: rare) follow in read order, 8 at a time.
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t base = 0;
 #pragma unroll
-            for (int i = 0; i < NK; ++i) {
+        for (int i = 0; i < NK; ++i) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t ee = e + u;
-                    if ((uint32_t)u < cnts[i] && ee >= pb && ee < pb + cap) {
-                        hl[ee - pb] = hx[i][u];
-                        ow[ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
-                    }
+            for (int u = 0; u < 8; ++u) {
+                const bool has = (uint32_t)u < cnts[i];
+                const uint64_t bal = __ballot(has);
+                const uint32_t ee = base + (uint32_t)__builtin_popcountll(bal & lt);
+                if (has && ee >= pb && ee < pb + cap) {
+                    hl[ee - pb] = hx[i][u];
+                    ow[ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
                 }
-                e += cnts[i];
+                base += (uint32_t)__builtin_popcountll(bal);
             }
         }
         {
-            uint32_t e = off;
+            uint32_t m8 = 0;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) m8 += cnts[i] > 8 ? cnts[i] - 8 : 0u;
+            const uint32_t incl8 = wave_incl_scan(m8, lane);
+            uint32_t e = base + incl8 - m8;
 #pragma unroll
             for (int i = 0; i < NK; ++i) {
                 const uint32_t c = cnts[i];
@@ -1722,14 +1731,14 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
                     for (int u = 0; u < 8; ++u) x[u] = j0 + u < c ? src[(uint64_t)(j0 + u) * p.n] : 0u;
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        const uint32_t ee = e + j0 + u;
+                        const uint32_t ee = e + (j0 - 8) + u;
                         if (j0 + u < c && ee >= pb && ee < pb + cap) {
                             hl[ee - pb] = x[u];
                             ow[ee - pb] = (uint8_t)(lane | ((uint32_t)i << 6));
                         }
                     }
                 }
-                e += c;
+                e += c > 8 ? c - 8 : 0u;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1760,7 +1769,6 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        constexpr int R = 4;  // rounds of 32 entries in flight together
         for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
             uint4 w[R];
             uint32_t own[R], hk[R];
@@ -2263,14 +2271,17 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             // words 0-7 (bitmap, overflow base, entry A's meta and t0..t4), the odd lane words
             // 8-15 (A's t5, entry B); four swaps give each lane what its half of the inserts
             // needs (even: t0..t2 of the key's entry, odd: t3..t5)
-            for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
+            // lane pair q walks entries [q * S, (q + 1) * S): the 32 entries of one round lie S apart,
+            // mostly in different reads' count tables (fewer LDS atomics on one address)
+            const uint32_t S = (ne + 31) >> 5;
+            for (uint32_t e0 = 0; e0 < S; e0 += R) {
                 uint4 b0[R], b1[R];
                 uint32_t own[R], hh[R];
                 bool ok[R];
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    const uint32_t e = e0 + 32 * u + (lane >> 1);
-                    const bool in = e < ne;
+                    const uint32_t e = (lane >> 1) * S + e0 + u;
+                    const bool in = e0 + u < S && e < ne;
                     hh[u] = s_h[in ? e : 0];
                     own[u] = s_own[in ? e : 0];
                     ok[u] = in && (hh[u] >> 5) < wlen;
@@ -2323,7 +2334,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
             continue;
         }
-        for (uint32_t e0 = 0; e0 < ne; e0 += 32 * R) {
+        // lane pair q walks entries [q * S, (q + 1) * S): the 32 entries of one round lie S apart,
+        // mostly in different reads' count tables (fewer LDS atomics on one address)
+        const uint32_t S = (ne + 31) >> 5;
+        for (uint32_t e0 = 0; e0 < S; e0 += R) {
             uint4 w[R];
             uint32_t own[R], hk[R];
             bool ok[R];
@@ -2331,8 +2345,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 // one entry each, at the slot listed with the hash
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    const uint32_t e = e0 + 32 * u + (lane >> 1);
-                    ok[u] = e < ne;
+                    const uint32_t e = (lane >> 1) * S + e0 + u;
+                    ok[u] = e0 + u < S && e < ne;
                     const uint32_t ee = ok[u] ? e : 0;
                     hk[u] = s_h[ee];
                     const uint32_t x = s_x[ee];
@@ -2342,8 +2356,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             } else {
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    const uint32_t e = e0 + 32 * u + (lane >> 1);
-                    const bool in = e < ne;
+                    const uint32_t e = (lane >> 1) * S + e0 + u;
+                    const bool in = e0 + u < S && e < ne;
                     hk[u] = s_h[in ? e : 0];
                     own[u] = s_own[in ? e : 0];
                     ok[u] = in && hk[u] < wlen;
@@ -2482,6 +2496,7 @@ __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
     uint32_t* s_bc = s_flag + WG;
     uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_rows + wv * 64);  // (row 0 of the wave's columns)
     const bool bin = cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
+    MAP1_STAMP(0);
     for (uint32_t e = tid; e < NK * 16 + 4; e += WG) {
         const uint64_t v = p.rolltab[e];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
@@ -2540,6 +2555,7 @@ __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    MAP1_STAMP(1);
     const bool live = lane < nr;
     const uint64_t r = live ? r0 + lane : 0;
     uint64_t start = 0, len = 0;
@@ -2659,6 +2675,7 @@ __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    MAP1_STAMP(2);
     // list entries a pass: hashes, then owners (then, compact tables, the hashes' slots)
     const uint32_t cap = (uint32_t)(wave_bytes / (CMP ? 9 : 5)) & ~31u;
     uint32_t key[TS];
@@ -2666,8 +2683,11 @@ __global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
                                                  s_wave + (size_t)cap * 4,
                                                  reinterpret_cast<uint32_t*>(s_wave + (size_t)cap * 5), cap,
                                                  s_flag + wv * 64, lane, key);
+    MAP1_STAMP(3);
+    MAP1_STAMP(4);
     // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
     if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_rows);
+    MAP1_STAMP(5);
 }
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
