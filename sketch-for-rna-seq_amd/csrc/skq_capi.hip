@@ -123,6 +123,7 @@ struct skq_session {
     uint32_t* bin_hdr[2] = {};
     uint32_t* bin_region[2] = {};
     uint32_t bin_par = 0;
+    uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     uint32_t* ctrl = nullptr;
@@ -755,6 +756,7 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
         (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
         (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
+        (rc = dev_alloc(&s->tx_acc, ix->ntx)) ||
         (rc = dev_alloc(&s->ctrl, skq::C_WORDS)) || (rc = ensure_hashes(s, hcap0))) {
         skq_session_free(s);
         return rc;
@@ -770,6 +772,7 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
             return rc;
         }
     if (hipMemset(s->tx_reads, 0, ix->ntx * 8ull) != hipSuccess ||
+        hipMemset(s->tx_acc, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->ctrl, 0, skq::C_WORDS * 4) != hipSuccess) {
         skq_session_free(s);
@@ -812,6 +815,7 @@ int skq_session_free(skq_session* s) {
         dev_free(s->bin_hdr[b]);
         dev_free(s->bin_region[b]);
     }
+    dev_free(s->tx_acc);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -929,7 +933,9 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         HIP_TRY(hipEventRecord(s->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
         record(s, 3, &t0, s->side);
-        if (skq::launch_bin(p, 1, s->side)) return fail(-3, "totals launch failed");
+        if (skq::launch_bin(p, 1, s->side) ||
+            skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, s->side))
+            return fail(-3, "totals launch failed");
         record_stop(s, 3, t0, s->side);
         HIP_TRY(hipEventRecord(s->ev_join[s->bin_par], s->side));
         s->join_rec[s->bin_par] = true;
@@ -951,8 +957,11 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         if (skq::launch_chain_slow(p, st)) return fail(-3, "chain slow-path launch failed");
     }
     if (accumulate && !fork) {
+        if (int rc = wait_totals(s, st)) return rc;  // (tx_acc: an earlier batch's fold may be pending)
         record(s, 3, &t0, st);
-        if (skq::launch_bin(p, p.slow_totals, st)) return fail(-3, "totals launch failed");
+        if (skq::launch_bin(p, p.slow_totals, st) ||
+            skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, st))
+            return fail(-3, "totals launch failed");
         record_stop(s, 3, t0, st);
     }
     if (accumulate && p.bin_nb) s->bin_par ^= 1;  // this batch's bins were written
@@ -989,6 +998,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.cand_ext_cap = s->cand_ext_cap;
     p.scratch = s->scratch;
     p.scratch_cap = s->scratch_cap;
+    p.tx_acc = s->tx_acc;
     p.tx_reads = s->tx_reads;
     p.tx_score = s->tx_score;
     p.ctrl = s->ctrl;
@@ -1155,6 +1165,7 @@ int skq_session_reset_totals(skq_session* s, void* stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (int rc = wait_totals(s, st)) return rc;
     HIP_TRY(hipMemsetAsync(s->tx_reads, 0, s->idx->ntx * 8ull, st));
+    HIP_TRY(hipMemsetAsync(s->tx_acc, 0, s->idx->ntx * 8ull, st));
     HIP_TRY(hipMemsetAsync(s->tx_score, 0, s->idx->ntx * 8ull, st));
     return 0;
 }

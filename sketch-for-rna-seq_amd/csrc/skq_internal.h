@@ -125,6 +125,7 @@ struct ChainParams {
     uint64_t cand_ext_cap;     // pairs
     uint64_t* scratch;
     uint64_t scratch_cap;      // u64 words
+    uint64_t* tx_acc;          // per batch: (reads << 40) | score (k_bin_sum), folded by k_fold_totals
     uint64_t* tx_reads;
     uint64_t* tx_score;
     uint32_t* ctrl;
@@ -193,8 +194,10 @@ int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
 // the wave slow path behind k_map1 / k_mapk (wide or compact tables, <= 4 k slots; -4 otherwise):
 // the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
 int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);
-// per-transcript totals of the batch's final candidates into p.tx_reads / p.tx_score (k_bin +
-// k_bin_sum; atomics, so they commute with the slow paths' direct adds)
+int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
+// per-transcript totals of the batch's final candidates into p.tx_acc (k_bin + k_bin_sum), then
+// launch_fold_totals adds them into p.tx_reads / p.tx_score with atomics (commuting with the slow
+// paths' direct adds)
 // (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs)
 int launch_bin(const ChainParams& p, int binned, void* stream);
 // whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)

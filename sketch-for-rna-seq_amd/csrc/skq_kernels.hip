@@ -3190,7 +3190,8 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
 // where bucket b starts in region w (b = nb: the region's total). Candidates that do not pack
 // (overflow lists, huge scores) are added directly. Pass 2, one workgroup per (chunk of
 // regions, bucket): an LDS histogram of the bucket, flushed with one coalesced atomic per
-// non-empty bin into the running totals (two atomics: reads, score).
+// non-empty bin into the batch's packed sums tx_acc, which k_fold_totals adds into the running
+// totals with atomics (commuting with the slow paths' direct adds) and clears.
 __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW, uint32_t* hdr,
                                            uint32_t* region) {
     __shared__ uint32_t s_cnt[WG + 1], s_fill[WG + 1];
@@ -3282,8 +3283,7 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
     for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
-__global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_reads, uint64_t* tx_score, uint32_t ntx, uint32_t bits,
-                                               uint32_t nb, uint32_t nW,
+__global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nb, uint32_t nW,
                                                uint32_t chunk, const uint32_t* hdr, const uint32_t* region) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
@@ -3325,10 +3325,19 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_reads, uint64_t* tx
     for (uint32_t i = t; i < bs; i += WG) {
         const unsigned long long a = s_bins[i];
         const uint32_t tx = b * bs + i;
-        // (a bin packs (reads << 40) | score: a batch holds < 2^24 reads of score <= 2^10)
-        if (a && tx < ntx) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&tx_reads[tx]), a >> 40);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&tx_score[tx]), a & ((1ull << 40) - 1));
+        // one packed atomic per bin ((reads << 40) | score: a batch holds < 2^24 reads of score
+        // <= 2^10); k_fold_totals unpacks the batch's sums once
+        if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx) {
+    for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < ntx; t += gridDim.x * WG) {
+        const uint64_t a = acc[t];
+        if (a) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&reads[t]), (unsigned long long)(a >> 40));
+            atomicAdd(reinterpret_cast<unsigned long long*>(&score[t]), (unsigned long long)(a & ((1ull << 40) - 1)));
+            acc[t] = 0;
         }
     }
 }
@@ -3563,6 +3572,14 @@ int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* va
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream) {
+    if (ntx == 0) return 0;
+    const unsigned grid = (unsigned)std::min<uint32_t>((ntx + WG - 1) / WG, 1024);
+    hipLaunchKernelGGL(k_fold_totals, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), acc, reads,
+                       score, ntx);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int launch_bin(const ChainParams& p, int binned, void* stream) {
     if (p.n == 0) return 0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -3583,7 +3600,7 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     if (lds > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-    hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_reads, p.tx_score, p.ntx, bits, nb,
+    hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits, nb,
                        nW, chunk, hdr, region);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
