@@ -2893,6 +2893,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
     __shared__ uint32_t s_h[NK][SW_H + 1];
     __shared__ uint32_t s_tid[SW_T], s_c[SW_T];
     __shared__ uint64_t s_key[SW_T];
+    __shared__ uint8_t s_seq[SW_NW + 64 + 16];  // the read's bases (len <= SW_NW + min k - 1)
     __shared__ uint32_t s_m[NK], s_flag, s_nc;
     __shared__ unsigned long long s_at;
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -2914,20 +2915,34 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
             uint32_t mink = p.ks[0];
 #pragma unroll
             for (int i = 1; i < NK; ++i) mink = min(mink, p.ks[i]);
-            if (len > (uint64_t)SW_NW + mink - 1) {
+            if (len > (uint64_t)SW_NW + mink - 1 || len > (uint64_t)SW_NW + 64) {  // (s_seq's size)
                 if (lane == 0) {
                     list_push(p.ctrl, C_OVF3, C_ERR1, ovf3, p.ovf_cap, r, E_OVF1_FULL);
                     list_push(cp.ctrl, C_OVF4, C_ERR2, ovf4, cp.ovf_cap, r, E_OVF2_FULL);
                 }
                 continue;
             }
-            const uint8_t* sb = p.reads + start;
+            // the bases to LDS first (all of a lane's loads in flight together): the hashing below
+            // reads each base up to twice, in dependent steps
             bool bad = false;
-            for (uint32_t q = lane; q < len; q += 64) {
-                const uint8_t c = sb[q];
-                bad |= !(c == 'A' || c == 'C' || c == 'G' || c == 'T');
+            {
+                const uint8_t* g = p.reads + start;
+                uint8_t c[(SW_NW + 64 + 63) / 64];
+#pragma unroll
+                for (uint32_t t = 0; t < (SW_NW + 64 + 63) / 64; ++t) {
+                    const uint32_t q = lane + 64 * t;
+                    c[t] = q < len ? g[q] : (uint8_t)'A';
+                }
+#pragma unroll
+                for (uint32_t t = 0; t < (SW_NW + 64 + 63) / 64; ++t) {
+                    const uint32_t q = lane + 64 * t;
+                    if (q < len) s_seq[q] = c[t];
+                    bad |= !(c[t] == 'A' || c[t] == 'C' || c[t] == 'G' || c[t] == 'T');
+                }
             }
             bad = __any(bad);
+            wave_sync();
+            const uint8_t* sb = s_seq;
             st = bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
             for (uint32_t i = lane; i < p.nk; i += 64) p.hash_cnt[(uint64_t)i * n + r] = 0;
             bool fits = true;
