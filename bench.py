@@ -240,7 +240,7 @@ def main(args):
     # algorithmic bytes per read, per kernel (DESIGN.md "Roofline"); an index lookup is priced at
     # the 8 B (key, list offset) it needs, a posting at its 4 B tid
     fused = kt[1][1] == 0  # no k_probe launches: the sketch kernel probed (direct/rank table)
-    # one fused map kernel (k_map1 / k_mapk: sketch + entry gathers + count), timed as kind 0
+    # the fused map (k_map1, or its passes for several k: sketch + entry gathers + count), timed as kind 0
     # with no separate count launches
     map1 = kt[2][1] == 0 and kt[0][1] > 0
     count_name = "k_count3" if tx.ntx <= (1 << 22) else "k_count"
@@ -251,7 +251,8 @@ def main(args):
         count_name: 2 + 4 * nk + 4 * h + 4 * P + 4 + 8 * Cn + 4 * Cn,
         "totals": 4 * Cn + 16.0 * tx.ntx / n,
     }
-    fused_name = "k_map1" if nk == 1 else "k_mapk"
+    # (2..4 k slots: one k_map1 pass per k slot, the last merging, timed together as one map)
+    fused_name = "k_map1" if nk == 1 else "k_map1 x%d passes" % nk
     if map1:  # the fused kernel: read in, one lookup per hash, postings, hashes + candidates out
         b_kern = {fused_name: L + 1 + 4 * nk + 4 * h + 8 * h + b_chain, "totals": b_kern["totals"]}
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula

@@ -124,6 +124,8 @@ struct skq_session {
     uint32_t* bin_region[2] = {};
     uint32_t bin_par = 0;
     uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
+    uint32_t* ktab = nullptr;    // multi-k map by passes: per-k count tables (allocated on first use)
+    uint8_t* kcnt = nullptr;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     uint32_t* ctrl = nullptr;
@@ -162,12 +164,15 @@ void dev_free(T*& p) {
 // the expected count plus 4 sigma (reads beyond it are still exact, through the wave slow path;
 // at 150 bp, 5 %: 16 at k = 31 (1.3e-4 of the reads past it), 32 at k = 21, 25, 31; 3 sigma (16
 // there) sent 18k of 10M reads to the slow path: 4 % slower at cfg5)
-uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold) {
+// (sigmas 3 for the multi-k passes: a capacity of 32 holds k_map1 at 3 workgroups per CU for
+// 2.0 ms a pass at cfg5 against 1.47 ms at 16, and the ~2e-4 of the reads past 16 at k = 21, 25
+// cost the wave slow path far less)
+uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold, double sigmas = 4.0) {
     const uint32_t L = std::min<uint32_t>(max_len, skq::LFAST);
     const double w = L >= mink ? (double)(L - mink + 1) : 0.0;
     const double f = ((double)threshold + 1.0) / 4294967296.0;
     const double mu = w * f;
-    const double need = mu + 4.0 * std::sqrt(mu * (1.0 - f));
+    const double need = mu + sigmas * std::sqrt(mu * (1.0 - f));
     if (need <= 16) return 16;
     if (need <= 32) return 32;
     return 64;
@@ -816,6 +821,8 @@ int skq_session_free(skq_session* s) {
         dev_free(s->bin_region[b]);
     }
     dev_free(s->tx_acc);
+    dev_free(s->ktab);
+    dev_free(s->kcnt);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -999,6 +1006,8 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.scratch = s->scratch;
     p.scratch_cap = s->scratch_cap;
     p.tx_acc = s->tx_acc;
+    p.ktab = s->ktab;
+    p.kcnt = s->kcnt;
     p.tx_reads = s->tx_reads;
     p.tx_score = s->tx_score;
     p.ctrl = s->ctrl;
@@ -1056,7 +1065,7 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
 }
 
 // Fused map: k_map1 (compact, wide or block tables, one k slot, a raw capacity of 16 or 32) or
-// k_mapk (compact or wide tables, 2..4 k slots); anything else takes the two-kernel path (a caller
+// k_map1 passes (compact or wide tables, 2..4 k slots); anything else takes the two-kernel path (a caller
 // can always ask for that path itself with skq_sketch + skq_chain)
 static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,
                         uint32_t threshold) {
@@ -1065,7 +1074,7 @@ static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t f
     const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(max_len, s->max_len), skq::LFAST));
     const uint32_t hcap = pick_hcap(Lc, ix->mink, threshold);
     if (ix->nk == 1) return ix->mode >= 3 && (hcap == 16 || hcap == 32);
-    // 2..4 k slots: k_mapk (wide or compact tables, hcap 16 or 32)
+    // 2..4 k slots: k_map1 passes (wide or compact tables, hcap 16 or 32)
     return (ix->mode == 3 || ix->mode == 5) && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32);
 }
 
@@ -1074,6 +1083,11 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
                      void* stream) {
     skq::SketchParams sp{};
     skq::ChainParams cp{};
+    if (s->idx->nk > 1 && !s->ktab) {  // the per-k tables of the multi-k passes
+        DeviceGuard g(s->idx->device);
+        if (int rc = dev_alloc(&s->ktab, (uint64_t)s->idx->nk * skq::DCAP * s->max_reads)) return rc;
+        if (int rc = dev_alloc(&s->kcnt, (uint64_t)s->idx->nk * s->max_reads)) return rc;
+    }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
@@ -1084,7 +1098,22 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     if (int rc = wait_bins(s, st)) return rc;
     hipEvent_t t0{};
     record(s, 0, &t0, st);
-    const int rc = s->idx->nk == 1 ? skq::launch_map1(sp, cp, stream) : skq::launch_mapk(sp, cp, stream);
+    int rc = 0;
+    if (s->idx->nk == 1) {
+        rc = skq::launch_map1(sp, cp, stream);
+    } else {
+        // 2..4 k slots: one k_map1 pass per k slot (each with the raw capacity its k needs), their
+        // per-k tables in the session's ktab / kcnt; the last pass merges, filters and bins
+        const uint32_t nk = s->idx->nk;
+        for (uint32_t i = 0; i < nk && !rc; ++i) {
+            skq::SketchParams pi = sp;
+            pi.kslot = i;
+            const uint32_t ml = d_offs ? max_len : fixed_len;
+            const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(ml, s->max_len), skq::LFAST));
+            rc = skq::launch_map1_pass(pi, cp, std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, 3.0)),
+                                       i + 1 == nk, stream);
+        }
+    }
     if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
     record_stop(s, 0, t0, st);
     if (int rc = chain_tail(s, &sp, cp, accumulate, st)) return rc;

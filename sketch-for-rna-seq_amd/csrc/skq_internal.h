@@ -84,6 +84,7 @@ struct SketchParams {
     uint32_t* ctrl;
     uint32_t* ovf1;
     uint32_t ovf_word;  // the control word counting ovf1 (k_sketch_slow: C_OVF1, or C_OVF3 behind k_slow_wave)
+    uint32_t kslot;     // k_map1 pass mode: the k slot this pass sketches and counts
     // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
@@ -143,6 +144,11 @@ struct ChainParams {
     uint32_t* bin_region;
     int slow_totals;
     uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
+    // multi-k map by passes (k_map1 pass mode; the final pass merges): per k slot i and read r, the read's
+    // count table at that k, unfiltered: kcnt[i * n + r] entries (tid << 8 | count) at
+    // ktab[(i * TS + j) * n + r]
+    uint32_t* ktab;
+    uint8_t* kcnt;
     // wide direct tables (DESIGN.md "Index"): entry h of k slot i is 8 words at wdir[i] + 8h,
     // [n, t0..t6] for lists of n <= 7 transcripts, [0x80000000 | list offset, t0..t6] for longer
     // ones (the rest at lists[offset + 8..]), n = 0 for no key; h >= wdir_len[i] is a miss.
@@ -186,12 +192,14 @@ int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid = 2048);
 // fused sketch + chain (k_map1: quant mode, one k slot, wide tables, hcap 16 or 32; -4 otherwise)
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
-// fused sketch + chain for 2..4 k slots (k_mapk: wide tables, hcap 16 or 32; -4 otherwise)
-int launch_mapk(const SketchParams& p, const ChainParams& cp, void* stream);
+// fused sketch + chain for 2..4 k slots (wide or compact tables) by passes: k_map1 in pass mode
+// for each k slot (p.kslot; a raw capacity `cap` of 16 or 32 hashes, at most the hashes' layout
+// stride p.hcap); the last (final_pass) merges the per-k tables, filters, orders and bins
+int launch_map1_pass(const SketchParams& p, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream);
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
-// the wave slow path behind k_map1 / k_mapk (wide or compact tables, <= 4 k slots; -4 otherwise):
+// the wave slow path behind k_map1 and its passes (wide or compact tables, <= 4 k slots; -4 otherwise):
 // the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
 int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);
 int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);

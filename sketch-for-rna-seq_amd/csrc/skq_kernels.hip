@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(WG) void k_route_slow(ChainParams p) {
 //   * the per-read words and the first 8 list offsets loaded together up front, and the list
 //     heads and second quads (tids 3..6) gathered in batches,
 //   * 32-bit sort keys ((1023 - score) << 22 | tid; needs ntx <= 2^22, scores <= 4 * 255).
-constexpr int TS = 16;    // distinct transcripts per read on the fast path (slot TS: sink)
+constexpr int TS = DCAP;  // distinct transcripts per read on the fast path (slot TS: sink)
 constexpr int PEND = 8;   // parked collisions per read (slot PEND: sink)
 
 // swap with the other lane of the pair (quad_perm(1,0,3,2))
@@ -1608,15 +1608,15 @@ __global__ __launch_bounds__(WG) void k_count3(ChainParams p) {
 // slot), slot s of read o in column (o + s) & 63 of the wave (distinct LDS banks). Then the
 // filter of src/sparse_chaining.cpp:76-110 at every k, the candidates, and the binning epilogue.
 // Reads with more than TS distinct transcripts go to the slow chain path, as in k_count3.
-// The count phase over wide tables for 2..4 k slots, one wave (k_countw, k_mapk): read r's
+// The count phase over wide tables for 2..4 k slots, one wave (k_countw): read r's
 // cnts[i] retained hashes of k slot i are at lofs (cnts zero for reads not counted); the wave's
 // hashes are listed at hl / ow in passes of `cap`; lane pairs gather the entries and insert into
 // the per-read tables in the wave's columns of the 2 * TS rows at colbase (tid words EMPTY and
 // count words 0 on entry); flagw (the wave's 64 words, zeroed) marks reads with more than TS
 // transcripts. Writes each counted read's candidates, or lists it for the slow chain path;
 // returns the candidate count, key[] holding them in output order. Every lane must call it.
-// R: rounds of 32 entries in flight together (8 in k_mapk, where LDS holds the kernel at 3 waves
-// per SIMD anyway: 5 % slower at cfg5)
+// R: rounds of 32 entries in flight together (8 measured 5 % slower in the round-2 fused multi-k
+// kernel, which LDS held at 3 waves per SIMD)
 template <int NK, bool CMP = false, int R = 4>
 __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64_t r, uint64_t rr, bool act,
                                                     uint32_t (&cnts)[NK], uint32_t* colbase, uint32_t* hl,
@@ -1748,7 +1748,7 @@ __device__ __forceinline__ uint32_t wide_count_wave(const ChainParams& p, uint64
         if constexpr (CMP) {
             // compact tables: every listed hash's slot, one lane per entry (all of the lane's
             // pilot loads in flight together), so the lane pairs gather without a dependent load
-            constexpr int SB = 4;  // (8 raises k_mapk's VGPRs past 128)
+            constexpr int SB = 4;  // (8 raised the multi-k kernels' VGPRs past 128)
             for (uint32_t e0 = 0; e0 < ne; e0 += 64 * SB) {
                 uint32_t kh[SB], pv[SB];
 #pragma unroll
@@ -1975,10 +1975,17 @@ size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
             cp.stamps[((uint64_t)blockIdx.x * (WG / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// TAB: 0 = wide tables, 1 = block tables, 2 = compact tables
-template <int HCAP, int MB, int TAB>
+// TAB: 0 = wide tables, 1 = block tables, 2 = compact tables. PASS: one k slot (p.kslot) of a
+// multi-k map: the read's count table at that k goes out unfiltered to cp.ktab / cp.kcnt, with
+// no candidates or binning; a read any pass lists for the slow path is listed once (pflag), and
+// a read an earlier pass found sketch-slow is skipped. FINAL (the last k slot's pass): the
+// earlier passes' tables are merged in registers with this pass's, then filtered, ordered,
+// written and binned as in the one-k map.
+template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     constexpr bool BLK = TAB == 1, CMP = TAB == 2;
+    static_assert(PASS || !FINAL, "the final pass is a pass");
+    const uint32_t ks = PASS ? p.kslot : 0u;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
@@ -1993,9 +2000,9 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * wave_bytes);
     uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + wv * 64);  // (row 0 of the wave's columns)
     uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1));
-    const bool bin = cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
-    for (uint32_t e = tid; e < 16 + 4; e += WG) {
-        const uint64_t v = p.rolltab[e];
+    const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
+    for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot ks's roll terms, then the seeds
+        const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
     }
     __syncthreads();
@@ -2083,15 +2090,18 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
     }
 
+    // pass mode, after the first pass: listed already (pf_prev), sketch-slow already (sk_prev)
+    const uint8_t pf_prev = (PASS && ks > 0 && live) ? p.pflag[r] : (uint8_t)0;
+    const bool sk_prev = PASS && ks > 0 && live && (p.status[r] & ST_SLOW1);
     uint32_t v[HCAP];
 #pragma unroll
     for (int j = 0; j < HCAP; ++j) v[j] = 0xFFFFFFFFu;
     uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
-    const bool hashing = live && !slow && st == SKQ_READ_OK;
+    const bool hashing = live && !slow && !sk_prev && st == SKQ_READ_OK;
     if (hashing) {
         const uint32_t T = p.threshold;
         const uint32_t L = (uint32_t)len;
-        const uint32_t k = p.ks[0];
+        const uint32_t k = p.ks[ks];
         auto codes16 = [&](uint32_t q) -> uint32_t {
             const uint32_t d = q >> 4;
             return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
@@ -2129,7 +2139,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
             bitonic_sort<HCAP>(v);
-            uint32_t* out = p.hashes + r;
+            uint32_t* out = p.hashes + (uint64_t)ks * p.hcap * p.n + r;
             uint32_t m = 0;
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) {
@@ -2139,19 +2149,22 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     keepm |= 1ull << j;
                 }
             }
-            p.hash_cnt[r] = m;
+            p.hash_cnt[(uint64_t)ks * p.n + r] = m;
         }
     }
-    if (live) {
+    if (live && !sk_prev) {
         if (slow) {
             st = ST_SLOW1;
-            list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
-            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+            if (!pf_prev) {
+                list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
+                list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+            }
         } else if (st != SKQ_READ_OK) {
-            p.hash_cnt[r] = 0;
+            p.hash_cnt[(uint64_t)ks * p.n + r] = 0;
         }
         p.status[r] = st;
-        p.pflag[r] = slow ? 1 : 0;  // (a later skq_chain on these results reads it)
+        // (a later skq_chain on these results reads it; pass mode: listed for the slow path)
+        if (!PASS || ks == 0 || slow) p.pflag[r] = slow ? 1 : 0;
     }
     MAP1_STAMP(2);
     // every lane of the wave has left the hashing loop: the staged codes become the parked lists
@@ -2165,7 +2178,9 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // owning read's transcript table with LDS atomics, so the work follows the tids the wave
     // really has rather than its longest read. Table of read (lane) o: column o of this wave in
     // the raw region, slot s at s * WG, (tid << 8 | count) or EMPTY; slot TS: overflow flag.
-    const bool act = hashing && !slow;
+    // (pass mode: a k slot the index has no table for is sketched but not counted,
+    // src/sparse_chaining.cpp:51-53)
+    const bool act = hashing && !slow && (!PASS || cp.tabs[ks].present);
     const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
     const uint32_t incl = wave_incl_scan(m, lane);
     const uint32_t off = incl - m;
@@ -2179,10 +2194,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
     uint32_t* s_x = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 4);  // compact: slot | lane << 26
     uint32_t* colbase = s_raw + wv * 64;
-    const uint32_t* wd = cp.wdir[0];
-    const uint64_t wlen = cp.wdir_len[0];
-    const uint16_t* cpil = cp.wpil[0];
-    const uint32_t cnb = cp.wnb[0], cseed = cp.wseed[0];
+    const uint32_t* wd = cp.wdir[ks];
+    const uint64_t wlen = cp.wdir_len[ks];
+    const uint16_t* cpil = cp.wpil[ks];
+    const uint32_t cnb = cp.wnb[ks], cseed = cp.wseed[ks];
     const bool odd = lane & 1u;
     // slot sl of read (lane) o sits in column (o + sl) & 63 of row sl: the slots of one read
     // fall in distinct LDS banks (the lane pairs of one round mostly insert into the same read)
@@ -2234,7 +2249,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             for (uint32_t d = 0; d < m; ++d) {
                 const uint32_t e = off + d;
                 if (e >= pb && e < pb + MAP_P) {
-                    s_h[e - pb] = p.hashes[(uint64_t)d * p.n + r];
+                    s_h[e - pb] = p.hashes[((uint64_t)ks * p.hcap + d) * p.n + r];
                     if (CMP) s_x[e - pb] = lane << 26;
                     else s_own[e - pb] = (uint8_t)lane;
                 }
@@ -2417,42 +2432,169 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(3);
     uint32_t key[TS];
     uint32_t nc = 0;
-    if (act) {
-        if (s_flag[lane] == 0) {
-            // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
-            uint32_t ev[TS];
-            uint32_t mx = 0;
+    if constexpr (PASS) {
+        bool listed = pf_prev != 0;  // listed for the slow path by this or an earlier pass
+        if (act) {
+            if (s_flag[lane] != 0) {  // more than TS transcripts at this k: the slow chain path
+                if (!listed) list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+                p.pflag[r] = 1;
+                listed = true;
+                if (!FINAL) cp.kcnt[(uint64_t)ks * cp.n + r] = 0;
+            } else if (!FINAL) {  // the read's table at this k, unfiltered, front-packed
+                uint32_t m = 0;
 #pragma unroll
-            for (int sl = 0; sl < TS; ++sl) {
-                ev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
-                mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
-            }
-            const double thr = cp.fraction * (double)mx;
-            uint32_t need = 0;
-            if (thr > 0.0) need = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
-#pragma unroll
-            for (int sl = 0; sl < TS; ++sl) {
-                const uint32_t cnt = ev[sl] & 0xFFu;
-                key[sl] = (ev[sl] != EMPTY && cnt >= need) ? ((1023u - cnt) << 22) | (ev[sl] >> 8) : ~0u;
-            }
-            bitonic_sort<TS>(key);
-            uint32_t* ct = cp.cand_tid + r;
-            uint32_t* cs = cp.cand_score + r;
-#pragma unroll
-            for (int d = 0; d < TS; ++d) {
-                if (key[d] != ~0u) {
-                    ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
-                    cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
-                    ++nc;
+                for (int sl = 0; sl < TS; ++sl) {
+                    const uint32_t ev = colbase[sl * WG + ((lane + sl) & 63u)];
+                    if (ev != EMPTY) cp.ktab[((uint64_t)ks * TS + m++) * cp.n + r] = ev;
                 }
+                cp.kcnt[(uint64_t)ks * cp.n + r] = (uint8_t)m;
             }
-            cp.cand_cnt[r] = nc;
-        } else {
-            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+        } else if (live && !FINAL) {
+            cp.kcnt[(uint64_t)ks * cp.n + r] = 0;
+        }
+        if constexpr (FINAL) {
+            // the union over the k slots, in registers: slot s holds tid ut[s] (EMPTY: free) and
+            // its 8-bit counts per k slot uc[s]; this pass's table as it lies (its slots), then the
+            // earlier passes' entries matched by tid or placed in a free slot (src/sparse_chaining.cpp:55-73)
+            const bool merge = hashing && !slow && !listed;
+            if (merge) {
+                uint32_t ut[TS], uc[TS];
+#pragma unroll
+                for (int sl = 0; sl < TS; ++sl) {
+                    const uint32_t ev = colbase[sl * WG + ((lane + sl) & 63u)];
+                    ut[sl] = ev != EMPTY ? ev >> 8 : EMPTY;
+                    uc[sl] = ev != EMPTY ? (ev & 0xFFu) << (8 * ks) : 0u;
+                }
+                bool full = false;
+                // the earlier passes' entry counts, then their entries 8 per k slot at a time, all of
+                // a batch's loads in flight together
+                uint32_t mk[NK_FAST - 1];
+#pragma unroll
+                for (int i = 0; i < NK_FAST - 1; ++i) mk[i] = (uint32_t)i < ks ? cp.kcnt[(uint64_t)i * cp.n + r] : 0u;
+                for (uint32_t j0 = 0; j0 < (uint32_t)TS; j0 += 8) {
+                    bool more = false;
+#pragma unroll
+                    for (int i = 0; i < NK_FAST - 1; ++i) more |= j0 < mk[i];
+                    if (!__any(more)) break;
+                    uint32_t eb[NK_FAST - 1][8];
+#pragma unroll
+                    for (int i = 0; i < NK_FAST - 1; ++i)
+#pragma unroll
+                        for (int u = 0; u < 8; ++u)
+                            eb[i][u] = j0 + u < mk[i] ? cp.ktab[((uint64_t)i * TS + j0 + u) * cp.n + r] : EMPTY;
+#pragma unroll
+                    for (int i = 0; i < NK_FAST - 1; ++i)
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t e = eb[i][u];
+                        if (e == EMPTY) continue;
+                        const uint32_t x = e >> 8, inc = (e & 0xFFu) << (8 * i);
+                        bool found = false;
+#pragma unroll
+                        for (int sl = 0; sl < TS; ++sl) {
+                            const bool h = ut[sl] == x;
+                            uc[sl] += h ? inc : 0u;
+                            found |= h;
+                        }
+                        bool placed = found;
+#pragma unroll
+                        for (int sl = 0; sl < TS; ++sl) {
+                            const bool f = !placed && ut[sl] == EMPTY;
+                            ut[sl] = f ? x : ut[sl];
+                            uc[sl] = f ? inc : uc[sl];
+                            placed |= f;
+                        }
+                        full |= !placed;
+                    }
+                }
+                if (full) {  // more than TS transcripts over the k slots
+                    list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+                    p.pflag[r] = 1;
+                    cp.cand_cnt[r] = 0;
+                } else {
+                    // filter at every k slot (src/sparse_chaining.cpp:76-101), as Counter::finish
+                    const uint32_t nk = p.nk;
+                    uint32_t need4 = 0;  // 8-bit needed count per k slot (256: none passes)
+                    bool none[NK_FAST] = {};
+#pragma unroll
+                    for (int i = 0; i < NK_FAST; ++i) {
+                        uint32_t mx = 0;
+#pragma unroll
+                        for (int sl = 0; sl < TS; ++sl) mx = max(mx, ut[sl] != EMPTY ? (uc[sl] >> (8 * i)) & 0xFFu : 0u);
+                        const double thr = cp.fraction * (double)mx;
+                        uint32_t ti = 0;
+                        if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+                        none[i] = (uint32_t)i < nk && ti > 255u;
+                        need4 |= ((uint32_t)i < nk ? min(ti, 255u) : 0u) << (8 * i);
+                    }
+#pragma unroll
+                    for (int sl = 0; sl < TS; ++sl) {
+                        bool ok = ut[sl] != EMPTY;
+                        uint32_t score = 0;
+#pragma unroll
+                        for (int i = 0; i < NK_FAST; ++i) {
+                            const uint32_t ci = (uc[sl] >> (8 * i)) & 0xFFu;
+                            ok &= ci >= ((need4 >> (8 * i)) & 0xFFu) && !none[i];
+                            score += ci;
+                        }
+                        // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
+                        key[sl] = ok ? ((1023u - score) << 22) | ut[sl] : ~0u;
+                    }
+                    bitonic_sort<TS>(key);
+                    uint32_t* ct = cp.cand_tid + r;
+                    uint32_t* cs = cp.cand_score + r;
+#pragma unroll
+                    for (int d = 0; d < TS; ++d) {
+                        if (key[d] != ~0u) {
+                            ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
+                            cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                            ++nc;
+                        }
+                    }
+                    cp.cand_cnt[r] = nc;
+                }
+            } else if (live) {
+                cp.cand_cnt[r] = 0;
+            }
+        }
+    } else {
+        if (act) {
+            if (s_flag[lane] == 0) {
+                // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
+                uint32_t ev[TS];
+                uint32_t mx = 0;
+#pragma unroll
+                for (int sl = 0; sl < TS; ++sl) {
+                    ev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
+                    mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
+                }
+                const double thr = cp.fraction * (double)mx;
+                uint32_t need = 0;
+                if (thr > 0.0) need = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
+#pragma unroll
+                for (int sl = 0; sl < TS; ++sl) {
+                    const uint32_t cnt = ev[sl] & 0xFFu;
+                    key[sl] = (ev[sl] != EMPTY && cnt >= need) ? ((1023u - cnt) << 22) | (ev[sl] >> 8) : ~0u;
+                }
+                bitonic_sort<TS>(key);
+                uint32_t* ct = cp.cand_tid + r;
+                uint32_t* cs = cp.cand_score + r;
+#pragma unroll
+                for (int d = 0; d < TS; ++d) {
+                    if (key[d] != ~0u) {
+                        ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
+                        cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                        ++nc;
+                    }
+                }
+                cp.cand_cnt[r] = nc;
+            } else {
+                list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
+                cp.cand_cnt[r] = 0;
+            }
+        } else if (live) {
             cp.cand_cnt[r] = 0;
         }
-    } else if (live) {
-        cp.cand_cnt[r] = 0;
     }
     MAP1_STAMP(4);
     // (bin_candidates places entries only after its barriers, when every wave's count tables
@@ -2461,234 +2603,6 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(5);
 }
 
-// Fused map kernel for 2..4 k slots over wide tables (the multi-k quant path): k_map1's staging
-// and validity, the ntHash roll of every k slot (each sorted retained set written out as k_sketch
-// writes it), then wide_count_wave over those sets (read back while they are still in L2) and the
-// binning epilogue, so the gathers of some waves overlap the hashing of others. LDS: the roll
-// terms; per wave the staged codes (the count phase's hash list once every lane has hashed);
-// max(HCAP + 1, 2 * TS) rows of WG words (the bad-chunk bits in row 0 of the wave's columns,
-// then the raw windows, then the count tables); per-read overflow flags; the binning counts.
-__host__ __device__ inline size_t mapk_wave_bytes(uint32_t wc) {
-    const size_t a = sketch_codes_bytes(wc), b = (size_t)128 * 5;  // >= 128 list entries a pass
-    return ((a > b ? a : b) + 15) & ~(size_t)15;
-}
-
-__host__ __device__ constexpr uint32_t mapk_rows(uint32_t hcap) { return hcap + 1 > 2 * TS ? hcap + 1 : 2 * TS; }
-
-size_t mapk_lds_bytes(uint32_t nk, uint32_t wave_chunks, uint32_t hcap) {
-    return sketch_tab_bytes(nk) + (WG / 64) * mapk_wave_bytes(wave_chunks) + (size_t)mapk_rows(hcap) * WG * 4 +
-           (size_t)WG * 4 + (size_t)(WG + 1) * 4;
-}
-
-template <int NK, int HCAP, bool CMP>
-__global__ __launch_bounds__(WG) void k_mapk(SketchParams p, ChainParams cp) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wv = tid >> 6;
-    const uint32_t wc = p.tile_chunks;  // chunks per wave
-    const size_t wave_bytes = mapk_wave_bytes(wc);
-    uint2* s_tab = reinterpret_cast<uint2*>(smem);
-    const uint2* s_seed = s_tab + NK * 16;
-    unsigned char* s_wave = smem + sketch_tab_bytes(NK) + wv * wave_bytes;
-    uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
-    uint32_t* s_rows = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(NK) + (WG / 64) * wave_bytes);
-    uint32_t* s_flag = s_rows + mapk_rows(HCAP) * WG;
-    uint32_t* s_bc = s_flag + WG;
-    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_rows + wv * 64);  // (row 0 of the wave's columns)
-    const bool bin = cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
-    MAP1_STAMP(0);
-    for (uint32_t e = tid; e < NK * 16 + 4; e += WG) {
-        const uint64_t v = p.rolltab[e];
-        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
-    }
-    s_flag[tid] = 0;
-    s_bc[tid] = 0;
-    __syncthreads();
-
-    const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
-    const uint32_t nr = r0 < p.n ? (uint32_t)min((uint64_t)64, p.n - r0) : 0u;  // wave-uniform
-    const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
-    const uintptr_t abase = base & ~(uintptr_t)15;
-    const uint64_t delta = base - abase;
-    uint64_t c0 = 0;
-    uint32_t nch = 0;
-    if (nr) {
-        uint64_t s0, l0, sl, ll;
-        read_extent(p.offs, p.fixed_len, r0, s0, l0);
-        read_extent(p.offs, p.fixed_len, r0 + nr - 1, sl, ll);
-        c0 = (s0 + delta) >> 4;
-        const uint64_t c1 = (sl + ll + delta + 15) >> 4;
-        nch = (uint32_t)min((uint64_t)wc, c1 - c0);
-        const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
-        constexpr uint32_t SU = 10;
-        for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
-            uint4 vv[SU];
-#pragma unroll
-            for (uint32_t u = 0; u < SU; ++u) {  // (non-temporal, as k_map1)
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + min(cb + u * 64, nch - 1)));
-                vv[u] = make_uint4(x.x, x.y, x.z, x.w);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < SU; ++u) {
-                const uint32_t c = cb + u * 64;
-                const uint4 v = vv[u];
-                const uint32_t cs = c < nch ? c : wc + 1;
-                const uint32_t ta = (v.x >> 1) & 0x03030303u, tb = (v.y >> 1) & 0x03030303u;
-                const uint32_t tc = (v.z >> 1) & 0x03030303u, td = (v.w >> 1) & 0x03030303u;
-                constexpr uint32_t W4 = 0x40100401u;
-                const uint32_t code = __builtin_amdgcn_udot4(ta, W4, 0u, false) |
-                                      (__builtin_amdgcn_udot4(tb, W4, 0u, false) << 8) |
-                                      (__builtin_amdgcn_udot4(tc, W4, 0u, false) << 16) |
-                                      (__builtin_amdgcn_udot4(td, W4, 0u, false) << 24);
-                constexpr uint32_t GTCA = 0x47544341u;
-                const uint32_t x = (__builtin_amdgcn_perm(0u, GTCA, ta) ^ v.x) | (__builtin_amdgcn_perm(0u, GTCA, tb) ^ v.y) |
-                                   (__builtin_amdgcn_perm(0u, GTCA, tc) ^ v.z) | (__builtin_amdgcn_perm(0u, GTCA, td) ^ v.w);
-                s_codes[cs] = code;
-                const uint64_t wbits = __ballot(x != 0);
-                if (lane == 0 && c < nch) s_badw[c >> 6] = wbits;
-            }
-        }
-        if (lane == 0) s_codes[nch] = 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    MAP1_STAMP(1);
-    const bool live = lane < nr;
-    const uint64_t r = live ? r0 + lane : 0;
-    uint64_t start = 0, len = 0;
-    if (live) read_extent(p.offs, p.fixed_len, r, start, len);
-    const uint64_t q0 = start + delta - c0 * 16;
-    bool slow = live && (len > (uint64_t)LFAST || q0 + len > (uint64_t)nch * 16);
-    uint8_t st = SKQ_READ_OK;
-    if (live && !slow) {
-        // is_valid_sequence (src/data_io.cpp:17-34), as in k_sketch
-        bool bad = false;
-        if (len) {
-            const uint32_t ca = (uint32_t)(q0 >> 4), cz = (uint32_t)((q0 + len - 1) >> 4);
-            for (uint32_t wd = ca >> 6; wd <= (cz >> 6); ++wd) {
-                uint64_t m = s_badw[wd];
-                const uint32_t lo = wd == (ca >> 6) ? (ca & 63) : 0u, hi = wd == (cz >> 6) ? (cz & 63) : 63u;
-                m &= (hi == 63 ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
-                bad |= m != 0;
-            }
-            if (bad) {
-                bad = false;
-                const uint8_t* rb = p.reads + start;
-                for (uint64_t q = 0; q < len; ++q) {
-                    const uint8_t ch = rb[q];
-                    bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
-                }
-            }
-        }
-        if (bad) st = SKQ_READ_INVALID;
-        else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
-    }
-
-    uint32_t cnts[NK];
-#pragma unroll
-    for (int i = 0; i < NK; ++i) cnts[i] = 0;
-    const bool hashing = live && !slow && st == SKQ_READ_OK;
-    if (hashing) {
-        const uint32_t T = p.threshold;
-        const uint32_t L = (uint32_t)len;
-        auto codes16 = [&](uint32_t q) -> uint32_t {
-            const uint32_t d = q >> 4;
-            return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
-        };
-        uint32_t* raw = s_rows + tid;
-#pragma unroll 1
-        for (int i = 0; i < NK; ++i) {
-            const uint32_t k = p.ks[i];
-            const uint2* tab = s_tab + i * 16;
-            uint32_t hlo = 0, hhi = 0;
-            for (uint32_t b = 0; b < k; b += 16) {
-                const uint32_t w = codes16((uint32_t)q0 + b);
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (b + j < k) roll33b(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
-            }
-            raw[0] = hlo;
-            uint32_t nraw = hlo <= T ? 1u : 0u;  // src/sketch.cpp:33-35
-            const uint32_t nw = L - k + 1;
-            const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
-            for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
-                const uint32_t win = codes16(qin + w0 - 1);
-                const uint32_t wout = codes16(qout + w0 - 1);
-                const uint32_t jn = nw - w0;
-                uint2 e[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) e[j] = tab[((win >> (2 * j)) & 3u) * 4 + ((wout >> (2 * j)) & 3u)];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    roll33b(hlo, hhi, e[j]);
-                    const bool rec = hlo <= T && (uint32_t)j < jn;
-                    raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
-                    nraw += rec ? 1u : 0u;
-                }
-            }
-            if (nraw > HCAP) {
-                slow = true;
-                break;
-            }
-            // set semantics: sort, drop repeats; SoA rows as k_sketch writes them
-            uint32_t v[HCAP];
-#pragma unroll
-            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_rows[j * WG + tid] : 0xFFFFFFFFu;
-            bitonic_sort<HCAP>(v);
-            uint32_t* out = p.hashes + (uint64_t)i * p.hcap * p.n + r;
-            uint32_t m = 0;
-#pragma unroll
-            for (int j = 0; j < HCAP; ++j)
-                if ((uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1])) out[(uint64_t)(m++) * p.n] = v[j];
-            p.hash_cnt[(uint64_t)i * p.n + r] = m;
-            cnts[i] = m;
-        }
-    }
-    if (live) {
-        if (slow) {
-            st = ST_SLOW1;
-            list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
-            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
-        } else if (st != SKQ_READ_OK) {
-#pragma unroll
-            for (int i = 0; i < NK; ++i) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
-        }
-        p.status[r] = st;
-        p.pflag[r] = slow ? 1 : 0;  // (a later skq_chain on these results reads it)
-    }
-    const bool act = hashing && !slow;
-    if (!act) {
-#pragma unroll
-        for (int i = 0; i < NK; ++i) cnts[i] = 0;
-    }
-    if (live && !act) cp.cand_cnt[r] = 0;
-    // every lane of the wave has hashed: this wave's columns of the rows become its count tables,
-    // its staged codes the hash list
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int rw = 0; rw < 2 * TS; ++rw) s_rows[rw * WG + tid] = (rw & 1) ? 0u : 0xFFFFFFFFu;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    MAP1_STAMP(2);
-    // list entries a pass: hashes, then owners (then, compact tables, the hashes' slots)
-    const uint32_t cap = (uint32_t)(wave_bytes / (CMP ? 9 : 5)) & ~31u;
-    uint32_t key[TS];
-    const uint32_t nc = wide_count_wave<NK, CMP>(cp, r, r, act, cnts, s_rows + wv * 64, reinterpret_cast<uint32_t*>(s_wave),
-                                                 s_wave + (size_t)cap * 4,
-                                                 reinterpret_cast<uint32_t*>(s_wave + (size_t)cap * 5), cap,
-                                                 s_flag + wv * 64, lane, key);
-    MAP1_STAMP(3);
-    MAP1_STAMP(4);
-    // (bin_candidates places entries only after its barriers, when every wave's tables are dead)
-    if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_rows);
-    MAP1_STAMP(5);
-}
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
 // LDS (global scratch beyond SLOW_CAP), sorted, and counted per transcript run.
@@ -3458,8 +3372,9 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
     if (cp.n == 0) return 0;
     if (cp.wide != 1 && cp.wide != 3) return -4;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // a 64-lane workgroup per listed read, grid-stride (the list length is on the device)
-    const dim3 grid(2048), blk(64);
+    // a 64-lane workgroup per listed read, grid-stride (the list length is on the device); 16
+    // per CU fit (LDS ~9 KB, < 100 VGPRs)
+    const dim3 grid(4096), blk(64);
     const bool cmp = cp.wide == 3;
     switch (cp.nk) {
     case 1:
@@ -3551,32 +3466,27 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_mapk(const SketchParams& p, const ChainParams& cp, void* stream) {
+int launch_map1_pass(const SketchParams& p, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
     if (p.n == 0) return 0;
-    if (p.hcap != 16 && p.hcap != 32) return -4;
+    if ((cp.wide != 1 && cp.wide != 3) || cap > p.hcap) return -4;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    const size_t lds = mapk_lds_bytes(p.nk, p.tile_chunks, p.hcap);
-    if (lds > 160 * 1024) return -4;
+    const size_t lds = map1_lds_bytes(p.tile_chunks, cap);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    auto go = [&](auto kern) {
-        if (lds > 64 * 1024)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-        hipLaunchKernelGGL(kern, grid, dim3(WG), lds, st, p, cp);
-    };
-    if (cp.wide != 1 && cp.wide != 3) return -4;
-    const bool cmp = cp.wide == 3;
-    switch (p.nk * 100 + p.hcap) {
-    case 216: cmp ? go(k_mapk<2, 16, true>) : go(k_mapk<2, 16, false>); break;
-    case 316: cmp ? go(k_mapk<3, 16, true>) : go(k_mapk<3, 16, false>); break;
-    case 416: cmp ? go(k_mapk<4, 16, true>) : go(k_mapk<4, 16, false>); break;
-    case 232: cmp ? go(k_mapk<2, 32, true>) : go(k_mapk<2, 32, false>); break;
-    case 332: cmp ? go(k_mapk<3, 32, true>) : go(k_mapk<3, 32, false>); break;
-    case 432: cmp ? go(k_mapk<4, 32, true>) : go(k_mapk<4, 32, false>); break;
+    switch (cap * 8 + (cp.wide == 3 ? 2 : 0) + (final_pass ? 1 : 0)) {
+    case 128: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;
+    case 129: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 130: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false>), grid, dim3(WG), lds, st, p, cp); break;
+    case 131: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 256: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;
+    case 257: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 258: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false>), grid, dim3(WG), lds, st, p, cp); break;
+    case 259: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+
 
 int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
                         uint64_t n, void* stream) {

@@ -482,7 +482,7 @@ def test_very_long_reads_and_large_postings():
 
 @pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
 def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
-    """With wide or compact tables, 2-4 k slots map through the fused k_mapk (no separate count launch);
+    """With wide or compact tables, 2-4 k slots map through the k_map1 passes (no separate count launch);
     every other probe structure through k_sketch + a count kernel. Both bit-exact."""
     gi, oi = build(ks, tx=tx300)
     bases, _, _ = synth.reads(tx300, 2000, read_len, seed=77, err=0.002)
