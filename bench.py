@@ -18,7 +18,9 @@ sharded (each rank its own seeded batch), the index is replicated; rank 0 prints
 After the timed steps (rank 0): the parity sample — the first --cpu-reads reads of the batch as
 FASTQ text through the CPU oracle (oracle/oracle.c, the checker), compared bit-exact with the GPU's
 statuses, retained-hash sets, candidate lists and per-transcript totals for the same reads; a
-mismatch exits non-zero. At N = 1 the same oracle runs are the CPU baseline (P threads and 1).
+mismatch exits non-zero. At N = 1 the same oracle runs are the CPU baseline (P threads and 1),
+and `end_to_end` reports quant as the CLI runs it (FASTQ file -> device parse -> sketch + chain ->
+EM + assignment) over the same batch, checked against the in-HBM map's totals; never `value`.
 """
 import argparse
 import os
@@ -39,6 +41,8 @@ def _args(argv=None):
                     help="parity sample / CPU-baseline sample (reads; N > 1: capped at 200k)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the 1-thread CPU timing")
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="skip the FASTQ-file -> EM leg reported beside the kernel path (N = 1)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -153,6 +157,71 @@ def parity_check(gpu, gtot, cpu, nk):
     if not (np.array_equal(gtot[0], cpu["tx_reads"]) and np.array_equal(gtot[1], cpu["tx_score"])):
         bad.append("per-transcript totals differ")
     return bad
+
+
+def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
+    """quant as the CLI runs it, beside the kernel-path metric (never `value`): the batch's reads
+    as a FASTQ file in the page cache -> pulled into pinned buffers -> records parsed on the
+    device -> sketch + chain -> candidates appended on the device -> EM (<= 20 rounds) +
+    assignment. One warm-up pass, then one timed pass. Check: the ingest path's per-transcript
+    totals equal those of the in-HBM map of the same reads, and every read is kept."""
+    import tempfile
+    fd, path = tempfile.mkstemp(suffix=".fq")
+    try:
+        size = 0
+        with os.fdopen(fd, "wb") as f:
+            for a in range(0, n, 1_000_000):
+                m = min(1_000_000, n - a)
+                buf = synth.fastq_bytes(bases[a * L:(a + m) * L], L, first=a)
+                size += buf.size
+                f.write(buf.tobytes())
+        with open(path, "rb") as f:  # page cache
+            while f.read(1 << 28):
+                pass
+        es = skq.Session(index, batch, 256)
+        emr = {}
+
+        def run():
+            g = skq.Ingest(es, path, chunk_bytes=64 << 20, io_threads=8)
+            em = skq.EMSet(ntx)
+            tot = 0
+            while True:
+                _, got = g.map(accumulate=True)
+                if got == 0:
+                    break
+                tot += got
+                em.add_session(es)
+            es.check()
+            kept = g.finish()
+            g.close()
+            t1 = time.perf_counter()
+            em.select(kept)
+            _, it = em.run(20, 0.01)
+            _, assigned = em.assign()
+            emr.update(em_ms=(time.perf_counter() - t1) * 1e3, em_rounds=it, assigned_transcripts=int(assigned.sum()))
+            em.free()
+            return tot, int(kept.sum())
+
+        run()
+        es.reset_totals()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        got, kept = run()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - ts
+        etot = es.totals()
+        es.free()
+        sess.reset_totals(sp)
+        sess.map(d_ptr, None, n, L, fixed_len=L, stream=sp, accumulate=True)
+        sess.check(sp)
+        dtot = sess.totals()
+        ok = got == n and kept == n and np.array_equal(etot[0], dtot[0]) and np.array_equal(etot[1], dtot[1])
+        return dict(what="quant end to end on 1 GPU: FASTQ file (page cache) -> device parse -> sketch + chain "
+                        "-> EM + assignment (the CLI's path; not the metric)",
+                   reads=got, fastq_GB=size / 1e9, seconds=dt, reads_per_s=got / dt,
+                   check="totals equal the in-HBM map's, all reads kept" if ok else "MISMATCH", **emr)
+    finally:
+        os.unlink(path)
 
 
 def cpu_model():
@@ -316,6 +385,10 @@ def main(args):
             cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
             if os.path.exists(cal):  # reference sparse_chain vs the oracle's, timed in the build container
                 cpu["calibration"] = json.load(open(cal)).get("summary")
+    e2e = None
+    if world == 1 and not args.no_end_to_end:
+        e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp)
+        log("end to end: %s" % json.dumps(e2e))
     if world > 1:
         dist.barrier()
 
@@ -341,12 +414,15 @@ def main(args):
                      "slow_reads_per_batch": {"sketch": slow[0], "chain": slow[1]}},
             "parity_sample": parity,
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
         }
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
     if parity is not None and parity.startswith("MISMATCH"):
         raise SystemExit(3)
+    if e2e is not None and e2e["check"] == "MISMATCH":
+        raise SystemExit(4)
 
 
 if __name__ == "__main__":

@@ -6,4 +6,4 @@ root=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$root"
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_stats -o run \
-  -- python3 bench.py --no-cpu-baseline --cpu-reads 200000 "$@" > gpurun_out/${tag}_stats.json 2> gpurun_out/${tag}_stats.err
+  -- python3 bench.py --no-cpu-baseline --no-end-to-end --cpu-reads 200000 "$@" > gpurun_out/${tag}_stats.json 2> gpurun_out/${tag}_stats.err

@@ -20,6 +20,7 @@ cfg, fdir, wdir, out = sys.argv[1:5]
 
 def per_read(d, counter):
     rows = collections.defaultdict(dict)
+    full = {}  # dispatch -> full kernel name (template arguments included)
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] != counter:
@@ -29,11 +30,30 @@ def per_read(d, counter):
             grid = int(row["Grid_Size"]) if "Grid_Size" in row else int(row["Grid_Size_X"])
             r = rows[name].setdefault(did, [grid, 0.0])
             r[1] += float(row["Counter_Value"])
+            full[did] = row["Kernel_Name"].split("(")[0]
     res = {}
     for name, ds in rows.items():
         gmax = max(g for g, _ in ds.values())
         vals = [v / g for g, v in ds.values() if g == gmax]
         res[name] = (statistics.median(vals), len(vals), gmax)
+    # several k slots: one k_map1 launch per k slot (template PASS = true), the last one FINAL;
+    # a step's map is the run of full-size pass dispatches ending in a final one, summed
+    # (bench.py names it "k_map1 xN passes")
+    ds = rows.get("k_map1", {})
+    if ds:
+        gmax = max(g for g, _ in ds.values())
+        groups, cur = collections.defaultdict(list), []
+        for did in sorted(ds):
+            g, v = ds[did]
+            targs = full[did].split("<", 1)[1].rstrip(">").replace(" ", "").split(",") if "<" in full[did] else []
+            if g != gmax or len(targs) < 5 or targs[3] != "true":
+                continue
+            cur.append(v / g)
+            if targs[4] == "true":
+                groups[len(cur)].append(sum(cur))
+                cur = []
+        for npass, vals in groups.items():
+            res["k_map1 x%d passes" % npass] = (statistics.median(vals), len(vals), gmax)
     return res
 
 
