@@ -1086,7 +1086,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     if (s->idx->nk > 1 && !s->ktab) {  // the per-k tables of the multi-k passes
         DeviceGuard g(s->idx->device);
         if (int rc = dev_alloc(&s->ktab, (uint64_t)s->idx->nk * skq::DCAP * s->max_reads)) return rc;
-        if (int rc = dev_alloc(&s->kcnt, (uint64_t)s->idx->nk * s->max_reads)) return rc;
+        if (int rc = dev_alloc(&s->kcnt, 2ull * s->idx->nk * s->max_reads)) return rc;  // counts, needs
     }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,

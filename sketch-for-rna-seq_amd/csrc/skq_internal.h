@@ -144,9 +144,10 @@ struct ChainParams {
     uint32_t* bin_region;
     int slow_totals;
     uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
-    // multi-k map by passes (k_map1 pass mode; the final pass merges): per k slot i and read r, the read's
-    // count table at that k, unfiltered: kcnt[i * n + r] entries (tid << 8 | count) at
-    // ktab[(i * TS + j) * n + r]
+    // multi-k map by passes (k_map1 pass mode; the final pass merges): per k slot i and read r, the
+    // entries of the read's count table at that k that meet that k's need (tid << 8 | count):
+    // kcnt[i * n + r] of them at ktab[(i * TS + j) * n + r], and the need itself (min(ceil(fraction
+    // * max), 255); 0: the k slot does not filter) at kcnt[(nk + i) * n + r]
     uint32_t* ktab;
     uint8_t* kcnt;
     // wide direct tables (DESIGN.md "Index"): entry h of k slot i is 8 words at wdir[i] + 8h,

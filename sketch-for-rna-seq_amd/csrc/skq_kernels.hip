@@ -1976,11 +1976,13 @@ size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
     } while (0)
 
 // TAB: 0 = wide tables, 1 = block tables, 2 = compact tables. PASS: one k slot (p.kslot) of a
-// multi-k map: the read's count table at that k goes out unfiltered to cp.ktab / cp.kcnt, with
-// no candidates or binning; a read any pass lists for the slow path is listed once (pflag), and
-// a read an earlier pass found sketch-slow is skipped. FINAL (the last k slot's pass): the
-// earlier passes' tables are merged in registers with this pass's, then filtered, ordered,
-// written and binned as in the one-k map.
+// multi-k map: the entries of the read's count table at that k that meet that k's need go out to
+// cp.ktab / cp.kcnt with the need (a transcript short of one k slot's need fails the multi-k
+// filter whatever the other k slots hold), with no candidates or binning; a read any pass lists
+// for the slow path is listed once (pflag), and a read an earlier pass found sketch-slow is
+// skipped. FINAL (the last k slot's pass): the earlier passes' entries are merged in registers with
+// this pass's table (matched only, when this k slot filters), then filtered, ordered, written and
+// binned as in the one-k map.
 template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     constexpr bool BLK = TAB == 1, CMP = TAB == 2;
@@ -2432,45 +2434,67 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(3);
     uint32_t key[TS];
     uint32_t nc = 0;
+    // the need at one k slot from its largest count (src/sparse_chaining.cpp:93: c >= fraction * max
+    // as the integer c >= ceil(fraction * max); 256: none passes; 0: all pass)
+    auto need_of = [&](uint32_t mx) -> uint32_t {
+        const double thr = cp.fraction * (double)mx;
+        return thr > 0.0 ? (thr >= 256.0 ? 256u : (uint32_t)ceil(thr)) : 0u;
+    };
     if constexpr (PASS) {
         bool listed = pf_prev != 0;  // listed for the slow path by this or an earlier pass
+        uint8_t* kneed = cp.kcnt + (uint64_t)p.nk * cp.n;
         if (act) {
             if (s_flag[lane] != 0) {  // more than TS transcripts at this k: the slow chain path
                 if (!listed) list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
                 p.pflag[r] = 1;
                 listed = true;
                 if (!FINAL) cp.kcnt[(uint64_t)ks * cp.n + r] = 0;
-            } else if (!FINAL) {  // the read's table at this k, unfiltered, front-packed
-                uint32_t m = 0;
+            } else if (!FINAL) {  // the entries meeting this k slot's need, front-packed, and the need
+                uint32_t ev[TS], mx = 0;
 #pragma unroll
                 for (int sl = 0; sl < TS; ++sl) {
-                    const uint32_t ev = colbase[sl * WG + ((lane + sl) & 63u)];
-                    if (ev != EMPTY) cp.ktab[((uint64_t)ks * TS + m++) * cp.n + r] = ev;
+                    ev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
+                    mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
                 }
+                const uint32_t need = need_of(mx);
+                uint32_t m = 0;
+#pragma unroll
+                for (int sl = 0; sl < TS; ++sl)
+                    if (ev[sl] != EMPTY && (ev[sl] & 0xFFu) >= need) cp.ktab[((uint64_t)ks * TS + m++) * cp.n + r] = ev[sl];
                 cp.kcnt[(uint64_t)ks * cp.n + r] = (uint8_t)m;
+                kneed[(uint64_t)ks * cp.n + r] = (uint8_t)min(need, 255u);
             }
-        } else if (live && !FINAL) {
+        } else if (live && !FINAL) {  // (a k slot the index lacks does not filter)
             cp.kcnt[(uint64_t)ks * cp.n + r] = 0;
+            kneed[(uint64_t)ks * cp.n + r] = 0;
         }
         if constexpr (FINAL) {
-            // the union over the k slots, in registers: slot s holds tid ut[s] (EMPTY: free) and
-            // its 8-bit counts per k slot uc[s]; this pass's table as it lies (its slots), then the
-            // earlier passes' entries matched by tid or placed in a free slot (src/sparse_chaining.cpp:55-73)
+            // the transcripts over the k slots, in registers: slot s holds tid ut[s] (EMPTY: free)
+            // and its 8-bit counts per k slot uc[s]; this pass's table as it lies (its slots), then
+            // the earlier passes' entries matched by tid — or, when this k slot does not filter
+            // (need 0), placed in a free slot (src/sparse_chaining.cpp:55-73)
             const bool merge = hashing && !slow && !listed;
             if (merge) {
-                uint32_t ut[TS], uc[TS];
+                uint32_t ut[TS], uc[TS], mxf = 0;
 #pragma unroll
                 for (int sl = 0; sl < TS; ++sl) {
                     const uint32_t ev = colbase[sl * WG + ((lane + sl) & 63u)];
                     ut[sl] = ev != EMPTY ? ev >> 8 : EMPTY;
                     uc[sl] = ev != EMPTY ? (ev & 0xFFu) << (8 * ks) : 0u;
+                    mxf = max(mxf, ev != EMPTY ? ev & 0xFFu : 0u);
                 }
+                const uint32_t needf = need_of(mxf);
+                const bool inter = needf > 0;  // only this k slot's transcripts can pass
                 bool full = false;
-                // the earlier passes' entry counts, then their entries 8 per k slot at a time, all of
-                // a batch's loads in flight together
-                uint32_t mk[NK_FAST - 1];
+                // the earlier passes' entry counts and needs, then their entries 8 per k slot at a
+                // time, all of a batch's loads in flight together
+                const uint8_t* kneed = cp.kcnt + (uint64_t)p.nk * cp.n;
+                uint32_t mk[NK_FAST - 1], nd[NK_FAST - 1];
 #pragma unroll
-                for (int i = 0; i < NK_FAST - 1; ++i) mk[i] = (uint32_t)i < ks ? cp.kcnt[(uint64_t)i * cp.n + r] : 0u;
+                for (int i = 0; i < NK_FAST - 1; ++i) {
+                    mk[i] = (uint32_t)i < ks ? cp.kcnt[(uint64_t)i * cp.n + r] : 0u;
+                    nd[i] = (uint32_t)i < ks ? kneed[(uint64_t)i * cp.n + r] : 0u;
+                }
                 for (uint32_t j0 = 0; j0 < (uint32_t)TS; j0 += 8) {
                     bool more = false;
 #pragma unroll
@@ -2496,15 +2520,17 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                             uc[sl] += h ? inc : 0u;
                             found |= h;
                         }
-                        bool placed = found;
+                        if (!found && !inter) {
+                            bool placed = false;
 #pragma unroll
-                        for (int sl = 0; sl < TS; ++sl) {
-                            const bool f = !placed && ut[sl] == EMPTY;
-                            ut[sl] = f ? x : ut[sl];
-                            uc[sl] = f ? inc : uc[sl];
-                            placed |= f;
+                            for (int sl = 0; sl < TS; ++sl) {
+                                const bool f = !placed && ut[sl] == EMPTY;
+                                ut[sl] = f ? x : ut[sl];
+                                uc[sl] = f ? inc : uc[sl];
+                                placed |= f;
+                            }
+                            full |= !placed;
                         }
-                        full |= !placed;
                     }
                 }
                 if (full) {  // more than TS transcripts over the k slots
@@ -2512,21 +2538,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     p.pflag[r] = 1;
                     cp.cand_cnt[r] = 0;
                 } else {
-                    // filter at every k slot (src/sparse_chaining.cpp:76-101), as Counter::finish
-                    const uint32_t nk = p.nk;
-                    uint32_t need4 = 0;  // 8-bit needed count per k slot (256: none passes)
-                    bool none[NK_FAST] = {};
+                    // filter at every k slot (src/sparse_chaining.cpp:76-101), as Counter::finish: the
+                    // earlier k slots' needs as their passes found them, this one's from its table
+                    // (counts <= 32 here, so a need of 255 passes nothing)
+                    uint32_t need4 = min(needf, 255u) << (8 * ks);
+                    const bool nonef = needf > 255u;
 #pragma unroll
-                    for (int i = 0; i < NK_FAST; ++i) {
-                        uint32_t mx = 0;
-#pragma unroll
-                        for (int sl = 0; sl < TS; ++sl) mx = max(mx, ut[sl] != EMPTY ? (uc[sl] >> (8 * i)) & 0xFFu : 0u);
-                        const double thr = cp.fraction * (double)mx;
-                        uint32_t ti = 0;
-                        if (thr > 0.0) ti = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
-                        none[i] = (uint32_t)i < nk && ti > 255u;
-                        need4 |= ((uint32_t)i < nk ? min(ti, 255u) : 0u) << (8 * i);
-                    }
+                    for (int i = 0; i < NK_FAST - 1; ++i) need4 |= nd[i] << (8 * i);
 #pragma unroll
                     for (int sl = 0; sl < TS; ++sl) {
                         bool ok = ut[sl] != EMPTY;
@@ -2534,7 +2552,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
                         for (int i = 0; i < NK_FAST; ++i) {
                             const uint32_t ci = (uc[sl] >> (8 * i)) & 0xFFu;
-                            ok &= ci >= ((need4 >> (8 * i)) & 0xFFu) && !none[i];
+                            ok &= ci >= ((need4 >> (8 * i)) & 0xFFu) && !nonef;
                             score += ci;
                         }
                         // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
