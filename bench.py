@@ -387,7 +387,10 @@ def main(args):
                 cpu["calibration"] = json.load(open(cal)).get("summary")
     e2e = None
     if world == 1 and not args.no_end_to_end:
-        e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp)
+        try:
+            e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp)
+        except (OSError, skq.SkqError) as ex:  # (e.g. no room for the FASTQ file): the metric line still prints
+            e2e = {"error": "%s: %s" % (type(ex).__name__, ex)}
         log("end to end: %s" % json.dumps(e2e))
     if world > 1:
         dist.barrier()
@@ -421,7 +424,7 @@ def main(args):
         dist.destroy_process_group()
     if parity is not None and parity.startswith("MISMATCH"):
         raise SystemExit(3)
-    if e2e is not None and e2e["check"] == "MISMATCH":
+    if e2e is not None and e2e.get("check") == "MISMATCH":
         raise SystemExit(4)
 
 
