@@ -921,14 +921,14 @@ static int wait_totals(skq_session* s, hipStream_t st) {
 
 // The tail of a chain: the slow paths and the per-transcript totals. When the count kernel binned
 // the fast reads' candidates, k_bin_sum only reads those bins and adds into the running totals
-// with atomics (commuting with the slow paths' direct adds). For batches of 4M+ reads it runs on
+// with atomics (commuting with the slow paths' direct adds). For batches of 512k+ reads it runs on
 // the session's side stream and nothing on the launch stream waits for it: it overlaps the slow
 // paths and the next batch's map kernel, which bins into the other buffer (wait_bins).
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
                       hipStream_t st) {
-    // (small batches: the extra stream hand-offs cost more than the overlap gains: 1M reads ran
-    // 12 % faster serial, 10M reads faster forked)
-    const bool fork = accumulate && p.slow_totals && p.n >= (1u << 22);
+    // (small batches: the extra stream hand-offs cost more than the overlap gains; with the
+    // grouped k_bin_sum for few buckets, 1M reads run 5 % faster forked, 10M reads too)
+    const bool fork = accumulate && p.slow_totals && p.n >= (1u << 19);
     hipEvent_t t0{};
     if (fork) {
         if (!s->side) {
