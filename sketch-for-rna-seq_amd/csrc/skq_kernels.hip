@@ -2828,12 +2828,17 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
     __shared__ uint8_t s_seq[SW_NW + 64 + 16];  // the read's bases (len <= SW_NW + min k - 1)
     __shared__ uint32_t s_m[NK], s_flag, s_nc;
     __shared__ unsigned long long s_at;
+    __shared__ uint64_t s_rt[NK * 16 + 4];  // the roll terms per k slot, then the seeds (the rolls
+                                            // below are chains of dependent lookups: LDS, not global)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
     const uint32_t lane = threadIdx.x;
     const uint32_t cnt = min(cp.ctrl[C_OVF2], cp.ovf_cap);
+    if (blockIdx.x >= cnt) return;  // (uniform) nothing listed for this workgroup
     unsigned long long* bump_h = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(cp.ctrl + C_BUMP_C);
-    const uint64_t* seed = p.rolltab + p.nk * 16;
+    for (uint32_t e = lane; e < NK * 16 + 4; e += 64) s_rt[e] = p.rolltab[e];
+    wave_sync();
+    const uint64_t* seed = s_rt + NK * 16;
     const uint64_t n = cp.n;
     for (uint32_t jr = blockIdx.x; jr < cnt; jr += gridDim.x) {
         const uint32_t r = cp.ovf2[jr];
@@ -2888,7 +2893,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                     uint32_t got[SW_NW / 64];
                     uint32_t keepb = 0;  // bit u: window wa + u is retained
                     if (wa < wb) {
-                        const uint64_t* tab = p.rolltab + i * 16;
+                        const uint64_t* tab = s_rt + i * 16;
                         uint32_t hlo = 0, hhi = 0;
                         for (uint32_t q = 0; q < k; ++q) roll33(hlo, hhi, seed[(sb[wa + q] >> 1) & 3u]);
 #pragma unroll
