@@ -294,7 +294,7 @@ def main(args):
     # (total ms, launches): sketch / fused map, probe, count, totals (k_bin_sum + fold)
     kt = [sess.kernel_time(kind) for kind in range(4)]
     elapsed = sdist.max_over_ranks(elapsed, device=dev)  # the slowest rank's time
-    slow = sess.slow_reads()
+    slow = sess.slow_counts()
 
     # the sample: the first m reads of this rank's batch, mapped alone (fresh totals), exported
     m = min(n, args.cpu_reads if world == 1 else min(args.cpu_reads, 200_000))
@@ -414,7 +414,8 @@ def main(args):
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
                      "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn,
-                     "slow_reads_per_batch": {"sketch": slow[0], "chain": slow[1]}},
+                     "slow_reads_per_batch": {"sketch": slow[0], "chain": slow[1],
+                                              "past_the_wave_path": {"sketch": slow[2], "chain": slow[3]}}},
             "parity_sample": parity,
             "cpu_baseline": cpu,
             "end_to_end": e2e,

@@ -251,6 +251,9 @@ int skq_session_set_stamps(skq_session* s, void* d_stamps);
 int skq_session_kernel_time(skq_session* s, int kind, double* total_ms, uint64_t* launches);
 /* Reads of the last batch that took the slow sketch / slow chain path (synchronous). */
 int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chain_slow);
+/* The same, and (fused map) the reads the wave slow path handed on to the general slow paths:
+ * counts[0..3] = sketch slow, chain slow, then second-level sketch, chain (synchronous). */
+int skq_session_slow_counts(skq_session* s, uint32_t* counts);
 
 #ifdef __cplusplus
 }

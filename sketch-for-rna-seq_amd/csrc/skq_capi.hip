@@ -733,6 +733,18 @@ int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chai
     return 0;
 }
 
+int skq_session_slow_counts(skq_session* s, uint32_t* counts) {
+    if (!s || !counts) return fail(-1, "null argument");
+    DeviceGuard g(s->idx->device);
+    uint32_t c[skq::C_WORDS];
+    HIP_TRY(hipMemcpy(c, s->ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    counts[0] = c[skq::C_OVF1];
+    counts[1] = c[skq::C_OVF2];
+    counts[2] = c[skq::C_OVF3];
+    counts[3] = c[skq::C_OVF4];
+    return 0;
+}
+
 int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? ix->mode : 0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {

@@ -53,6 +53,7 @@ def lib():
             "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
             "skq_index_direct": (i32, [vp]),
             "skq_session_slow_reads": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
+            "skq_session_slow_counts": (i32, [vp, C.POINTER(u32)]),
             "skq_session_create": (i32, [vp, u64, u32, C.POINTER(vp)]),
             "skq_session_free": (i32, [vp]),
             "skq_sketch": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
@@ -302,6 +303,12 @@ class Session:
         a, b = C.c_uint32(), C.c_uint32()
         _check(lib().skq_session_slow_reads(self.h, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    def slow_counts(self):
+        """(sketch slow, chain slow, second-level sketch, second-level chain) reads of the last batch."""
+        c = (C.c_uint32 * 4)()
+        _check(lib().skq_session_slow_counts(self.h, c))
+        return tuple(c)
 
     def kernel_time(self, kind):
         ms, n = C.c_double(), C.c_uint64()
