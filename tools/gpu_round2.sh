@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-t=r2h
+t=r2i
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${t}_tests.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > gpurun_out/${t}_bench.json 2> gpurun_out/${t}_bench.err &&
 bash tools/profile_round.sh ${t} &&
