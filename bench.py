@@ -163,7 +163,7 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
     """quant as the CLI runs it, beside the kernel-path metric (never `value`): the batch's reads
     as a FASTQ file in the page cache -> pulled into pinned buffers -> records parsed on the
     device -> sketch + chain -> candidates appended on the device -> EM (<= 20 rounds) +
-    assignment. One warm-up pass, then one timed pass. Check: the ingest path's per-transcript
+    assignment. One warm-up pass, then three timed passes (the median is reported; the totals of the last are checked). Check: the ingest path's per-transcript
     totals equal those of the in-HBM map of the same reads, and every read is kept."""
     import tempfile
     need = n * (2 * L + 20)  # the FASTQ's bytes (fixed-width ids)
@@ -211,12 +211,15 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
             return tot, int(kept.sum())
 
         run()
-        es.reset_totals()
-        torch.cuda.synchronize()
-        ts = time.perf_counter()
-        got, kept = run()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - ts
+        times = []
+        for _ in range(3):  # three timed passes; the median is reported (boxes' host paths vary)
+            es.reset_totals()
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            got, kept = run()
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - ts)
+        dt = sorted(times)[1]
         etot = es.totals()
         es.free()
         sess.reset_totals(sp)
@@ -226,7 +229,7 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
         ok = got == n and kept == n and np.array_equal(etot[0], dtot[0]) and np.array_equal(etot[1], dtot[1])
         return dict(what="quant end to end on 1 GPU: FASTQ file (in memory: /dev/shm or the page cache) -> device parse -> sketch + chain "
                         "-> EM + assignment (the CLI's path; not the metric)",
-                   reads=got, fastq_GB=size / 1e9, seconds=dt, reads_per_s=got / dt,
+                   reads=got, fastq_GB=size / 1e9, fastq_in="/dev/shm" if tmpdir else "page cache (%s)" % os.path.dirname(path), seconds=dt, reads_per_s=got / dt, pass_reads_per_s=[got / t for t in times],
                    check="totals equal the in-HBM map's, all reads kept" if ok else "MISMATCH", **emr)
     finally:
         os.unlink(path)
