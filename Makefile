@@ -13,15 +13,16 @@ oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
 
 .PHONY: oracle
 
-# the reference's own chain / EM / IO code, test-only (oracle/ref.mk; skipped without /root/reference)
-ref:
-	$(MAKE) -f oracle/ref.mk
+# the reference's own chain / EM / IO code, test-only (oracle/ref.mk; skipped without /root/reference),
+# and the reference's own CLI (src/main.cpp) linked against libskq.so through include/dropin
+ref: $(OUT)/libskq.so
+	$(MAKE) -f oracle/ref.mk all
 .PHONY: ref
 
 HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
 LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o \
             $(OUT)/obj/skq_io.o $(OUT)/obj/skq_ingest.o $(OUT)/obj/skq_em.o \
-            $(OUT)/obj/skq_build.o
+            $(OUT)/obj/skq_build.o $(OUT)/obj/skq_dropin_io.o
 HOST_CXX ?= g++
 HOSTFLAGS := $(CXXFLAGS_COMMON) -pthread
 

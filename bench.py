@@ -39,10 +39,11 @@ def _args(argv=None):
     ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
     ap.add_argument("--cpu-reads", type=int, default=2_000_000,
                     help="parity sample / CPU-baseline sample (reads; N > 1: capped at 200k)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: min(16, cpus))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: min(16, affinity CPUs): the box's CPU share per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the 1-thread CPU timing")
     ap.add_argument("--no-end-to-end", action="store_true",
-                    help="skip the FASTQ-file -> EM leg reported beside the kernel path (N = 1)")
+                    help="skip the FASTQ-file -> EM leg reported beside the kernel path")
     ap.add_argument("--dist-backend", default="nccl",
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -159,39 +160,64 @@ def parity_check(gpu, gtot, cpu, nk):
     return bad
 
 
-def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
-    """quant as the CLI runs it, beside the kernel-path metric (never `value`): the batch's reads
-    as a FASTQ file in the page cache -> pulled into pinned buffers -> records parsed on the
-    device -> sketch + chain -> candidates appended on the device -> EM (<= 20 rounds) +
-    assignment. One warm-up pass, then three timed passes (the median is reported; the totals of the last are checked). Check: the ingest path's per-transcript
-    totals equal those of the in-HBM map of the same reads, and every read is kept."""
+def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, rank=0, world=1, dev=None, batch=2_000_000):
+    """quant as the CLI runs it, beside the kernel-path metric (never `value`): the job's reads as
+    ONE FASTQ file in memory (/dev/shm when there is room, else the page cache; each rank writes
+    its shard's records at its own offset) -> split at line starts into one part per rank
+    (skq_fastq_split) -> each rank pulls its part into pinned buffers, parses the records on its
+    device, sketch + chain, candidates appended on the device -> EM (<= 20 rounds) + assignment:
+    on one GPU skq_em_run; on N GPUs every round's posterior sums all-reduced over RCCL
+    (skq/dist.py em_gpu / assign_gpu, src/main.cpp:165-197). One warm-up pass, then three timed
+    passes (median reported; the slowest rank's time each). Check: the per-transcript totals of
+    the ingest path, summed over ranks, equal those of the in-HBM map of the same reads, and every
+    read is kept."""
     import tempfile
-    need = n * (2 * L + 20)  # the FASTQ's bytes (fixed-width ids)
+    rs = 2 * L + 19                       # one record of synth.fastq_bytes (fixed-width ids)
+    need = world * n * rs
     tmpdir = None
-    try:  # a RAM-backed file when there is room (the timed pass reads it from memory either way)
-        st = os.statvfs("/dev/shm")
-        if st.f_bavail * st.f_frsize > 3 * need:
-            tmpdir = "/dev/shm"
-    except OSError:
-        pass
-    fd, path = tempfile.mkstemp(suffix=".fq", dir=tmpdir)
+    if rank == 0:
+        try:  # a RAM-backed file when there is room (the timed pass reads it from memory either way)
+            st = os.statvfs("/dev/shm")
+            if st.f_bavail * st.f_frsize > 3 * need:
+                tmpdir = "/dev/shm"
+        except OSError:
+            pass
+        fd, path = tempfile.mkstemp(suffix=".fq", dir=tmpdir)
+        os.ftruncate(fd, need)
+        os.close(fd)
+    else:
+        path = None
+    if world > 1:
+        box = [path, tmpdir]
+        dist.broadcast_object_list(box, src=0)
+        path, tmpdir = box
     try:
-        size = 0
-        with os.fdopen(fd, "wb") as f:
-            for a in range(0, n, 1_000_000):
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            for a in range(0, n, 1_000_000):  # this rank's records, ids numbered across the job
                 m = min(1_000_000, n - a)
-                buf = synth.fastq_bytes(bases[a * L:(a + m) * L], L, first=a)
-                size += buf.size
-                f.write(buf.tobytes())
-        with open(path, "rb") as f:  # page cache
-            while f.read(1 << 28):
-                pass
+                buf = synth.fastq_bytes(bases[a * L:(a + m) * L], L, first=rank * n + a)
+                os.pwrite(fd, buf.tobytes(), (rank * n + a) * rs)
+        finally:
+            os.close(fd)
+        if world > 1:
+            dist.barrier()
+        offs, states = skq.fastq_split(path, world)
+        part = (int(offs[rank]), int(offs[rank + 1]), int(states[rank]))
+        with open(path, "rb") as f:  # this rank's part into the page cache
+            f.seek(part[0])
+            left = part[1] - part[0]
+            while left > 0:
+                got = len(f.read(min(left, 1 << 28)))
+                if not got:
+                    break
+                left -= got
         es = skq.Session(index, batch, 256)
         emr = {}
 
         def run():
-            g = skq.Ingest(es, path, chunk_bytes=64 << 20, io_threads=8)
-            em = skq.EMSet(ntx)
+            g = skq.Ingest(es, path, chunk_bytes=64 << 20, io_threads=8, part=part)
+            em = skq.EMSet(ntx, device=dev.index if dev is not None else 0)
             tot = 0
             while True:
                 _, got = g.map(accumulate=True)
@@ -204,9 +230,15 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
             g.close()
             t1 = time.perf_counter()
             em.select(kept)
-            _, it = em.run(20, 0.01)
-            _, assigned = em.assign()
-            emr.update(em_ms=(time.perf_counter() - t1) * 1e3, em_rounds=it, assigned_transcripts=int(assigned.sum()))
+            if world == 1:
+                _, it = em.run(20, 0.01)
+                _, assigned = em.assign()
+                na = int(assigned.sum())
+            else:
+                pi, it = sdist.em_gpu(em, 20, 0.01, device=dev)
+                _, assigned = sdist.assign_gpu(em, pi)
+                na = int(assigned.sum().item())
+            emr.update(em_ms=(time.perf_counter() - t1) * 1e3, em_rounds=it, assigned_transcripts=na)
             em.free()
             return tot, int(kept.sum())
 
@@ -215,24 +247,39 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, batch=2_000_000):
         for _ in range(3):  # three timed passes; the median is reported (boxes' host paths vary)
             es.reset_totals()
             torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
             ts = time.perf_counter()
             got, kept = run()
             torch.cuda.synchronize()
-            times.append(time.perf_counter() - ts)
+            if world > 1:
+                dist.barrier()
+            times.append(sdist.max_over_ranks(time.perf_counter() - ts, device=dev))
         dt = sorted(times)[1]
-        etot = es.totals()
+        etot = torch.from_numpy(np.stack(es.totals()).astype(np.int64)).to(dev)
         es.free()
         sess.reset_totals(sp)
         sess.map(d_ptr, None, n, L, fixed_len=L, stream=sp, accumulate=True)
         sess.check(sp)
-        dtot = sess.totals()
-        ok = got == n and kept == n and np.array_equal(etot[0], dtot[0]) and np.array_equal(etot[1], dtot[1])
-        return dict(what="quant end to end on 1 GPU: FASTQ file (in memory: /dev/shm or the page cache) -> device parse -> sketch + chain "
-                        "-> EM + assignment (the CLI's path; not the metric)",
-                   reads=got, fastq_GB=size / 1e9, fastq_in="/dev/shm" if tmpdir else "page cache (%s)" % os.path.dirname(path), seconds=dt, reads_per_s=got / dt, pass_reads_per_s=[got / t for t in times],
-                   check="totals equal the in-HBM map's, all reads kept" if ok else "MISMATCH", **emr)
+        dtot = torch.from_numpy(np.stack(sess.totals()).astype(np.int64)).to(dev)
+        cnt = torch.tensor([got, kept], dtype=torch.int64, device=dev)
+        for t in (etot, dtot, cnt):
+            sdist.allreduce_totals(t)
+        got_all, kept_all = (int(x) for x in cnt.tolist())
+        ok = got_all == world * n and kept_all == world * n and torch.equal(etot, dtot)
+        return dict(what="quant end to end on %d GPU%s: one FASTQ file (in memory: /dev/shm or the page cache) split "
+                         "into one part per GPU -> device parse -> sketch + chain -> EM + assignment%s (the CLI's path; "
+                         "not the metric)" % (world, "s" if world > 1 else "",
+                                              " with RCCL all-reduces" if world > 1 else ""),
+                    reads=got_all, fastq_GB=need / 1e9,
+                    fastq_in="/dev/shm" if tmpdir else "page cache (%s)" % os.path.dirname(path), seconds=dt,
+                    reads_per_s=got_all / dt, pass_reads_per_s=[got_all / t for t in times],
+                    check="totals equal the in-HBM map's, all reads kept" if ok else "MISMATCH", **emr)
     finally:
-        os.unlink(path)
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            os.unlink(path)
 
 
 def cpu_model():
@@ -339,7 +386,12 @@ def main(args):
     names = (fused_name if map1 else "k_sketch", "k_probe", count_name, "totals")
     avg = {name: ms / cnt for name, (ms, cnt) in zip(names, kt) if cnt}
     kname = max(avg, key=avg.get)                       # dominant kernel
-    achieved = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
+    # roofline basis: SURVEY.md §8(d)'s algorithmic bytes per read (b_path) when the dominant launch
+    # is the fused map (the whole hot path: sketch + lookups + chain in it); the kernel's own
+    # input/output bytes (b_kern: + the status byte, hash counts, the binned totals) reported beside
+    b_basis = b_path if kname == fused_name else b_kern[kname]
+    achieved = n * b_basis / (avg[kname] * 1e-3) / 1e9
+    kio = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % cname)
     probe = index.stats()["probe"]
@@ -370,6 +422,8 @@ def main(args):
             ncpu = len(os.sched_getaffinity(0))
         except AttributeError:
             ncpu = os.cpu_count() or 1
+        # the box's CPU share: 16 threads per GPU (the pool's rule for worker pools); the affinity
+        # set can list the whole machine's CPUs, reported beside it
         P_thr = args.cpu_threads or max(1, min(16, ncpu))
         tc = time.perf_counter()
         cout = orc.fastq_map(oi, fq, nthreads=P_thr, outputs=True, hcap=64, ccap=64)
@@ -380,7 +434,9 @@ def main(args):
         log("parity sample: %s" % parity)
         if world == 1:
             cpu = {"value": m / dt_p, "unit": "reads/s", "cores": P_thr, "kind": "port",
-                   "cpu_model": cpu_model(),
+                   "cpu_model": cpu_model(), "affinity_cpus": ncpu,
+                   "cores_note": "threads = the box's CPU share per GPU (16) unless --cpu-threads; the "
+                                 "reference itself is single-threaded (see single_core)",
                    "sample": "first %d reads of the same batch as FASTQ text (%d MB in RAM), same index: "
                              "oracle/oracle.c orc_fastq_map (record machine, is_valid_sequence, sketch, "
                              "sparse_chain, id map, totals), %d threads over read shards, %.1fs"
@@ -397,9 +453,9 @@ def main(args):
             if os.path.exists(cal):  # reference sparse_chain vs the oracle's, timed in the build container
                 cpu["calibration"] = json.load(open(cal)).get("summary")
     e2e = None
-    if world == 1 and not args.no_end_to_end:
+    if not args.no_end_to_end:
         try:
-            e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp)
+            e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp, rank, world, dev)
         except (OSError, skq.SkqError) as ex:  # (e.g. no room for the FASTQ file): the metric line still prints
             e2e = {"error": "%s: %s" % (type(ex).__name__, ex)}
         log("end to end: %s" % json.dumps(e2e))
@@ -417,7 +473,10 @@ def main(args):
                        + (", 1 all-reduce of per-transcript totals per step" if world > 1 else "")},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes": n * b_kern[kname], "avg_launch_ms": avg[kname],
+                         "algorithmic_bytes": n * b_basis, "avg_launch_ms": avg[kname],
+                         "bytes_basis": ("SURVEY.md 8(d): L + 8h + 4P + 4h + 8C per read" if b_basis == b_path
+                                         else "kernel input/output bytes"),
+                         "kernel_io_bytes": n * b_kern[kname], "kernel_io_frac": kio / HBM_PEAK_GBS,
                          "requests": requests,
                          "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None},
             "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + index gathers + count fused)" if map1 else

@@ -137,8 +137,10 @@ typedef struct {
     const uint32_t* cand_ext;
     const uint64_t* tx_reads; /* per transcript: reads listing it as a candidate (accumulated) */
     const uint64_t* tx_score; /* per transcript: sum of those reads' scores (accumulated)      */
-    /* (batches of 4M+ reads finish their totals on the session's own side stream: read these
-     * through skq_session_totals, which waits for it, or after a device synchronize) */
+    /* (batches of 512k+ reads finish their totals on the session's own side stream, which the
+     * launch stream does not wait for: skq_session_results blocks the host until that work is
+     * done, so tx_reads / tx_score are current once the caller's stream is synchronized too;
+     * skq_session_totals waits for it on the caller's stream instead) */
 } skq_results;
 int skq_session_results(skq_session* s, skq_results* out);
 

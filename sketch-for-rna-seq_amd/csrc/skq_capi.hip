@@ -503,10 +503,13 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     const bool wide_ok = ids_ok && need * 8 <= budget && need * 8 <= fr / 2;
     if (wide_ok && (!force || forced("wide"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
     if (forced("wide")) return 0;  // forced but does not fit: bucket table
-    if (ids_ok && (!force || forced("compact"))) {
+    uint64_t cmp_need = 0;  // compact tables: m / 0.95 slots of 32 B + 2-B pilots per 5 keys, per k
+    for (uint32_t t = 0; t < ntables; ++t)
+        cmp_need += (uint64_t)std::ceil((double)dkeys[t].size() / 0.95) * 32 + 64 + (dkeys[t].size() + 4) / 5 * 2;
+    if (ids_ok && (forced("compact") || (!force && cmp_need <= budget && cmp_need <= fr / 2))) {
         const int rc = build_compact(ix, ntables, tables, dkeys, dvals, lists);
-        if (rc == 0 || rc == -3 || forced("compact")) return rc;
-        for (auto& d : ix->d_wdir_t) dev_free(d);  // (placement failed: another kind)
+        if (rc == 0 || forced("compact")) return rc;
+        for (auto& d : ix->d_wdir_t) dev_free(d);  // (placement or allocation failed: another kind)
         for (auto& d : ix->d_wpil_t) dev_free(d);
         for (auto& w : ix->wdir) w = nullptr;
         for (auto& w : ix->wpil) w = nullptr;
@@ -1095,10 +1098,17 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
                      void* stream) {
     skq::SketchParams sp{};
     skq::ChainParams cp{};
-    if (s->idx->nk > 1 && !s->ktab) {  // the per-k tables of the multi-k passes
+    if (s->idx->nk > 1 && (!s->ktab || !s->kcnt)) {  // the per-k tables of the multi-k passes
         DeviceGuard g(s->idx->device);
-        if (int rc = dev_alloc(&s->ktab, (uint64_t)s->idx->nk * skq::DCAP * s->max_reads)) return rc;
-        if (int rc = dev_alloc(&s->kcnt, 2ull * s->idx->nk * s->max_reads)) return rc;  // counts, needs
+        dev_free(s->ktab);  // (both or neither: a failed pair is retried whole)
+        dev_free(s->kcnt);
+        int rc = dev_alloc(&s->ktab, (uint64_t)s->idx->nk * skq::DCAP * s->max_reads);
+        if (!rc) rc = dev_alloc(&s->kcnt, 2ull * s->idx->nk * s->max_reads);  // counts, needs
+        if (rc) {
+            dev_free(s->ktab);
+            dev_free(s->kcnt);
+            return rc;
+        }
     }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
@@ -1164,6 +1174,11 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
 
 int skq_session_results(skq_session* s, skq_results* o) {
     if (!s || !o) return fail(-1, "null argument");
+    {  // the totals of forked batches (chain_tail) may still run on the side stream
+        DeviceGuard g(s->idx->device);
+        for (int b = 0; b < 2; ++b)
+            if (s->side && s->join_rec[b]) HIP_TRY(hipEventSynchronize(s->ev_join[b]));
+    }
     o->n_reads = s->n_reads;
     o->nk = s->idx->nk;
     o->hcap = s->hcap;

@@ -51,7 +51,9 @@ void print_help(const std::string& prog) {
               << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
               << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_DEVICES (GPU list for quant,\n"
               << "             e.g. 0,1,2,3 or all), SKQ_BATCH (reads per batch), SKQ_CHUNK_MB (FASTQ MiB\n"
-              << "             per device chunk, default 64).\n";
+              << "             per device chunk, default 64), SKQ_REDUCE (rccl | host: how the EM sums\n"
+              << "             reduce over devices; rccl on one device runs the sharded EM over a\n"
+              << "             one-rank RCCL communicator).\n";
 }
 
 const float kSketchSize = 0.05f;  // src/main.cpp:43
@@ -131,6 +133,14 @@ struct Part {
     }
 };
 
+// SKQ_REDUCE: "rccl" forces the sharded EM and RCCL even on one device (a one-rank communicator:
+// the library path the multi-GPU run takes, testable on a one-GPU box); "host" forces the
+// host-staged sums; unset: RCCL when the devices are distinct, the host when one repeats
+std::string reduce_mode() {
+    const char* e = std::getenv("SKQ_REDUCE");
+    return e ? std::string(e) : std::string();
+}
+
 // Sum (or max) of one device array over the parts, left in every part's copy: RCCL over xGMI
 // when the devices are distinct; a host-staged sum in part order when a device repeats (several
 // parts sharing one GPU, as the tests run them).
@@ -145,6 +155,9 @@ struct Reducer {
         std::vector<int> u = devs;
         std::sort(u.begin(), u.end());
         host = std::unique(u.begin(), u.end()) != u.end();
+        const std::string mode = reduce_mode();
+        if (mode == "rccl" && host) throw std::runtime_error("SKQ_REDUCE=rccl needs distinct devices");
+        if (mode == "host") host = true;
         if (!host) {
             comms.resize(parts.size());
             if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess)
@@ -268,7 +281,7 @@ void quantification(const std::string& index_path, const std::string& reads_path
     }
     std::vector<double> pi(ntx), counts(ntx);
     std::vector<uint8_t> assigned(ntx);
-    if (D == 1) {
+    if (D == 1 && reduce_mode() != "rccl") {
         Part& p = parts[0];
         int iters = 0;
         check(skq_em_run(p.em, 20, 0.01, pi.data(), &iters), "EM");

@@ -783,7 +783,9 @@ int skq_ingest_supersede(skq_ingest* const* gs, uint32_t nparts, uint8_t* const*
     (void)hipGetDevice(&prev);
     for (uint32_t d = 0; d < nparts; ++d) {
         const skq_ingest* g = gs[d];
-        if (!g || !kept[d]) return ifail(-1, "null part");
+        // (a part may hold no records — a short file split many ways — and then no kept array:
+        // an empty std::vector's data() is null)
+        if (!g || (!kept[d] && g->records)) return ifail(-1, "null part");
         if (!g->finished) return ifail(-1, "call skq_ingest_finish on every part first");
         std::vector<uint64_t> h(g->records);
         (void)hipSetDevice(g->device);

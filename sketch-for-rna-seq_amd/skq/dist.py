@@ -26,7 +26,8 @@ def shard(n, rank, world_size):
 
 def allreduce_totals(totals):
     """Sum a [2, ntx] int64 tensor of per-transcript totals over all ranks, in place. A no-op
-    without an initialised process group (single GPU)."""
+    without an initialised process group (single GPU); with one, the collective runs at any world
+    size (a world-1 RCCL group exercises the library path, tests/test_rccl_gpu.py)."""
     return _allreduce(totals)
 
 
@@ -42,7 +43,7 @@ def max_over_ranks(value, device=None):
 def _allreduce(t, op=None):
     """Sum (or op) over ranks in place. RCCL takes device tensors directly; on gloo (CPU tests and
     one-GPU rehearsals) a device tensor goes through host memory."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         op = dist.ReduceOp.SUM if op is None else op
         if t.is_cuda and dist.get_backend() == "gloo":
             h = t.cpu()

@@ -112,13 +112,15 @@ def test_cfg5_multi_k_200k_transcripts(tx200k):
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
 
 
-def test_cfg3_full_batch_totals(tx200k):
-    """The bench's own batch (10M x 150 bp, one skq_map): per-transcript totals equal the
-    oracle's over the same 10M reads as FASTQ text."""
-    ks, L, n = [31], 150, 10_000_000
+@pytest.mark.parametrize("n,seed", [(10_000_000, 1000), (12_500_000, 1003)], ids=["cfg3_10M", "cfg4_rank3_12.5M"])
+def test_full_batch_totals(tx200k, n, seed):
+    """The bench's own batches, one skq_map each: cfg3 (10M x 150 bp, rank 0) and cfg4's per-GPU
+    shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it): per-transcript totals
+    equal the oracle's over the same reads as FASTQ text."""
+    ks, L = [31], 150
     tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
     index = skq.Index(ks, tx200k.ntx, tables)
-    bases, _, _ = synth.reads(tx200k, n, L, seed=1000, err=0.001)  # bench.py's rank-0 batch
+    bases, _, _ = synth.reads(tx200k, n, L, seed=seed, err=0.001)  # bench.py's batch of rank seed - 1000
     s = skq.Session(index, n, L)
     d = skq.DeviceBuffer.from_numpy(bases)
     s.map(d.ptr, None, n, L, fixed_len=L)
