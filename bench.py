@@ -392,13 +392,15 @@ def main(args):
     b_basis = b_path if kname == fused_name else b_kern[kname]
     achieved = n * b_basis / (avg[kname] * 1e-3) / 1e9
     kio = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % cname)
     probe = index.stats()["probe"]
     if os.path.exists(tf):                               # PMC FETCH/WRITE passes (tools/traffic.py)
         tr = json.load(open(tf))
-        if kname in tr.get("kernels", {}) and tr.get("probe", probe) == probe:
+        if kname in tr.get("kernels", {}) and tr.get("probe", probe) == probe and "calibration" in tr:
             traffic = tr["kernels"][kname]["hbm_bytes_per_read"] * n
+            traffic_src = "profiles/traffic_%s.json (%s); %s" % (cname, tr.get("measured", "builder's PMC passes"),
+                                                                tr["calibration"])
     requests = None
     if map1:  # random index requests per launch against the measured gather ceiling
         rps = n * h / (avg[kname] * 1e-3) / 1e9
@@ -478,7 +480,8 @@ def main(args):
                                          else "kernel input/output bytes"),
                          "kernel_io_bytes": n * b_kern[kname], "kernel_io_frac": kio / HBM_PEAK_GBS,
                          "requests": requests,
-                         "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None},
+                         "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None,
+                         "traffic_source": traffic_src},
             "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + index gathers + count fused)" if map1 else
                                                 "fused in k_sketch" if fused else "k_probe"),
                      "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,

@@ -1,12 +1,17 @@
 #!/usr/bin/env python3
 """HBM traffic per read, per kernel, from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over bench.py.
 
-usage: tools/traffic.py CONFIG FETCH_DIR WRITE_DIR OUT.json
+usage: tools/traffic.py CONFIG FETCH_DIR WRITE_DIR OUT.json [KERNEL=STREAMED_BYTES_PER_READ ...]
 
-Applies MI355X_MICROARCH.md "HBM [CDNA4]": on gfx950 FETCH_SIZE reports half the bytes of a wide
-coalesced read, so bytes = 2 * FETCH_SIZE(kB) * 1024 + WRITE_SIZE(kB) * 1024. Only the full-size
-dispatches of each kernel are used (largest grid); the figure is divided by the grid's threads,
-one per read, giving bytes per read that bench.py scales to its launch.
+Calibrated per profiles/r3_fetch_calibration.json (tools/micro/calib.hip on known byte counts, as
+MI355X_MICROARCH.md "HBM [CDNA4]" requires for access widths other than wide streaming reads):
+FETCH_SIZE tallies 64 B per memory-side read request; a streamed (coalesced) request moves 128 B,
+a random 32-B entry gather is one 64-B request. So per kernel
+    bytes = FETCH_SIZE(kB) * 1024 + STREAMED / 2 + WRITE_SIZE(kB) * 1024,
+STREAMED being the bytes the kernel reads as coalesced streams (k_map1: the read bases, L per
+read; given on the command line). Only the full-size dispatches of each kernel are used (largest
+grid); the figure is divided by the grid's reads (one thread per read, 256 per workgroup),
+giving bytes per read that bench.py scales to its launch.
 """
 import collections
 import csv
@@ -16,6 +21,7 @@ import statistics
 import sys
 
 cfg, fdir, wdir, out = sys.argv[1:5]
+streamed = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in sys.argv[5:]}
 
 
 def per_read(d, counter):
@@ -63,10 +69,14 @@ kern = {}
 for name in sorted(set(fetch) & set(write)):
     f, nf, g = fetch[name]
     w, nw, _ = write[name]
-    kern[name] = {"fetch_bytes_per_read": 2 * f * 1024, "write_bytes_per_read": w * 1024,
-                  "hbm_bytes_per_read": 2 * f * 1024 + w * 1024, "grid_threads": g,
+    sb = streamed.get(name, 0.0)
+    kern[name] = {"fetch_size_bytes_per_read": f * 1024, "streamed_read_bytes_per_read": sb,
+                  "fetch_bytes_per_read": f * 1024 + sb / 2, "write_bytes_per_read": w * 1024,
+                  "hbm_bytes_per_read": f * 1024 + sb / 2 + w * 1024, "grid_threads": g,
                   "dispatches": [nf, nw]}
 json.dump({"config": cfg, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace over "
-           "bench.py; FETCH doubled per MI355X_MICROARCH.md (gfx950)", "kernels": kern},
+           "bench.py", "calibration": "profiles/r3_fetch_calibration.json: bytes = FETCH_SIZE + streamed/2 + "
+           "WRITE_SIZE (FETCH_SIZE tallies 64 B per request; streamed requests move 128 B, random 32-B "
+           "gathers are 64-B requests)", "kernels": kern},
           open(out, "w"), indent=1)
 print(json.dumps(kern, indent=1))
