@@ -77,6 +77,12 @@ int skq_index_stats(const skq_index* idx, uint64_t* device_bytes, uint64_t* npos
  * bucket table) and half the free device memory is built; SKQ_PROBE = wide | dir | rank forces
  * one kind. */
 int skq_index_direct(const skq_index* ix);
+/* Partitions of the partitioned map's tables (0: none). With one k slot, ids within 22 bits and
+ * wide or compact tables, SKQ_PART=1 at index creation adds per-key-range compact tables small
+ * enough for one XCD's L2; skq_map then runs the partitioned map (k_part_a: sketch + the retained
+ * hashes grouped by key range; k_part_b: the lookups of one key range per workgroup, on one XCD;
+ * k_part_c: the per-read vote), identical results. */
+int skq_index_partitions(const skq_index* ix);
 
 /* A session owns the device workspace for batches of up to max_reads reads of at most
  * max_len bases each (longer reads are still handled exactly, by the slow path). */

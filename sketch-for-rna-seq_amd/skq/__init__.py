@@ -52,6 +52,7 @@ def lib():
             "skq_index_free": (i32, [vp]),
             "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
             "skq_index_direct": (i32, [vp]),
+            "skq_index_partitions": (i32, [vp]),
             "skq_session_slow_reads": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
             "skq_session_slow_counts": (i32, [vp, C.POINTER(u32)]),
             "skq_session_create": (i32, [vp, u64, u32, C.POINTER(vp)]),
@@ -212,7 +213,8 @@ class Index:
         _check(lib().skq_index_stats(self.h, C.byref(b), C.byref(n), C.byref(m)))
         return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
                     direct=bool(lib().skq_index_direct(self.h)),
-                    probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 4: "block", 5: "compact"}[lib().skq_index_direct(self.h)])
+                    probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 4: "block", 5: "compact"}[lib().skq_index_direct(self.h)],
+                    partitions=lib().skq_index_partitions(self.h))
 
     def free(self):
         if self.h:

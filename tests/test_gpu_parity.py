@@ -17,14 +17,22 @@ pytestmark = pytest.mark.gpu
 SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the wide-split mode)
 
 
-@pytest.fixture(autouse=True, params=["compact", "compact-split", "block", "wide", "wide-split", "dir", "rank",
-                                      "bucket"])
+@pytest.fixture(autouse=True, params=["part", "part-compact", "compact", "compact-split", "block", "wide",
+                                      "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
     """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables,
     block tables and wide direct tables gathered by the map or count kernel, 4-B direct and rank
     tables probed inside the sketch kernel, and the bucket table probed by k_probe
-    (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map)."""
-    if request.param == "bucket":
+    (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map).
+    "part": the partitioned map (k_part_a/b/c; SKQ_PART=1) over wide tables for the slow paths,
+    "part-compact" over compact tables; indexes it does not apply to (several k) run as wide /
+    compact."""
+    monkeypatch.setenv("SKQ_PART", "0")
+    if request.param.startswith("part"):
+        monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
+        monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "part-compact" else "wide")
+        monkeypatch.setenv("SKQ_PART", "1")
+    elif request.param == "bucket":
         monkeypatch.setenv("SKQ_DIRECT_MB", "0")
     elif request.param.endswith("-split"):
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")

@@ -94,14 +94,20 @@ def _case(tx, ks, L, nreads, seed, err=0.001):
     return cpu, st, slow
 
 
-def test_cfg2_10k_transcripts_100bp(tx10k):
+@pytest.mark.parametrize("part", ["0", "1"], ids=["map1", "part"])
+def test_cfg2_10k_transcripts_100bp(tx10k, part, monkeypatch):
+    monkeypatch.setenv("SKQ_PART", part)
     cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201)
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
 
 
-def test_cfg3_200k_transcripts_150bp(tx200k):
+@pytest.mark.parametrize("part", ["0", "1"], ids=["map1", "part"])
+def test_cfg3_200k_transcripts_150bp(tx200k, part, monkeypatch):
+    """part = 1: the partitioned map (k_part_a/b/c) over the same index."""
+    monkeypatch.setenv("SKQ_PART", part)
     cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301)
+    assert (st["partitions"] > 50) == (part == "1"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert st["max_list"] >= 10  # GENCODE-scale postings (long lists take the inline overflow)
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed

@@ -32,13 +32,17 @@ tx = synth.transcriptome(a.ntx, seed=1)
 tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
 indexes, sessions = {}, {}
 for pm in a.probes.split(","):
-    if pm == "auto":
+    # "<kind>/part": that probe kind plus the partitioned map's tables (SKQ_PART=1)
+    kind, _, part = pm.partition("/")
+    if kind == "auto":
         os.environ.pop("SKQ_PROBE", None)
     else:
-        os.environ["SKQ_PROBE"] = pm
+        os.environ["SKQ_PROBE"] = kind
+    os.environ["SKQ_PART"] = "1" if part == "part" else "0"
     indexes[pm] = skq.Index(ks, tx.ntx, tables)
     print(pm, indexes[pm].stats(), flush=True)
 os.environ.pop("SKQ_PROBE", None)
+os.environ.pop("SKQ_PART", None)
 bases, _, _ = synth.reads(tx, a.reads, a.len, seed=1000, err=0.001)
 dev = torch.device("cuda", 0)
 d = torch.from_numpy(bases).to(dev)
@@ -79,6 +83,18 @@ for rnd in range(a.rounds + 1):
             res[name].append((wall, k1, k2, k3, k4))
 for pm, sx in sessions.items():
     print(pm, "slow reads (sketch, chain) of the last batch:", sx.slow_reads())
+# every layout's per-transcript totals over the batch must be identical (each is checked against
+# the oracle by the GPU tests; here they are checked against each other at full size)
+tot0 = None
+for pm, sx in sessions.items():
+    sx.reset_totals(sp)
+    sx.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=True)
+    sx.check(sp)
+    tot = sx.totals()
+    if tot0 is None:
+        tot0 = tot
+    same = bool(np.array_equal(tot[0], tot0[0]) and np.array_equal(tot[1], tot0[1]))
+    print(pm, "totals", "identical to %s" % pm0 if same else "DIFFER from %s" % pm0, int(tot[0].sum()), flush=True)
 for name, v in res.items():
     v = np.array(v)
     med = np.median(v, axis=0)
