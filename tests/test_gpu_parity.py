@@ -116,8 +116,12 @@ def totals_from(ref, n, ntx):
 def test_probe_mode_is_selected(tx300, probe_mode):
     gi, _ = build([21, 31], tx=tx300)
     st = gi.stats()
-    assert st["probe"] == probe_mode.split("-")[0]
+    base = {"part": "wide", "part-compact": "compact"}.get(probe_mode, probe_mode.split("-")[0])
+    assert st["probe"] == base
     assert st["device_bytes"] > 0
+    assert st["partitions"] == 0  # (several k: no partitioned tables)
+    gi1, _ = build([31], tx=tx300)
+    assert (gi1.stats()["partitions"] > 0) == probe_mode.startswith("part")
 
 
 @pytest.fixture(scope="module")
