@@ -1273,15 +1273,20 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         pp.bw = 64;
         if (const char* e = std::getenv("SKQ_PART_BW")) pp.bw = (uint32_t)std::max(1, std::min(256, std::atoi(e)));
         pp.nbk = (uint32_t)((n_reads + skq::WG - 1) / skq::WG);
+        // bucket strides padded off powers of two (SKQ_PART_PAD=0: unpadded, for A/B)
+        const char* pe = std::getenv("SKQ_PART_PAD");
+        const bool pad = !pe || std::atoi(pe) != 0;
+        pp.pstride = pp.cap + (pad ? 48u : 0u);
+        pp.ostride = 8ull * pp.cap + (pad ? 80u : 0u);
         if (s->part_hcap < sp.hcap) {  // the workspace, sized for the session's batch at this capacity
             dev_free(s->part_pairs);
             dev_free(s->part_poff);
             dev_free(s->part_out);
             s->part_hcap = 0;
             const uint64_t nW = (s->max_reads + skq::WG - 1) / skq::WG;
-            int arc = dev_alloc(&s->part_pairs, nW * pp.cap);
+            int arc = dev_alloc(&s->part_pairs, nW * (pp.cap + 48ull));
             if (!arc) arc = dev_alloc(&s->part_poff, nW * pp.row);
-            if (!arc) arc = dev_alloc(&s->part_out, nW * 8ull * pp.cap);
+            if (!arc) arc = dev_alloc(&s->part_out, nW * (8ull * pp.cap + 80ull));
             if (arc) {
                 dev_free(s->part_pairs);
                 dev_free(s->part_poff);

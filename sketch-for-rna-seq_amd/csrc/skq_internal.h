@@ -179,9 +179,9 @@ struct ChainParams {
 // a minimal perfect hash over that partition's keys alone), small enough for one XCD's L2.
 //   k_part_a: per workgroup (bucket w of 256 reads): sketch as k_map1, then the retained hashes as
 //             pair words (hash & (2^shift - 1)) | lane << shift, grouped by partition:
-//             pairs[w * cap + poff[w * row + p] ...], poff[w * row + np] = the bucket's pairs;
+//             pairs[w * pstride + poff[w * row + p] ...], poff[w * row + np] = the bucket's pairs;
 //   k_part_b: per (partition, run of bw buckets), with partition p on the XCD of blocks p mod 8:
-//             every pair looked up in p's table; per (w, p) piece, at out[w * 8 * cap + 8 * poff]:
+//             every pair looked up in p's table; per (w, p) piece, at out[w * ostride + 8 * poff]:
 //             one header word per pair (lane | F << 8 | tid offset << 12, or PART_MISS) followed by
 //             the tids of the hits (F <= 7 inline; F = 8: one word, the list offset in lists[]);
 //   k_part_c: per bucket: the pieces' tids counted per read in LDS, then filter, order, write and
@@ -205,6 +205,10 @@ struct PartParams {
     uint32_t cap;   // pair slots per bucket (WG * raw capacity)
     uint32_t bw;    // buckets per k_part_b workgroup
     uint32_t nbk;   // buckets (k_part_a / k_part_c workgroups)
+    // words per bucket of pairs (>= cap) and of out (>= 8 * cap): padded past powers of two, so
+    // that one partition's pieces in consecutive buckets do not all map to one L2 channel / set
+    uint32_t pstride;
+    uint64_t ostride;
     uint32_t* pairs;
     uint16_t* poff;
     uint32_t* out;

@@ -2856,7 +2856,7 @@ __global__ __launch_bounds__(WG) void k_part_a(SketchParams p, ChainParams cp, P
         if (pr[j] != ~0u) s_stage[s_hist[pr[j] & 255u] + (pr[j] >> 8)] = v[j];
     __syncthreads();
     const uint32_t total = s_hist[npx];
-    uint4* dst = reinterpret_cast<uint4*>(pp.pairs + (uint64_t)blockIdx.x * pp.cap);
+    uint4* dst = reinterpret_cast<uint4*>(pp.pairs + (uint64_t)blockIdx.x * pp.pstride);
     const uint4* sr = reinterpret_cast<const uint4*>(s_stage);
     for (uint32_t q = tid; q < (total + 3) / 4; q += WG) dst[q] = sr[q];
     uint16_t* prow = pp.poff + (uint64_t)blockIdx.x * pp.row;
@@ -2895,7 +2895,7 @@ __global__ __launch_bounds__(WG) void k_part_b(PartParams pp) {
     __syncthreads();
     const PartDesc d = pp.desc[p];
     const uint32_t shift = pp.shift, mask = (1u << shift) - 1u;
-    const uint64_t ocap = 8ull * pp.cap;
+    const uint64_t ocap = pp.ostride;
     uint32_t carry = 0;  // tid words of the earlier rounds
     for (uint32_t base = 0; base < M; base += WG * R) {  // block-uniform
         uint32_t hdr[R], nw[R], bk[R], loc[R];
@@ -2919,7 +2919,7 @@ __global__ __launch_bounds__(WG) void k_part_b(PartParams pp) {
                 }
                 bk[u] = lo;
                 loc[u] = i - s_pre[lo];
-                const uint32_t pw = pp.pairs[(uint64_t)(w0 + lo) * pp.cap + s_st[lo] + loc[u]];
+                const uint32_t pw = pp.pairs[(uint64_t)(w0 + lo) * pp.pstride + s_st[lo] + loc[u]];
                 const uint32_t key = (p << shift) | (pw & mask);
                 const uint32_t kh = cmp_key_hash(key, d.seed);
                 const uint32_t pv = pp.pil[d.pil_base + cmp_scale(kh, d.nb)];
@@ -2989,7 +2989,7 @@ __global__ __launch_bounds__(WG) void k_part_c(SketchParams p, ChainParams cp, P
     for (uint32_t q = t; q <= pp.np; q += WG) s_off[q] = prow[q];
     __syncthreads();
     const uint32_t np = pp.np, M = s_off[np];
-    const uint32_t* region = pp.out + (uint64_t)w * 8ull * pp.cap;
+    const uint32_t* region = pp.out + (uint64_t)w * pp.ostride;
     auto tab = [&](uint32_t o, uint32_t sl) -> uint32_t* { return s_cnt + sl * WG + (o & ~63u) + ((o + sl) & 63u); };
     auto ains_probe = [&](uint32_t x, uint32_t o) {
         uint32_t sl = Counter<1, WG>::slot_of(x);
@@ -3086,7 +3086,8 @@ __global__ __launch_bounds__(WG) void k_part_c(SketchParams p, ChainParams cp, P
 int launch_part(const SketchParams& p, const ChainParams& cp, const PartParams& pp, void* stream) {
     if (p.n == 0) return 0;
     if (pp.nbk != (uint32_t)((p.n + WG - 1) / WG) || pp.npx % 8 || pp.np > pp.npx || pp.npx > PART_MAX_NP ||
-        pp.row < pp.npx + 1 || pp.cap != (uint32_t)WG * p.hcap || pp.bw == 0 || pp.bw > (uint32_t)WG)
+        pp.row < pp.npx + 1 || pp.cap != (uint32_t)WG * p.hcap || pp.bw == 0 || pp.bw > (uint32_t)WG ||
+        pp.pstride < pp.cap || pp.pstride % 4 || pp.ostride < 8ull * pp.cap)
         return -4;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid(pp.nbk);
