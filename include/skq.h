@@ -84,6 +84,19 @@ int skq_index_direct(const skq_index* ix);
  * k_part_c: the per-read vote), identical results. */
 int skq_index_partitions(const skq_index* ix);
 
+/* skq_index_create plus, for an index of one k whose transcripts are given (seqs[seq_offs[t] ..
+ * seq_offs[t+1]), the sequences the tables were built from, sketched at `threshold`), chained
+ * tables: per possible key a 128-B entry holding its postings list and those of the keys that
+ * follow it along the transcripts (nearest first, whole lists). skq_map then settles a read's
+ * retained hashes with about 1.5 entry requests instead of one per hash; results
+ * are identical (a record is used only for its exact key). SKQ_CHAIN=0 leaves them out. Other
+ * indexes: as skq_index_create. */
+int skq_index_create_chained(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
+                             const skq_kmer_table* tables, const uint8_t* seqs, const uint64_t* seq_offs,
+                             uint32_t nseq, uint32_t threshold, skq_index** out);
+/* 0: no chained tables; else 1 + the mean successor records per entry */
+double skq_index_chained(const skq_index* ix);
+
 /* A session owns the device workspace for batches of up to max_reads reads of at most
  * max_len bases each (longer reads are still handled exactly, by the slow path). */
 int skq_session_create(skq_index* idx, uint64_t max_reads, uint32_t max_len, skq_session** out);

@@ -86,6 +86,13 @@ struct skq_index {
     skq::PartDesc* d_pdesc = nullptr;
     uint32_t part_shift = 0, part_np = 0, part_npx = 0;
     uint64_t part_bytes = 0;
+    // chained tables (one k slot; ChainParams::chain): a 128-B entry per possible key up to the
+    // largest, carrying the key's postings list and those of the keys that follow it in the
+    // transcripts; k_map1 then settles a read with ~1.5 entry requests instead of one per hash
+    uint4* d_chain = nullptr;
+    uint64_t chain_len = 0;
+    uint64_t chain_bytes = 0;
+    double chain_succ = 0;  // mean successor records per entry (stats)
     // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 4 = block tables,
     // 5 = compact tables
     int mode = 0;
@@ -589,6 +596,166 @@ int build_part(skq_index* ix, const std::vector<uint32_t>& keys, const std::vect
     return 0;
 }
 
+
+// Chained tables for one k slot (ChainParams::chain). The transcripts are sketched in position
+// order (the index's own hashing: skq::sketch_positions); every retained k-mer's successors within
+// CHAIN_HOPS retained positions in any transcript are candidates for its entry, nearest first
+// (ties: smaller key); each candidate's record carries its WHOLE postings list from the index's
+// own tables (lists[] through the key's list offset), so whatever a record settles is exactly
+// what a lookup of that key would have returned. Records are added while they fit in 31 words.
+// The entries (one per present key) are built on the host and scattered on the device into a
+// table of 128-B entries for every possible key up to the largest (27.5 GB at (double)0.05f and
+// 4.24M keys: HBM3E holds it; one 128-B request per lookup, no key hashing).
+constexpr uint32_t CHAIN_HOPS = 8;
+
+__global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* ent, uint64_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n * 8) return;
+    tab[(uint64_t)keys[j >> 3] * 8 + (j & 7)] = ent[j];
+}
+
+int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
+                const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
+                uint32_t nseq, uint32_t threshold) {
+    const uint64_t m = keys.size();
+    if (m == 0) return 0;
+    const uint64_t len = (uint64_t)keys.back() + 1;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || len * 128 > fr / 2) return 0;  // (does not fit: no chains)
+    const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // (key, successor, hop) triples, bucketed by key range, one sort per bucket
+    constexpr uint32_t NB = 256;
+    struct Cand {
+        uint32_t h, g, d;
+        bool operator<(const Cand& o) const {
+            return h != o.h ? h < o.h : (d != o.d ? d < o.d : g < o.g);
+        }
+    };
+    const uint64_t span = len / NB + 1;
+    std::vector<std::vector<std::vector<Cand>>> part(P, std::vector<std::vector<Cand>>(NB));
+    {
+        std::atomic<uint32_t> next{0};
+        std::vector<std::thread> pool;
+        for (uint32_t w = 0; w < P; ++w)
+            pool.emplace_back([&, w] {
+                std::vector<uint32_t> run;
+                for (uint32_t t; (t = next.fetch_add(64)) < nseq;)
+                    for (uint32_t u = t; u < std::min(nseq, t + 64); ++u) {
+                        run.clear();
+                        skq::sketch_positions(seqs + offs[u], offs[u + 1] - offs[u], k, threshold, run);
+                        for (size_t i = 0; i < run.size(); ++i)
+                            for (uint32_t d = 1; d <= CHAIN_HOPS && i + d < run.size(); ++d)
+                                if (run[i + d] != run[i] && run[i] < len)
+                                    part[w][run[i] / span].push_back({run[i], run[i + d], d});
+                    }
+            });
+        for (auto& t : pool) t.join();
+    }
+    std::vector<uint32_t> ent(m * skq::CHAIN_WORDS, 0);
+    std::atomic<uint64_t> nsucc{0};
+    {
+        std::atomic<uint32_t> next{0};
+        std::vector<std::thread> pool;
+        for (uint32_t w = 0; w < P; ++w)
+            pool.emplace_back([&] {
+                std::vector<Cand> c;
+                uint64_t ns = 0;
+                auto index_of = [&](uint32_t key) -> int64_t {
+                    const auto it = std::lower_bound(keys.begin(), keys.end(), key);
+                    return it != keys.end() && *it == key ? (int64_t)(it - keys.begin()) : -1;
+                };
+                // one record: [key, n << 22 | t0, t1 ..] or [key, 8 << 22, offset]; false: no room
+                auto put = [&](uint32_t* e, uint32_t& used, uint32_t key, uint32_t off) -> bool {
+                    const uint32_t n = lists[off];
+                    const uint32_t words = n <= 7 ? n + 1 : 3;
+                    if (used + words > skq::CHAIN_WORDS) return false;
+                    e[used] = key;
+                    if (n <= 7) {
+                        e[used + 1] = (n << 22) | lists[off + 1];
+                        for (uint32_t q = 1; q < n; ++q) e[used + 1 + q] = lists[off + 1 + q];
+                    } else {
+                        e[used + 1] = skq::CMP_LONG << 22;
+                        e[used + 2] = off;
+                    }
+                    used += words;
+                    return true;
+                };
+                for (uint32_t b; (b = next.fetch_add(1)) < NB;) {
+                    c.clear();
+                    for (uint32_t q = 0; q < P; ++q) c.insert(c.end(), part[q][b].begin(), part[q][b].end());
+                    std::sort(c.begin(), c.end());
+                    for (size_t i = 0; i < c.size();) {
+                        size_t j = i;
+                        while (j < c.size() && c[j].h == c[i].h) ++j;
+                        const int64_t x = index_of(c[i].h);
+                        if (x >= 0) {
+                            uint32_t* e = ent.data() + (uint64_t)x * skq::CHAIN_WORDS;
+                            uint32_t used = 1;
+                            if (e[0] == 0 && put(e, used, c[i].h, vals[x])) {  // the key's own record first
+                                std::vector<uint32_t> seen;
+                                for (size_t q = i; q < j; ++q) {
+                                    if (std::find(seen.begin(), seen.end(), c[q].g) != seen.end()) continue;
+                                    seen.push_back(c[q].g);
+                                    const int64_t y = index_of(c[q].g);
+                                    if (y < 0) continue;
+                                    if (!put(e, used, c[q].g, vals[y])) break;
+                                    ++ns;
+                                }
+                                e[0] = used - 1;
+                            }
+                        }
+                        i = j;
+                    }
+                    for (uint32_t q = 0; q < P; ++q) std::vector<Cand>().swap(part[q][b]);  // (this thread's bucket)
+                }
+                nsucc += ns;
+            });
+        for (auto& t : pool) t.join();
+    }
+    // keys no transcript of `seqs` retained still get their own record
+    for (uint64_t x = 0; x < m; ++x) {
+        uint32_t* e = ent.data() + x * skq::CHAIN_WORDS;
+        if (e[0]) continue;
+        const uint32_t off = vals[x], n = lists[off];
+        e[1] = keys[x];
+        if (n <= 7) {
+            e[2] = (n << 22) | lists[off + 1];
+            for (uint32_t q = 1; q < n; ++q) e[2 + q] = lists[off + 1 + q];
+            e[0] = n + 1;
+        } else {
+            e[2] = skq::CMP_LONG << 22;
+            e[3] = off;
+            e[0] = 3;
+        }
+    }
+    uint32_t* dk = nullptr;
+    uint4* de = nullptr;
+    if (dev_alloc(&ix->d_chain, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
+        dev_free(dk);
+        dev_free(de);
+        dev_free(ix->d_chain);
+        return fail(-3, "chained table allocation failed");
+    }
+    hipStream_t st = nullptr;
+    const bool ok = hipMemsetAsync(ix->d_chain, 0, len * 128, st) == hipSuccess &&
+                    hipMemcpy(dk, keys.data(), m * 4, hipMemcpyHostToDevice) == hipSuccess &&
+                    hipMemcpy(de, ent.data(), m * 128, hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_chain_scatter, dim3((unsigned)((m * 8 + 255) / 256)), dim3(256), 0, st, ix->d_chain, dk, de, m);
+    }
+    const bool done = ok && hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+    dev_free(dk);
+    dev_free(de);
+    if (!done) {
+        dev_free(ix->d_chain);
+        return fail(-3, "chained table build failed");
+    }
+    ix->chain_len = len;
+    ix->chain_bytes = len * 128;
+    ix->chain_succ = (double)nsucc.load() / (double)m;
+    return 0;
+}
+
 // Probe structure, for ids that fit k_count3: wide tables when they fit SKQ_DIRECT_MB (default
 // 49152 MiB) and half the free device memory, else compact tables (a few % of the wide tables'
 // size); otherwise 4-B direct tables when they fit, else the bucket table alone.
@@ -681,8 +848,9 @@ uint32_t skq_threshold(double fraction) {
     return static_cast<uint32_t>(H * fraction);
 }
 
-int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
-                     const skq_kmer_table* tables, skq_index** out) {
+static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
+                             const skq_kmer_table* tables, const uint8_t* seqs, const uint64_t* seq_offs,
+                             uint32_t nseq, uint32_t threshold, skq_index** out) {
     if (!out) return fail(-1, "out is null");
     *out = nullptr;
     if (nk == 0 || nk > SKQ_MAX_K) return fail(-1, "k list must hold 1..SKQ_MAX_K entries");
@@ -828,8 +996,32 @@ int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, 
                     return rc2;
                 }
     }
+    // chained tables (one k slot, ids within 22 bits, transcripts given): SKQ_CHAIN = 0 turns them off
+    if (seqs && seq_offs && nk == 1 && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
+        (ix->mode == 3 || ix->mode == 5)) {
+        const char* e = std::getenv("SKQ_CHAIN");
+        if (!e || std::atoi(e) != 0)
+            for (uint32_t t = 0; t < ntables; ++t)
+                if (tables[t].k == ks[0])
+                    if (int rc2 = build_chain(ix, dkeys[t], dvals[t], lists, ks[0], seqs, seq_offs, nseq, threshold)) {
+                        skq_index_free(ix);
+                        return rc2;
+                    }
+    }
     *out = ix;
     return 0;
+}
+
+int skq_index_create(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
+                     const skq_kmer_table* tables, skq_index** out) {
+    return index_create_impl(device, ntx, nk, ks, ntables, tables, nullptr, nullptr, 0, 0, out);
+}
+
+int skq_index_create_chained(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
+                             const skq_kmer_table* tables, const uint8_t* seqs, const uint64_t* seq_offs,
+                             uint32_t nseq, uint32_t threshold, skq_index** out) {
+    if (nseq && (!seqs || !seq_offs)) return fail(-1, "null sequences");
+    return index_create_impl(device, ntx, nk, ks, ntables, tables, seqs, seq_offs, nseq, threshold, out);
 }
 
 int skq_index_free(skq_index* ix) {
@@ -844,6 +1036,7 @@ int skq_index_free(skq_index* ix) {
     dev_free(ix->d_pent);
     dev_free(ix->d_ppil);
     dev_free(ix->d_pdesc);
+    dev_free(ix->d_chain);
     dev_free(ix->d_buckets);
     dev_free(ix->d_lists);
     dev_free(ix->d_rolltab);
@@ -853,7 +1046,7 @@ int skq_index_free(skq_index* ix) {
 
 int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npostings, uint32_t* max_list) {
     if (!ix) return fail(-1, "null index");
-    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4 + ix->dir_bytes + ix->part_bytes;
+    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4 + ix->dir_bytes + ix->part_bytes + ix->chain_bytes;
     if (npostings) *npostings = ix->npostings;
     if (max_list) *max_list = ix->max_list;
     return 0;
@@ -883,6 +1076,7 @@ int skq_session_slow_counts(skq_session* s, uint32_t* counts) {
 
 int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? ix->mode : 0; }
 int skq_index_partitions(const skq_index* ix) { return ix ? (int)ix->part_np : 0; }
+double skq_index_chained(const skq_index* ix) { return ix && ix->d_chain ? 1.0 + ix->chain_succ : 0.0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
     if (!ix || !out) return fail(-1, "null argument");
@@ -1182,6 +1376,8 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
             p.wseed[i] = ix->wseed[i];
         }
     }
+    p.chain = reinterpret_cast<const uint32_t*>(ix->d_chain);
+    p.chain_len = ix->chain_len;
     p.stamps = s->stamps;
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;

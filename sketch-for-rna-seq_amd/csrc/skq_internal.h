@@ -171,6 +171,13 @@ struct ChainParams {
     const uint32_t* wdir[SKQ_MAX_K];
     uint64_t wdir_len[SKQ_MAX_K];
     const uint32_t* wovf[SKQ_MAX_K];
+    // chained tables (k_map1 TAB = 3, one k slot): a 128-B entry per possible key
+    // (chain_len of them, 8 uint4 each): word 0 = payload words used (0: no key), then records
+    // [key, n << 22 | t0, t1 .. t(n-1)] (n <= 7) or [key, 8 << 22, list offset], the entry's own
+    // key first, then keys that follow it along the transcripts (nearest first), each with its
+    // whole postings list: one 128-B request settles a run of a read's retained hashes
+    const uint32_t* chain;
+    uint64_t chain_len;
 };
 
 // Partitioned map (one k slot; k_part_a -> k_part_b -> k_part_c): the keys of the
@@ -220,6 +227,10 @@ int set_error(int code, const char* msg);
 int session_device(const skq_session* s);
 uint64_t session_max_reads(const skq_session* s);
 
+// host: one sequence's retained hashes at k in position order (repeats kept; ntHash's window
+// rules: windows holding a byte outside ACGTUacgtu skipped) (skq_tables.cpp)
+void sketch_positions(const uint8_t* s, uint64_t len, uint32_t k, uint32_t thr, std::vector<uint32_t>& out);
+constexpr uint32_t CHAIN_WORDS = 32;  // chained entry: 128 B
 // host: ascending sort with threads (skq_tables.cpp)
 void parallel_sort_u64(std::vector<uint64_t>& v, int threads);
 // host: tables from (key << 32 | tid) words per distinct k (consumed; duplicates removed)

@@ -1946,18 +1946,19 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // binning counts in wave 0's region, dead once every wave has counted; HCAP + 1 raw rows, the
 // last one the sink of windows past the capacity)
 constexpr uint32_t MAP_P = 384;
-__host__ __device__ inline size_t map1_wave_bytes(uint32_t wc) {
+constexpr uint32_t CHN_STAGE = 32 * CHAIN_WORDS * 4;  // chained tables: 32 entries staged per half-wave
+__host__ __device__ inline size_t map1_wave_bytes(uint32_t wc, bool chn = false) {
     const size_t a = sketch_codes_bytes(wc);
     // the list: hashes, then owning lanes (u8; compact tables: u32 slot | lane << 26), then the
-    // per-read overflow flags
-    const size_t b = (size_t)MAP_P * 8 + 64 * 4;
+    // per-read overflow flags (chained tables: 32 staged entries, then the flags)
+    const size_t b = (chn ? (size_t)CHN_STAGE : (size_t)MAP_P * 8) + 64 * 4;
     const size_t c = (size_t)(WG + 1) * 4;
     const size_t m = a > b ? a : b;
     return ((m > c ? m : c) + 15) & ~(size_t)15;
 }
 
-size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
-    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks) + ((size_t)hcap + 1) * WG * 4;
+size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap, bool chn = false) {
+    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks, chn) + ((size_t)hcap + 1) * WG * 4;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -1985,8 +1986,9 @@ size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap) {
 // binned as in the one-k map.
 template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
-    constexpr bool BLK = TAB == 1, CMP = TAB == 2;
+    constexpr bool BLK = TAB == 1, CMP = TAB == 2, CHN = TAB == 3;
     static_assert(PASS || !FINAL, "the final pass is a pass");
+    static_assert(!(CHN && PASS), "chained tables serve one k slot");
     const uint32_t ks = PASS ? p.kslot : 0u;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1994,7 +1996,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t lane = tid & 63, wv = tid >> 6;
     MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
-    const size_t wave_bytes = map1_wave_bytes(wc);
+    const size_t wave_bytes = map1_wave_bytes(wc, CHN);
     uint2* s_tab = reinterpret_cast<uint2*>(smem);
     const uint2* s_seed = s_tab + 16;
     unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
@@ -2099,6 +2101,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
     for (int j = 0; j < HCAP; ++j) v[j] = 0xFFFFFFFFu;
     uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
+    uint32_t nraw_out = 0;  // retained windows in the raw rows (position order), fast reads
     const bool hashing = live && !slow && !sk_prev && st == SKQ_READ_OK;
     if (hashing) {
         const uint32_t T = p.threshold;
@@ -2138,6 +2141,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         if (nraw > HCAP) {
             slow = true;
         } else {
+            nraw_out = nraw;
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
             bitonic_sort<HCAP>(v);
@@ -2188,9 +2192,17 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t off = incl - m;
     const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+    // chained tables: this lane's retained windows in position order (repeats kept), read from its
+    // own raw column before the count table overlays it
+    uint32_t pr[CHN ? HCAP : 1];
+    const uint32_t npr = CHN && act ? nraw_out : 0u;
+    if constexpr (CHN) {
+#pragma unroll
+        for (int j = 0; j < HCAP; ++j) pr[j] = (uint32_t)j < npr ? s_raw[j * WG + tid] : 0u;
+    }
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
-    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 8);  // per read: > TS transcripts
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + (CHN ? CHN_STAGE : MAP_P * 8));  // per read: > TS transcripts
     s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
@@ -2227,6 +2239,95 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         if ((old >> 8) == x) atomicAdd(a, 1u);
         else ains_probe(x, o);
     };
+    if constexpr (CHN) {
+        // chained tables: per round, every read with retained windows still unsettled fetches the
+        // entry of its first unsettled one (position order); the lane groups of 8 load 128-B
+        // entries cooperatively, 32 at a time through LDS; the owner then walks the entry's
+        // records and counts every record whose key it holds and has not counted (each distinct
+        // hash exactly once), marking all its windows of that key settled. A key absent from the
+        // table (no entry, or beyond the largest key) settles as a miss.
+        const uint4* ctab = reinterpret_cast<const uint4*>(cp.chain);
+        const uint64_t clen = cp.chain_len;
+        uint4* s_ent = reinterpret_cast<uint4*>(s_wave);
+        const uint32_t full = npr >= 32 ? 0xFFFFFFFFu : (1u << npr) - 1u;
+        uint32_t cov = 0;
+        auto match = [&](uint32_t key) -> uint32_t {
+            uint32_t mm = 0;
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) mm |= (pr[j] == key ? 1u : 0u) << j;
+            return mm & full;
+        };
+        // this lane's own table (no other lane inserts into it): plain LDS read-modify-write
+        auto own_ins = [&](uint32_t x) {
+            uint32_t sl = Counter<1, WG>::slot_of(x);
+#pragma unroll 1
+            for (int z = 0; z < TS; ++z) {
+                uint32_t* a = colbase + sl * WG + ((lane + sl) & 63u);
+                const uint32_t e = *a;
+                if (e == EMPTY) {
+                    *a = (x << 8) | 1u;
+                    return;
+                }
+                if ((e >> 8) == x) {
+                    *a = e + 1u;
+                    return;
+                }
+                sl = (sl + 1) & (TS - 1);
+            }
+            s_flag[lane] = 1u;  // more than TS distinct transcripts
+        };
+        while (__any(cov != full)) {  // wave-uniform
+            const bool want = cov != full;
+            const uint32_t qi = want ? (uint32_t)__builtin_ctz(~cov & full) : 0u;
+            uint32_t q = 0;
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) q = (uint32_t)j == qi ? pr[j] : q;
+            const int fetch = want && q < clen ? 1 : 0;
+#pragma unroll
+            for (uint32_t half = 0; half < 2; ++half) {
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u) {
+                    const uint32_t src = 32 * half + 8 * u + (lane >> 3);
+                    const uint32_t qs = __shfl(q, src, 64);
+                    uint4 x = make_uint4(0, 0, 0, 0);
+                    if (__shfl(fetch, src, 64)) x = ctab[(uint64_t)qs * 8 + (lane & 7u)];
+                    s_ent[(8 * u + (lane >> 3)) * 8 + (lane & 7u)] = x;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (want && (lane >> 5) == half) {
+                    const uint32_t* e = reinterpret_cast<const uint32_t*>(s_ent + (lane & 31u) * 8);
+                    const uint32_t nw = min(e[0], CHAIN_WORDS - 1u);
+                    uint32_t idx = 1;
+#pragma unroll 1
+                    while (idx + 1 <= nw) {
+                        const uint32_t K = e[idx], B = e[idx + 1], n = B >> 22;
+                        const uint32_t sz = n < CMP_LONG ? n + 1u : 3u;
+                        if (idx + sz - 1 > nw) break;
+                        const uint32_t mm = match(K);
+                        if (mm & ~cov) {
+                            if (n < CMP_LONG) {
+                                own_ins(B & TID_MASK);
+#pragma unroll 1
+                                for (uint32_t t2 = 1; t2 < n; ++t2) own_ins(e[idx + 1 + t2]);
+                            } else {  // a list longer than 7: from lists[]
+                                const uint32_t lo = e[idx + 2], ln = cp.lists[lo];
+#pragma unroll 1
+                                for (uint32_t t2 = 0; t2 < ln; ++t2) own_ins(cp.lists[lo + 1 + t2]);
+                            }
+                        }
+                        cov |= mm;
+                        idx += sz;
+                    }
+                    cov |= match(q);  // the query is settled (counted above, or a miss)
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+    } else {
     // the first pass's list, straight from the sorted registers (v dies here)
     {
         uint32_t rank = 0;
@@ -2428,6 +2529,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
         }
     }
+    }  // (TAB != 3)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -3991,10 +4093,13 @@ int launch_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* cont
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    const size_t lds = map1_lds_bytes(p.tile_chunks, p.hcap);
+    const bool chn = cp.chain != nullptr;
+    const size_t lds = map1_lds_bytes(p.tile_chunks, p.hcap, chn);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // (MB: gather rounds in flight)
-    switch (p.hcap * 4 + (cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
+    switch (p.hcap * 4 + (chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
+    case 67: hipLaunchKernelGGL((k_map1<16, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
+    case 131: hipLaunchKernelGGL((k_map1<32, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
     case 64: hipLaunchKernelGGL((k_map1<16, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
     case 65: hipLaunchKernelGGL((k_map1<16, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
     case 66: hipLaunchKernelGGL((k_map1<16, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;

@@ -73,6 +73,12 @@ void sort_unique(std::vector<uint32_t>& v) {
 }  // namespace
 
 namespace skq {
+void sketch_positions(const uint8_t* s, uint64_t len, uint32_t k, uint32_t thr, std::vector<uint32_t>& out) {
+    uint64_t rk[4];
+    for (int c = 0; c < 4; ++c) rk[c] = rot33(SEED33[c], k);
+    sketch_into(s, len, k, thr, rk, out);
+}
+
 // Sorts ascending with up to `threads` threads: sorted chunks, then rounds of pairwise merges.
 // Input that is already sorted (the product's own index files) costs one pass.
 void parallel_sort_u64(std::vector<uint64_t>& v, int threads) {

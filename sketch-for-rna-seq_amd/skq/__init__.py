@@ -53,6 +53,8 @@ def lib():
             "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
             "skq_index_direct": (i32, [vp]),
             "skq_index_partitions": (i32, [vp]),
+            "skq_index_chained": (C.c_double, [vp]),
+            "skq_index_create_chained": (i32, [i32, u32, u32, vp, u32, vp, vp, vp, u32, u32, C.POINTER(vp)]),
             "skq_session_slow_reads": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
             "skq_session_slow_counts": (i32, [vp, C.POINTER(u32)]),
             "skq_session_create": (i32, [vp, u64, u32, C.POINTER(vp)]),
@@ -190,7 +192,9 @@ class DeviceBuffer:
 class Index:
     """Device-resident inverted index. tables: {k: (keys u32 asc, offs u64 [nkeys+1], tids u32)}."""
 
-    def __init__(self, ks, ntx, tables, device=0):
+    def __init__(self, ks, ntx, tables, device=0, seqs=None, thr=None):
+        """seqs = (flat bytes, offs[ntx + 1]): the transcripts the tables were built from; with
+        one k they add the chained tables (skq_index_create_chained), sketched at thr."""
         self.ks = [int(k) for k in ks]
         self.ntx = int(ntx)
         self.device = device
@@ -204,8 +208,15 @@ class Index:
             arr[j] = _KmerTable(int(k), len(keys), _p(keys), _p(offs), _p(tids))
         ka = np.array(self.ks, np.uint32)
         self.h = C.c_void_p()
-        _check(lib().skq_index_create(device, self.ntx, len(self.ks), _p(ka), len(tables),
-                                      C.cast(arr, C.c_void_p), C.byref(self.h)))
+        if seqs is None:
+            _check(lib().skq_index_create(device, self.ntx, len(self.ks), _p(ka), len(tables),
+                                          C.cast(arr, C.c_void_p), C.byref(self.h)))
+        else:
+            sb = np.ascontiguousarray(seqs[0], np.uint8)
+            so = np.ascontiguousarray(seqs[1], np.uint64)
+            _check(lib().skq_index_create_chained(device, self.ntx, len(self.ks), _p(ka), len(tables),
+                                                  C.cast(arr, C.c_void_p), _p(sb), _p(so), len(so) - 1,
+                                                  threshold() if thr is None else thr, C.byref(self.h)))
         self._keep = None
 
     def stats(self):
@@ -214,7 +225,8 @@ class Index:
         return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
                     direct=bool(lib().skq_index_direct(self.h)),
                     probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 4: "block", 5: "compact"}[lib().skq_index_direct(self.h)],
-                    partitions=lib().skq_index_partitions(self.h))
+                    partitions=lib().skq_index_partitions(self.h),
+                    chained=lib().skq_index_chained(self.h))
 
     def free(self):
         if self.h:

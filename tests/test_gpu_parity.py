@@ -15,10 +15,11 @@ from skq import synth
 
 pytestmark = pytest.mark.gpu
 SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the wide-split mode)
+CHAINED = False  # build: indexes from sequences get the chained tables (skq_index_create_chained)
 
 
-@pytest.fixture(autouse=True, params=["part", "part-compact", "compact", "compact-split", "block", "wide",
-                                      "wide-split", "dir", "rank", "bucket"])
+@pytest.fixture(autouse=True, params=["chain", "chain-compact", "part", "part-compact", "compact", "compact-split",
+                                      "block", "wide", "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
     """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables,
     block tables and wide direct tables gathered by the map or count kernel, 4-B direct and rank
@@ -28,7 +29,12 @@ def probe_mode(request, monkeypatch):
     "part-compact" over compact tables; indexes it does not apply to (several k) run as wide /
     compact."""
     monkeypatch.setenv("SKQ_PART", "0")
-    if request.param.startswith("part"):
+    if request.param.startswith("chain"):
+        # chained tables (one k, indexes built from sequences) over wide / compact tables
+        monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
+        monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "chain-compact" else "wide")
+        monkeypatch.setattr(sys.modules[__name__], "CHAINED", True)
+    elif request.param.startswith("part"):
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
         monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "part-compact" else "wide")
         monkeypatch.setenv("SKQ_PART", "1")
@@ -62,7 +68,8 @@ def build(ks, seqs=None, tx=None, pairs=None, ntx=None):
         seqs = [tx.seq(t) for t in range(tx.ntx)]
     buf, offs = skq.pack_reads(seqs)
     tables = skq.build_tables(buf, offs, ks)
-    return skq.Index(ks, len(seqs), tables), orc.Index(ks, seqs=seqs)
+    return (skq.Index(ks, len(seqs), tables, seqs=(buf, offs) if CHAINED else None),
+            orc.Index(ks, seqs=seqs))
 
 
 def run_gpu(index, reads, fixed_len=0, fraction=0.9, thr=None, max_len=None):
@@ -116,12 +123,15 @@ def totals_from(ref, n, ntx):
 def test_probe_mode_is_selected(tx300, probe_mode):
     gi, _ = build([21, 31], tx=tx300)
     st = gi.stats()
-    base = {"part": "wide", "part-compact": "compact"}.get(probe_mode, probe_mode.split("-")[0])
+    base = {"part": "wide", "part-compact": "compact", "chain": "wide", "chain-compact": "compact"}.get(
+        probe_mode, probe_mode.split("-")[0])
     assert st["probe"] == base
     assert st["device_bytes"] > 0
     assert st["partitions"] == 0  # (several k: no partitioned tables)
+    assert st["chained"] == 0  # (several k: no chained tables)
     gi1, _ = build([31], tx=tx300)
     assert (gi1.stats()["partitions"] > 0) == probe_mode.startswith("part")
+    assert (gi1.stats()["chained"] > 1) == probe_mode.startswith("chain")
 
 
 @pytest.fixture(scope="module")
@@ -511,7 +521,7 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     s.check()
     s.enable_timing(False)
     count_launches = s.kernel_time(2)[1]
-    if probe_mode in ("wide", "compact", "part", "part-compact"):
+    if probe_mode in ("wide", "compact", "part", "part-compact", "chain", "chain-compact"):
         assert count_launches == 0 and s.kernel_time(0)[1] == 1
     else:
         assert count_launches == 1

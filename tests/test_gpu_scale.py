@@ -74,9 +74,9 @@ def _compare(out, tot, cpu, nk):
     np.testing.assert_array_equal(tot[1], cpu["tx_score"])
 
 
-def _case(tx, ks, L, nreads, seed, err=0.001):
+def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
     tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=NTHREADS)
-    index = skq.Index(ks, tx.ntx, tables)
+    index = skq.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs) if chained else None)
     bases, _, _ = synth.reads(tx, nreads, L, seed=seed, err=err)
     # a sprinkle of edge reads at scale: invalid bases and lowercase
     rng = np.random.default_rng(seed)
@@ -94,20 +94,21 @@ def _case(tx, ks, L, nreads, seed, err=0.001):
     return cpu, st, slow
 
 
-@pytest.mark.parametrize("part", ["0", "1"], ids=["map1", "part"])
-def test_cfg2_10k_transcripts_100bp(tx10k, part, monkeypatch):
-    monkeypatch.setenv("SKQ_PART", part)
-    cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201)
+@pytest.mark.parametrize("mode", ["map1", "part", "chain"])
+def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
+    monkeypatch.setenv("SKQ_PART", "1" if mode == "part" else "0")
+    cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode == "chain")
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
 
 
-@pytest.mark.parametrize("part", ["0", "1"], ids=["map1", "part"])
-def test_cfg3_200k_transcripts_150bp(tx200k, part, monkeypatch):
-    """part = 1: the partitioned map (k_part_a/b/c) over the same index."""
-    monkeypatch.setenv("SKQ_PART", part)
-    cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301)
-    assert (st["partitions"] > 50) == (part == "1"), st
+@pytest.mark.parametrize("mode", ["map1", "part", "chain"])
+def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
+    """part: the partitioned map (k_part_a/b/c); chain: k_map1 over the chained tables."""
+    monkeypatch.setenv("SKQ_PART", "1" if mode == "part" else "0")
+    cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode == "chain")
+    assert (st["partitions"] > 50) == (mode == "part"), st
+    assert (st["chained"] > 2) == (mode == "chain"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert st["max_list"] >= 10  # GENCODE-scale postings (long lists take the inline overflow)
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed

@@ -71,8 +71,10 @@ __global__ void gather_coop(const uint32_t* __restrict__ tab, uint64_t mask, uin
 }
 
 template <int C>
-int run_coop(uint64_t max_mb, uint32_t* out, uint64_t n, hipEvent_t a, hipEvent_t b) {
-    for (uint64_t mb : {256ull, 512ull, 1024ull, 2048ull, 8192ull}) {
+int run_coop(uint64_t max_mb, uint32_t* out, uint64_t n, hipEvent_t a, hipEvent_t b, bool big = false) {
+    const std::vector<uint64_t> sizes = big ? std::vector<uint64_t>{544, 1024, 8192, 16384, 28672}
+                                            : std::vector<uint64_t>{256, 512, 1024, 2048, 8192};
+    for (uint64_t mb : sizes) {
         if (mb > max_mb) break;
         const uint64_t bytes = mb << 20, entries = bytes / (16 * C);
         uint32_t* tab;
@@ -132,6 +134,10 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    if (argc > 2 && argv[2][0] == 'b') {  // 128-B entries (chained tables) up to 28 GiB: TLB reach
+        if (run_coop<8>(max_mb, out, n, a, b, true) || run_coop<2>(max_mb, out, n, a, b, true)) return 1;
+        return 0;
+    }
     if (argc > 2) {  // coop only
         if (run_coop<2>(max_mb, out, n, a, b) || run_coop<4>(max_mb, out, n, a, b)) return 1;
         return 0;
