@@ -50,6 +50,13 @@ int skq_tables_free(skq_tables* t);
 /* convenience: upload built tables; ks = the k list in CLI order */
 int skq_index_from_tables(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks,
                           const skq_tables* t, skq_index** out);
+/* the same with the chained tables (skq_index_create_chained) from the transcripts' sequences in
+ * tx (the tables' transcripts, dense ids in tx order), sketched at threshold; tx without
+ * sequences (null, or names only): as skq_index_from_tables */
+struct skq_seqs;
+int skq_index_from_tables_chained(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks,
+                                  const skq_tables* t, const struct skq_seqs* tx, uint32_t threshold,
+                                  skq_index** out);
 
 /* Single-sequence sketch on the host, used on the index side (transcripts): sorted unique
  * retained hashes, ntHash semantics. out needs len-k+1 slots. Returns the count, or -1 if

@@ -616,12 +616,18 @@ __global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* e
 
 int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
                 const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
-                uint32_t nseq, uint32_t threshold) {
+                uint32_t nseq, uint32_t threshold, bool force) {
     const uint64_t m = keys.size();
     if (m == 0) return 0;
     const uint64_t len = (uint64_t)keys.back() + 1;
+    // 128 B per possible key: built when it fits half the free memory and, unless forced, when
+    // the keys fill at least 1/128 of their range (200k transcripts: 1/51, 27.5 GB; a 10k-transcript
+    // index would spend 27 GB on 217k keys)
+    uint64_t budget = 65536ull << 20;
+    if (const char* e = std::getenv("SKQ_CHAIN_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || len * 128 > fr / 2) return 0;  // (does not fit: no chains)
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || len * 128 > fr / 2 || len * 128 > budget) return 0;
+    if (!force && len > 128 * m) return 0;
     const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // (key, successor, hop) triples, bucketed by key range, one sort per bucket
     constexpr uint32_t NB = 256;
@@ -996,14 +1002,17 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
                     return rc2;
                 }
     }
-    // chained tables (one k slot, ids within 22 bits, transcripts given): SKQ_CHAIN = 0 turns them off
+    // chained tables (one k slot, ids within 22 bits, transcripts given): SKQ_CHAIN = 0 turns them
+    // off, 1 builds them whatever the key density (build_chain)
     if (seqs && seq_offs && nk == 1 && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
         (ix->mode == 3 || ix->mode == 5)) {
         const char* e = std::getenv("SKQ_CHAIN");
-        if (!e || std::atoi(e) != 0)
+        const int cm = e ? std::atoi(e) : -1;
+        if (cm != 0)
             for (uint32_t t = 0; t < ntables; ++t)
                 if (tables[t].k == ks[0])
-                    if (int rc2 = build_chain(ix, dkeys[t], dvals[t], lists, ks[0], seqs, seq_offs, nseq, threshold)) {
+                    if (int rc2 = build_chain(ix, dkeys[t], dvals[t], lists, ks[0], seqs, seq_offs, nseq, threshold,
+                                              cm == 1)) {
                         skq_index_free(ix);
                         return rc2;
                     }

@@ -100,8 +100,11 @@ struct Part {
     uint8_t* d_assigned = nullptr;
     std::string err;
 
-    void map(const std::string& reads_path, uint32_t ntx, uint32_t nk, const uint32_t* ks, const skq_tables* tabs) {
-        check(skq_index_from_tables(dev, ntx, nk, ks, tabs, &ix), "device index");
+    void map(const std::string& reads_path, uint32_t ntx, uint32_t nk, const uint32_t* ks, const skq_tables* tabs,
+             const skq_seqs* tx) {
+        // (one k: the chained tables from the index's transcripts)
+        check(skq_index_from_tables_chained(dev, ntx, nk, ks, tabs, tx, skq_threshold((double)kSketchSize), &ix),
+              "device index");
         uint64_t batch = 1u << 21;  // reads per batch (2M and 64-MiB chunks: tools/ingest_bench.py sweep)
         if (const char* e = std::getenv("SKQ_BATCH")) batch = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
         check(skq_session_create(ix, batch, 256, &s), "session");
@@ -251,10 +254,10 @@ void quantification(const std::string& index_path, const std::string& reads_path
     {
         std::vector<std::thread> ts;
         for (Part& p : parts)
-            ts.emplace_back([&p, &reads_path, ntx, nk, ks, tabs] {
+            ts.emplace_back([&p, &reads_path, ntx, nk, ks, tabs, tx] {
                 try {
                     hip_check(hipSetDevice(p.dev), "device");
-                    p.map(reads_path, ntx, nk, ks, tabs);
+                    p.map(reads_path, ntx, nk, ks, tabs, tx);
                 } catch (const std::exception& e) {
                     p.err = e.what();
                 }

@@ -403,7 +403,7 @@ int skq_legacy_index_write(const char* path, uint32_t nk, const uint32_t* ks, co
 // to the legacy file whenever the stamp does not match.
 namespace {
 
-constexpr char kSidecarMagic[8] = {'S', 'K', 'Q', 'I', 'D', 'X', '0', '1'};
+constexpr char kSidecarMagic[8] = {'S', 'K', 'Q', 'I', 'D', 'X', '0', '2'};  // 02: with sequences
 
 std::string sidecar_path(const char* legacy) { return std::string(legacy) + ".skq"; }
 
@@ -440,6 +440,10 @@ int skq_sidecar_write(const char* legacy_path, uint32_t nk, const uint32_t* ks, 
     w.u64(tx->names.size());
     w.raw(tx->names.data(), tx->names.size());
     w.raw(tx->name_offs.data(), (ntx + 1) * 8);
+    // the sequences (quant's chained tables follow the transcripts: skq_index_create_chained)
+    w.u64(tx->bytes.size());
+    w.raw(tx->bytes.data(), tx->bytes.size());
+    w.raw(tx->offs.data(), (ntx + 1) * 8);
     const uint32_t nt = skq_tables_count(tables);
     w.u64(nt);
     for (uint32_t i = 0; i < nt; ++i) {
@@ -593,7 +597,16 @@ int skq_index_open(const char* path, skq_legacy_index** out, int* from_sidecar) 
                     r.raw(ix->tx.names.data(), nb);
                     ix->tx.name_offs.resize(ntx + 1);
                     r.raw(ix->tx.name_offs.data(), (ntx + 1) * 8);
-                    ix->tx.offs.assign(ntx + 1, 0);  // no sequences
+                    const uint64_t sb = r.u64();
+                    if (r.ok && sb <= f.n) {
+                        ix->tx.bytes.resize(sb);
+                        r.raw(ix->tx.bytes.data(), sb);
+                        ix->tx.offs.resize(ntx + 1);
+                        r.raw(ix->tx.offs.data(), (ntx + 1) * 8);
+                        r.ok = r.ok && ix->tx.offs[0] == 0 && ix->tx.offs[ntx] == sb;
+                    } else {
+                        r.ok = false;
+                    }
                 } else {
                     r.ok = false;
                 }

@@ -274,4 +274,19 @@ int skq_index_from_tables(int device, uint32_t ntx, uint32_t nk, const uint32_t*
     return skq_index_create(device, ntx, nk, ks, (uint32_t)v.size(), v.data(), out);
 }
 
+int skq_index_from_tables_chained(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, const skq_tables* t,
+                                  const skq_seqs* tx, uint32_t threshold, skq_index** out) {
+    if (!t) return hfail(-1, "null tables");
+    std::vector<skq_kmer_table> v(t->t.size());
+    for (uint32_t i = 0; i < v.size(); ++i) skq_tables_get(t, i, &v[i]);
+    const uint8_t* bytes = nullptr;
+    const uint64_t* offs = nullptr;
+    const uint64_t n = tx ? skq_seqs_count(tx) : 0;
+    if (tx) skq_seqs_view(tx, &bytes, &offs, nullptr, nullptr);
+    if (!tx || n == 0 || offs[n] == 0)  // (no sequences: nothing to chain)
+        return skq_index_create(device, ntx, nk, ks, (uint32_t)v.size(), v.data(), out);
+    return skq_index_create_chained(device, ntx, nk, ks, (uint32_t)v.size(), v.data(), bytes, offs, (uint32_t)n,
+                                    threshold, out);
+}
+
 }  // extern "C"

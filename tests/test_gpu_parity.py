@@ -33,6 +33,7 @@ def probe_mode(request, monkeypatch):
         # chained tables (one k, indexes built from sequences) over wide / compact tables
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
         monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "chain-compact" else "wide")
+        monkeypatch.setenv("SKQ_CHAIN", "1")  # (small test indexes: whatever the key density)
         monkeypatch.setattr(sys.modules[__name__], "CHAINED", True)
     elif request.param.startswith("part"):
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")

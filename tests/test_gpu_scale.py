@@ -97,6 +97,7 @@ def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
 @pytest.mark.parametrize("mode", ["map1", "part", "chain"])
 def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
     monkeypatch.setenv("SKQ_PART", "1" if mode == "part" else "0")
+    monkeypatch.setenv("SKQ_CHAIN", "1")  # (a 10k-transcript index: below the automatic key density)
     cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode == "chain")
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
