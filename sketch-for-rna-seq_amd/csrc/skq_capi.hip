@@ -600,12 +600,14 @@ int build_part(skq_index* ix, const std::vector<uint32_t>& keys, const std::vect
 // Chained tables for one k slot (ChainParams::chain). The transcripts are sketched in position
 // order (the index's own hashing: skq::sketch_positions); every retained k-mer's successors within
 // CHAIN_HOPS retained positions in any transcript are candidates for its entry, nearest first
-// (ties: smaller key); each candidate's record carries its WHOLE postings list from the index's
-// own tables (lists[] through the key's list offset), so whatever a record settles is exactly
-// what a lookup of that key would have returned. Records are added while they fit in 31 words.
-// The entries (one per present key) are built on the host and scattered on the device into a
-// table of 128-B entries for every possible key up to the largest (27.5 GB at (double)0.05f and
-// 4.24M keys: HBM3E holds it; one 128-B request per lookup, no key hashing).
+// (ties: smaller key). An entry is 8 slots of 16 B: records [key, n << 22 | t0, t1, t2] (a list
+// of 4-7 continues in the next slot as [t3, t4, t5, t6]; longer: [key, 8 << 22, list offset, 0]),
+// the key's own record first, then successors while slots remain. Each record carries its key's
+// WHOLE postings list from the index's own tables (lists[] through the key's list offset), so
+// whatever a record settles is exactly what a lookup of that key returns. The entries (one per
+// present key) are built on the host and scattered on the device into a table of 128-B entries
+// for every possible key up to the largest (27.5 GB at (double)0.05f and 4.24M keys: HBM3E holds
+// it; one 128-B request per lookup, no key hashing).
 constexpr uint32_t CHAIN_HOPS = 8;
 
 __global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* ent, uint64_t n) {
@@ -658,6 +660,7 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
         for (auto& t : pool) t.join();
     }
     std::vector<uint32_t> ent(m * skq::CHAIN_WORDS, 0);
+    std::vector<uint8_t> built(m, 0);
     std::atomic<uint64_t> nsucc{0};
     {
         std::atomic<uint32_t> next{0};
@@ -670,20 +673,21 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
                     const auto it = std::lower_bound(keys.begin(), keys.end(), key);
                     return it != keys.end() && *it == key ? (int64_t)(it - keys.begin()) : -1;
                 };
-                // one record: [key, n << 22 | t0, t1 ..] or [key, 8 << 22, offset]; false: no room
+                // one record in slots (4 words each); false: no room
                 auto put = [&](uint32_t* e, uint32_t& used, uint32_t key, uint32_t off) -> bool {
                     const uint32_t n = lists[off];
-                    const uint32_t words = n <= 7 ? n + 1 : 3;
-                    if (used + words > skq::CHAIN_WORDS) return false;
-                    e[used] = key;
+                    const uint32_t slots = (n >= 4 && n <= 7) ? 2u : 1u;
+                    if (used + slots > skq::CHAIN_WORDS / 4) return false;
+                    uint32_t* w = e + 4 * used;
+                    w[0] = key;
                     if (n <= 7) {
-                        e[used + 1] = (n << 22) | lists[off + 1];
-                        for (uint32_t q = 1; q < n; ++q) e[used + 1 + q] = lists[off + 1 + q];
+                        w[1] = (n << 22) | lists[off + 1];
+                        for (uint32_t q = 1; q < n; ++q) w[1 + q] = lists[off + 1 + q];  // (t3.. run into the next slot)
                     } else {
-                        e[used + 1] = skq::CMP_LONG << 22;
-                        e[used + 2] = off;
+                        w[1] = skq::CMP_LONG << 22;
+                        w[2] = off;
                     }
-                    used += words;
+                    used += slots;
                     return true;
                 };
                 for (uint32_t b; (b = next.fetch_add(1)) < NB;) {
@@ -694,20 +698,19 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
                         size_t j = i;
                         while (j < c.size() && c[j].h == c[i].h) ++j;
                         const int64_t x = index_of(c[i].h);
-                        if (x >= 0) {
+                        if (x >= 0 && !built[x]) {
                             uint32_t* e = ent.data() + (uint64_t)x * skq::CHAIN_WORDS;
-                            uint32_t used = 1;
-                            if (e[0] == 0 && put(e, used, c[i].h, vals[x])) {  // the key's own record first
-                                std::vector<uint32_t> seen;
-                                for (size_t q = i; q < j; ++q) {
-                                    if (std::find(seen.begin(), seen.end(), c[q].g) != seen.end()) continue;
-                                    seen.push_back(c[q].g);
-                                    const int64_t y = index_of(c[q].g);
-                                    if (y < 0) continue;
-                                    if (!put(e, used, c[q].g, vals[y])) break;
-                                    ++ns;
-                                }
-                                e[0] = used - 1;
+                            uint32_t used = 0;
+                            put(e, used, c[i].h, vals[x]);  // the key's own record first (always fits)
+                            built[x] = 1;
+                            std::vector<uint32_t> seen;
+                            for (size_t q = i; q < j; ++q) {
+                                if (std::find(seen.begin(), seen.end(), c[q].g) != seen.end()) continue;
+                                seen.push_back(c[q].g);
+                                const int64_t y = index_of(c[q].g);
+                                if (y < 0) continue;
+                                if (!put(e, used, c[q].g, vals[y])) break;
+                                ++ns;
                             }
                         }
                         i = j;
@@ -720,18 +723,16 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
     }
     // keys no transcript of `seqs` retained still get their own record
     for (uint64_t x = 0; x < m; ++x) {
+        if (built[x]) continue;
         uint32_t* e = ent.data() + x * skq::CHAIN_WORDS;
-        if (e[0]) continue;
         const uint32_t off = vals[x], n = lists[off];
-        e[1] = keys[x];
+        e[0] = keys[x];
         if (n <= 7) {
-            e[2] = (n << 22) | lists[off + 1];
-            for (uint32_t q = 1; q < n; ++q) e[2 + q] = lists[off + 1 + q];
-            e[0] = n + 1;
+            e[1] = (n << 22) | lists[off + 1];
+            for (uint32_t q = 1; q < n; ++q) e[1 + q] = lists[off + 1 + q];
         } else {
-            e[2] = skq::CMP_LONG << 22;
-            e[3] = off;
-            e[0] = 3;
+            e[1] = skq::CMP_LONG << 22;
+            e[2] = off;
         }
     }
     uint32_t* dk = nullptr;
@@ -1005,7 +1006,7 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
     // chained tables (one k slot, ids within 22 bits, transcripts given): SKQ_CHAIN = 0 turns them
     // off, 1 builds them whatever the key density (build_chain)
     if (seqs && seq_offs && nk == 1 && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
-        (ix->mode == 3 || ix->mode == 5)) {
+        ix->mode == 3) {  // (the entry list behind the chain step gathers wide entries)
         const char* e = std::getenv("SKQ_CHAIN");
         const int cm = e ? std::atoi(e) : -1;
         if (cm != 0)

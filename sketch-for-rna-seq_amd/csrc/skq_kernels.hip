@@ -1946,19 +1946,21 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // binning counts in wave 0's region, dead once every wave has counted; HCAP + 1 raw rows, the
 // last one the sink of windows past the capacity)
 constexpr uint32_t MAP_P = 384;
-constexpr uint32_t CHN_STAGE = 32 * CHAIN_WORDS * 4;  // chained tables: 32 entries staged per half-wave
-__host__ __device__ inline size_t map1_wave_bytes(uint32_t wc, bool chn = false) {
+// chained tables: the wave's reads' retained hashes ([64][hcap]), kept masks and counted masks
+// before the per-read overflow flags
+__host__ __device__ inline size_t chn_flag_at(uint32_t hcap) { return (size_t)64 * hcap * 4 + 512; }
+__host__ __device__ inline size_t map1_wave_bytes(uint32_t wc, bool chn = false, uint32_t hcap = 16) {
     const size_t a = sketch_codes_bytes(wc);
     // the list: hashes, then owning lanes (u8; compact tables: u32 slot | lane << 26), then the
-    // per-read overflow flags (chained tables: 32 staged entries, then the flags)
-    const size_t b = (chn ? (size_t)CHN_STAGE : (size_t)MAP_P * 8) + 64 * 4;
+    // per-read overflow flags (chained tables: chn_flag_at)
+    const size_t b = (chn ? chn_flag_at(hcap) : (size_t)MAP_P * 8) + 64 * 4;
     const size_t c = (size_t)(WG + 1) * 4;
     const size_t m = a > b ? a : b;
     return ((m > c ? m : c) + 15) & ~(size_t)15;
 }
 
 size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap, bool chn = false) {
-    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks, chn) + ((size_t)hcap + 1) * WG * 4;
+    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks, chn, hcap) + ((size_t)hcap + 1) * WG * 4;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -1996,7 +1998,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t lane = tid & 63, wv = tid >> 6;
     MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
-    const size_t wave_bytes = map1_wave_bytes(wc, CHN);
+    const size_t wave_bytes = map1_wave_bytes(wc, CHN, HCAP);
     uint2* s_tab = reinterpret_cast<uint2*>(smem);
     const uint2* s_seed = s_tab + 16;
     unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
@@ -2187,22 +2189,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // (pass mode: a k slot the index has no table for is sketched but not counted,
     // src/sparse_chaining.cpp:51-53)
     const bool act = hashing && !slow && (!PASS || cp.tabs[ks].present);
-    const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
-    const uint32_t incl = wave_incl_scan(m, lane);
-    const uint32_t off = incl - m;
-    const uint32_t M = __shfl(incl, 63, 64);  // the wave's retained hashes
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
-    // chained tables: this lane's retained windows in position order (repeats kept), read from its
-    // own raw column before the count table overlays it
-    uint32_t pr[CHN ? HCAP : 1];
-    const uint32_t npr = CHN && act ? nraw_out : 0u;
-    if constexpr (CHN) {
-#pragma unroll
-        for (int j = 0; j < HCAP; ++j) pr[j] = (uint32_t)j < npr ? s_raw[j * WG + tid] : 0u;
-    }
+    // chained tables: the read's first retained window (position order) is its chain query, read
+    // from its own raw column before the count table overlays it
+    const uint32_t cq = CHN && act && nraw_out ? s_raw[tid] : 0u;
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
-    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + (CHN ? CHN_STAGE : MAP_P * 8));  // per read: > TS transcripts
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + (CHN ? chn_flag_at(HCAP) : MAP_P * 8));  // per read: > TS transcripts
     s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
@@ -2240,94 +2233,105 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         else ains_probe(x, o);
     };
     if constexpr (CHN) {
-        // chained tables: per round, every read with retained windows still unsettled fetches the
-        // entry of its first unsettled one (position order); the lane groups of 8 load 128-B
-        // entries cooperatively, 32 at a time through LDS; the owner then walks the entry's
-        // records and counts every record whose key it holds and has not counted (each distinct
-        // hash exactly once), marking all its windows of that key settled. A key absent from the
-        // table (no entry, or beyond the largest key) settles as a miss.
+        // chained tables, one request per read (ChainParams::chain): the entry of the read's first
+        // retained window holds 8 slots of 16 B — records [key, n << 22 | t0, t1, t2] (a list of
+        // 4-7 continues in the next slot as [t3, t4, t5, t6]; n = 8: [key, 8 << 22, list offset]),
+        // the window's own record first, then those of the keys that follow it in the transcripts.
+        // Lane group g of 8 loads the entry of read 8u + g, one slot per lane, u = 0..7; a lane
+        // matches its record's key against the owner's distinct retained hashes (LDS) and, on a
+        // match, inserts the record's tids into the owner's count table (the CAS inserts below)
+        // and marks the hash counted. What is left goes through the entry list as before.
         const uint4* ctab = reinterpret_cast<const uint4*>(cp.chain);
         const uint64_t clen = cp.chain_len;
-        uint4* s_ent = reinterpret_cast<uint4*>(s_wave);
-        const uint32_t full = npr >= 32 ? 0xFFFFFFFFu : (1u << npr) - 1u;
-        uint32_t cov = 0;
-        auto match = [&](uint32_t key) -> uint32_t {
-            uint32_t mm = 0;
+        uint32_t* s_vals = reinterpret_cast<uint32_t*>(s_wave);          // [64][HCAP]: v, per read
+        uint32_t* s_keep = s_vals + 64 * HCAP;                            // [64]: keepm, per read
+        uint32_t* s_cov = s_keep + 64;                                    // [64]: hashes counted
 #pragma unroll
-            for (int j = 0; j < HCAP; ++j) mm |= (pr[j] == key ? 1u : 0u) << j;
-            return mm & full;
-        };
-        // this lane's own table (no other lane inserts into it): plain LDS read-modify-write
-        auto own_ins = [&](uint32_t x) {
-            uint32_t sl = Counter<1, WG>::slot_of(x);
+        for (int j = 0; j < HCAP; ++j) s_vals[lane * HCAP + j] = v[j];
+        s_keep[lane] = act ? (uint32_t)keepm : 0u;
+        s_cov[lane] = 0u;
+        s_flag[lane] = 0;
+        const int has_q = act && nraw_out ? 1 : 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t slot = lane & 7u;
 #pragma unroll 1
-            for (int z = 0; z < TS; ++z) {
-                uint32_t* a = colbase + sl * WG + ((lane + sl) & 63u);
-                const uint32_t e = *a;
-                if (e == EMPTY) {
-                    *a = (x << 8) | 1u;
-                    return;
-                }
-                if ((e >> 8) == x) {
-                    *a = e + 1u;
-                    return;
-                }
-                sl = (sl + 1) & (TS - 1);
+        for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t o = 8 * u + (lane >> 3);  // the owner: this wave's read 8u + g
+            const uint32_t qo = __shfl(cq, o, 64);
+            const int ho = __shfl(has_q, o, 64);
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (ho && qo < clen) x = ctab[(uint64_t)qo * 8 + slot];
+            const uint32_t n = x.y >> 22;
+            const uint32_t nprev = __shfl_up(n, 1, 64);
+            // the owner's distinct retained hashes
+            uint32_t ov[HCAP];
+#pragma unroll
+            for (int j = 0; j < HCAP; j += 4) {
+                const uint4 w4 = *reinterpret_cast<const uint4*>(s_vals + o * HCAP + j);
+                ov[j] = w4.x;
+                ov[j + 1] = w4.y;
+                ov[j + 2] = w4.z;
+                ov[j + 3] = w4.w;
             }
-            s_flag[lane] = 1u;  // more than TS distinct transcripts
-        };
-        while (__any(cov != full)) {  // wave-uniform
-            const bool want = cov != full;
-            const uint32_t qi = want ? (uint32_t)__builtin_ctz(~cov & full) : 0u;
-            uint32_t q = 0;
+            const uint32_t okeep = s_keep[o];
+            auto match = [&](uint32_t key) -> uint32_t {
+                uint32_t mm = 0;
 #pragma unroll
-            for (int j = 0; j < HCAP; ++j) q = (uint32_t)j == qi ? pr[j] : q;
-            const int fetch = want && q < clen ? 1 : 0;
+                for (int j = 0; j < HCAP; ++j) mm |= (ov[j] == key ? 1u : 0u) << j;
+                return mm & okeep;
+            };
+            const bool head = ho && n >= 1;
+            const uint32_t mm = head ? match(x.x) : 0u;
+            const bool hit = mm != 0;
+            const bool cont = ho && slot > 0 && n == 0 && nprev >= 4 && nprev <= 7;
+            const bool chit = __shfl_up(hit ? 1 : 0, 1, 64) != 0 && cont;
+            // the inserts: a head's t0..t2, a continuation's t3..t6 (first attempts together)
+            uint32_t xs[4];
+            bool vs[4];
+            xs[0] = cont ? x.x : x.y & TID_MASK;
+            xs[1] = cont ? x.y : x.z;
+            xs[2] = cont ? x.z : x.w;
+            xs[3] = x.w;
+            vs[0] = (hit && n <= 7) || chit;
+            vs[1] = (hit && n >= 2 && n <= 7) || (chit && nprev >= 5);
+            vs[2] = (hit && n >= 3 && n <= 7) || (chit && nprev >= 6);
+            vs[3] = chit && nprev >= 7;
+            uint32_t olds[4];
 #pragma unroll
-            for (uint32_t half = 0; half < 2; ++half) {
-#pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
-                    const uint32_t src = 32 * half + 8 * u + (lane >> 3);
-                    const uint32_t qs = __shfl(q, src, 64);
-                    uint4 x = make_uint4(0, 0, 0, 0);
-                    if (__shfl(fetch, src, 64)) x = ctab[(uint64_t)qs * 8 + (lane & 7u)];
-                    s_ent[(8 * u + (lane >> 3)) * 8 + (lane & 7u)] = x;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (want && (lane >> 5) == half) {
-                    const uint32_t* e = reinterpret_cast<const uint32_t*>(s_ent + (lane & 31u) * 8);
-                    const uint32_t nw = min(e[0], CHAIN_WORDS - 1u);
-                    uint32_t idx = 1;
-#pragma unroll 1
-                    while (idx + 1 <= nw) {
-                        const uint32_t K = e[idx], B = e[idx + 1], n = B >> 22;
-                        const uint32_t sz = n < CMP_LONG ? n + 1u : 3u;
-                        if (idx + sz - 1 > nw) break;
-                        const uint32_t mm = match(K);
-                        if (mm & ~cov) {
-                            if (n < CMP_LONG) {
-                                own_ins(B & TID_MASK);
-#pragma unroll 1
-                                for (uint32_t t2 = 1; t2 < n; ++t2) own_ins(e[idx + 1 + t2]);
-                            } else {  // a list longer than 7: from lists[]
-                                const uint32_t lo = e[idx + 2], ln = cp.lists[lo];
-#pragma unroll 1
-                                for (uint32_t t2 = 0; t2 < ln; ++t2) own_ins(cp.lists[lo + 1 + t2]);
-                            }
-                        }
-                        cov |= mm;
-                        idx += sz;
-                    }
-                    cov |= match(q);  // the query is settled (counted above, or a miss)
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+                olds[q] = vs[q] ? atomicCAS(colbase + sl * WG + ((o + sl) & 63u), EMPTY, (xs[q] << 8) | 1u) : EMPTY;
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t xq = xs[q], sl = Counter<1, WG>::slot_of(xq), ol = olds[q];
+                if (ol == EMPTY) continue;
+                if ((ol >> 8) == xq) atomicAdd(colbase + sl * WG + ((o + sl) & 63u), 1u);
+                else ains_probe(xq, o);
+            }
+            const bool lng = hit && n == CMP_LONG;  // a list longer than 7 (rare): all of it from lists[]
+            if (__any(lng) && lng) {
+                const uint32_t lo = x.z, len = cp.lists[lo];
+                for (uint32_t q = 0; q < len; ++q) ains(cp.lists[lo + 1 + q], o);
+            }
+            // counted: the matched hash; slot 0 also settles the query itself (a key the table
+            // lacks is a miss, whatever the entry)
+            const uint32_t done = mm | (ho && slot == 0 ? match(qo) : 0u);
+            if (done) atomicOr(s_cov + o, done);
         }
-    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        keepm &= ~(uint64_t)s_cov[lane];
+    }
+    // the wave's entry list: every retained hash not counted above
+    const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
+    const uint32_t incl = wave_incl_scan(m, lane);
+    const uint32_t off = incl - m;
+    const uint32_t M = __shfl(incl, 63, 64);
+    {
     // the first pass's list, straight from the sorted registers (v dies here)
     {
         uint32_t rank = 0;
@@ -2529,7 +2533,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
         }
     }
-    }  // (TAB != 3)
+    }  // (the entry list)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

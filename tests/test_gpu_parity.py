@@ -18,7 +18,7 @@ SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the 
 CHAINED = False  # build: indexes from sequences get the chained tables (skq_index_create_chained)
 
 
-@pytest.fixture(autouse=True, params=["chain", "chain-compact", "part", "part-compact", "compact", "compact-split",
+@pytest.fixture(autouse=True, params=["chain", "part", "part-compact", "compact", "compact-split",
                                       "block", "wide", "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
     """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables,
@@ -30,9 +30,9 @@ def probe_mode(request, monkeypatch):
     compact."""
     monkeypatch.setenv("SKQ_PART", "0")
     if request.param.startswith("chain"):
-        # chained tables (one k, indexes built from sequences) over wide / compact tables
+        # chained tables (one k, indexes built from sequences) over wide tables
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
-        monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "chain-compact" else "wide")
+        monkeypatch.setenv("SKQ_PROBE", "wide")
         monkeypatch.setenv("SKQ_CHAIN", "1")  # (small test indexes: whatever the key density)
         monkeypatch.setattr(sys.modules[__name__], "CHAINED", True)
     elif request.param.startswith("part"):
@@ -124,7 +124,7 @@ def totals_from(ref, n, ntx):
 def test_probe_mode_is_selected(tx300, probe_mode):
     gi, _ = build([21, 31], tx=tx300)
     st = gi.stats()
-    base = {"part": "wide", "part-compact": "compact", "chain": "wide", "chain-compact": "compact"}.get(
+    base = {"part": "wide", "part-compact": "compact", "chain": "wide"}.get(
         probe_mode, probe_mode.split("-")[0])
     assert st["probe"] == base
     assert st["device_bytes"] > 0
@@ -522,7 +522,7 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     s.check()
     s.enable_timing(False)
     count_launches = s.kernel_time(2)[1]
-    if probe_mode in ("wide", "compact", "part", "part-compact", "chain", "chain-compact"):
+    if probe_mode in ("wide", "compact", "part", "part-compact", "chain"):
         assert count_launches == 0 and s.kernel_time(0)[1] == 1
     else:
         assert count_launches == 1

@@ -29,6 +29,9 @@ ap.add_argument("--k", type=int, default=31)
 ap.add_argument("--hops", default="1,2,4,6,8,12")
 ap.add_argument("--words", default="16,32,64")
 ap.add_argument("--both", action="store_true", help="neighbours on both sides; queries in value order")
+ap.add_argument("--single", action="store_true", help="word layout, one chain request per read, the rest one each")
+ap.add_argument("--slots", type=int, default=0, help="slot layout: N slots of 4 words (a list of <= 3 tids takes one "
+                "slot, 4-7 two, longer one); one chain request per read, the rest one request per hash")
 a = ap.parse_args()
 T = orc.threshold()
 
@@ -52,6 +55,8 @@ print("retained per read %.2f (distinct %.2f)" % (np.mean([len(r) for r in rr]),
 
 def rec_words(h):
     n = len(post[h])
+    if a.slots:
+        return 1 if (n <= 3 or n > 7) else 2
     return 1 + (n if n <= 7 else 1)
 
 
@@ -67,7 +72,7 @@ for H in [int(x) for x in a.hops.split(",")]:
                     g = r[j]
                     if g != h and (g not in succ[h] or succ[h][g] > d):
                         succ[h][g] = d
-    for W in [int(x) for x in a.words.split(",")]:
+    for W in ([a.slots] if a.slots else [int(x) for x in a.words.split(",")]):
         cover = {}
         full = 0
         for h in post:
@@ -85,6 +90,13 @@ for H in [int(x) for x in a.hops.split(",")]:
         for r in rr:
             left = set(r)
             n = 0
+            if a.slots or a.single:  # one chain request (the first retained hash), then one per uncovered hash
+                if r:
+                    left -= cover.get(r[0], {r[0]})
+                    left.discard(r[0])
+                    n = 1 + len(left)
+                req.append(n)
+                continue
             for h in (sorted(set(r)) if a.both else r):  # position order (value order with --both)
                 if h not in left:
                     continue

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --ti
 tail -2 gpurun_out/${t}_parity.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread -k "chain" > gpurun_out/${t}_scale.log 2>&1 || { echo "scale failed"; tail -40 gpurun_out/${t}_scale.log; exit 1; }
 tail -2 gpurun_out/${t}_scale.log
-timeout -k 10 400 python -u tools/kbench.py --probes wide,wide/chain,compact/chain --rounds 5 > gpurun_out/${t}_kbench.log 2>&1 || { echo "kbench failed"; tail -30 gpurun_out/${t}_kbench.log; exit 1; }
+timeout -k 10 400 python -u tools/kbench.py --probes wide,wide/chain --rounds 5 > gpurun_out/${t}_kbench.log 2>&1 || { echo "kbench failed"; tail -30 gpurun_out/${t}_kbench.log; exit 1; }
 grep -v "^setup" gpurun_out/${t}_kbench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${t}_stats -o run -- python3 tools/kbench.py --probes wide/chain --rounds 3 > gpurun_out/${t}_stats.log 2>&1 || { echo "rocprof failed"; exit 1; }
 echo "stats ok"
