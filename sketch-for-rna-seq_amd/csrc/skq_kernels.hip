@@ -2189,6 +2189,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // (pass mode: a k slot the index has no table for is sketched but not counted,
     // src/sparse_chaining.cpp:51-53)
     const bool act = hashing && !slow && (!PASS || cp.tabs[ks].present);
+    const uint64_t keepm_all = keepm;  // the read's distinct retained hashes (as written out)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
     // chained tables: the read's first retained window (position order) is its chain query, read
     // from its own raw column before the count table overlays it
@@ -2327,6 +2328,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         keepm &= ~(uint64_t)s_cov[lane];
     }
     // the wave's entry list: every retained hash not counted above
+    const uint64_t keep0 = keepm_all;
     const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
     const uint32_t incl = wave_incl_scan(m, lane);
     const uint32_t off = incl - m;
@@ -2352,14 +2354,22 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (pb) {  // (rare: more than MAP_P hashes in the wave) this lane's hashes, as written above
-#pragma unroll 1
-            for (uint32_t d = 0; d < m; ++d) {
-                const uint32_t e = off + d;
-                if (e >= pb && e < pb + MAP_P) {
-                    s_h[e - pb] = p.hashes[((uint64_t)ks * p.hcap + d) * p.n + r];
-                    if (CMP) s_x[e - pb] = lane << 26;
-                    else s_own[e - pb] = (uint8_t)lane;
+            // (the d-th listed hash is the d-th still in keepm; its place among the read's written
+            // hashes is its rank in keep0, which differs once the chain step counted some)
+            uint32_t d = 0, rank = 0;
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) {
+                if (!((keep0 >> j) & 1ull)) continue;
+                if ((keepm >> j) & 1ull) {
+                    const uint32_t e = off + d;
+                    if (e >= pb && e < pb + MAP_P) {
+                        s_h[e - pb] = p.hashes[((uint64_t)ks * p.hcap + rank) * p.n + r];
+                        if (CMP) s_x[e - pb] = lane << 26;
+                        else s_own[e - pb] = (uint8_t)lane;
+                    }
+                    ++d;
                 }
+                ++rank;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
