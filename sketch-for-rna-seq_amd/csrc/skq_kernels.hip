@@ -2257,13 +2257,28 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t slot = lane & 7u;
+        // all of the lane's slot loads in flight together (CHN_BATCH owners at a time), then each
+        // slot's record matched and inserted
+        constexpr uint32_t CB = 4;
 #pragma unroll 1
-        for (uint32_t u = 0; u < 8; ++u) {
-            const uint32_t o = 8 * u + (lane >> 3);  // the owner: this wave's read 8u + g
-            const uint32_t qo = __shfl(cq, o, 64);
-            const int ho = __shfl(has_q, o, 64);
-            uint4 x = make_uint4(0, 0, 0, 0);
-            if (ho && qo < clen) x = ctab[(uint64_t)qo * 8 + slot];
+        for (uint32_t u0 = 0; u0 < 8; u0 += CB) {
+        uint4 xb[CB];
+        uint32_t qb[CB];
+        int hb[CB];
+#pragma unroll
+        for (uint32_t w = 0; w < CB; ++w) {
+            const uint32_t o = 8 * (u0 + w) + (lane >> 3);
+            qb[w] = __shfl(cq, o, 64);
+            hb[w] = __shfl(has_q, o, 64);
+            xb[w] = make_uint4(0, 0, 0, 0);
+            if (hb[w] && qb[w] < clen) xb[w] = ctab[(uint64_t)qb[w] * 8 + slot];
+        }
+#pragma unroll
+        for (uint32_t w = 0; w < CB; ++w) {
+            const uint32_t o = 8 * (u0 + w) + (lane >> 3);  // the owner: this wave's read 8u + g
+            const uint32_t qo = qb[w];
+            const int ho = hb[w];
+            const uint4 x = xb[w];
             const uint32_t n = x.y >> 22;
             const uint32_t nprev = __shfl_up(n, 1, 64);
             // the owner's distinct retained hashes
@@ -2321,6 +2336,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             // lacks is a miss, whatever the entry)
             const uint32_t done = mm | (ho && slot == 0 ? match(qo) : 0u);
             if (done) atomicOr(s_cov + o, done);
+        }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
