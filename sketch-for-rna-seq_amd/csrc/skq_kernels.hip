@@ -2259,7 +2259,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         const uint32_t slot = lane & 7u;
         // all of the lane's slot loads in flight together (CHN_BATCH owners at a time), then each
         // slot's record matched and inserted
-        constexpr uint32_t CB = 4;
+        constexpr uint32_t CB = MB >= 8 ? 8 : 4;
 #pragma unroll 1
         for (uint32_t u0 = 0; u0 < 8; u0 += CB) {
         uint4 xb[CB];
@@ -4128,8 +4128,10 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // (MB: gather rounds in flight)
     switch (p.hcap * 4 + (chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
-    case 67: hipLaunchKernelGGL((k_map1<16, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
-    case 131: hipLaunchKernelGGL((k_map1<32, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
+    // (chained tables: every chain-slot load of the lane in flight at once (CB = 8) and 8 rounds
+    // of the remaining entry list, one memory round trip each for a wave)
+    case 67: hipLaunchKernelGGL((k_map1<16, 8, 3>), grid, dim3(WG), lds, st, p, cp); break;
+    case 131: hipLaunchKernelGGL((k_map1<32, 8, 3>), grid, dim3(WG), lds, st, p, cp); break;
     case 64: hipLaunchKernelGGL((k_map1<16, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
     case 65: hipLaunchKernelGGL((k_map1<16, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
     case 66: hipLaunchKernelGGL((k_map1<16, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;
