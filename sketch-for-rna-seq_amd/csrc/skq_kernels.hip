@@ -1946,9 +1946,9 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // binning counts in wave 0's region, dead once every wave has counted; HCAP + 1 raw rows, the
 // last one the sink of windows past the capacity)
 constexpr uint32_t MAP_P = 384;
-// chained tables: the wave's reads' retained hashes ([64][hcap]), kept masks and counted masks
-// before the per-read overflow flags
-__host__ __device__ inline size_t chn_flag_at(uint32_t hcap) { return (size_t)64 * hcap * 4 + 512; }
+// chained tables: the wave's entries' record keys ([64][8]) and hit masks ([64]) before the
+// per-read overflow flags
+__host__ __device__ inline size_t chn_flag_at(uint32_t) { return (size_t)64 * 8 * 4 + 256; }
 __host__ __device__ inline size_t map1_wave_bytes(uint32_t wc, bool chn = false, uint32_t hcap = 16) {
     const size_t a = sketch_codes_bytes(wc);
     // the list: hashes, then owning lanes (u8; compact tables: u32 slot | lane << 26), then the
@@ -2244,104 +2244,109 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // and marks the hash counted. What is left goes through the entry list as before.
         const uint4* ctab = reinterpret_cast<const uint4*>(cp.chain);
         const uint64_t clen = cp.chain_len;
-        uint32_t* s_vals = reinterpret_cast<uint32_t*>(s_wave);          // [64][HCAP]: v, per read
-        uint32_t* s_keep = s_vals + 64 * HCAP;                            // [64]: keepm, per read
-        uint32_t* s_cov = s_keep + 64;                                    // [64]: hashes counted
-#pragma unroll
-        for (int j = 0; j < HCAP; ++j) s_vals[lane * HCAP + j] = v[j];
-        s_keep[lane] = act ? (uint32_t)keepm : 0u;
-        s_cov[lane] = 0u;
+        uint32_t* s_keys = reinterpret_cast<uint32_t*>(s_wave);  // [64 owners][8 slots]: record keys
+        uint32_t* s_hit = s_keys + 64 * 8;                         // [64 owners]: slots whose key it holds
         s_flag[lane] = 0;
         const int has_q = act && nraw_out ? 1 : 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t slot = lane & 7u;
-        // all of the lane's slot loads in flight together (CHN_BATCH owners at a time), then each
-        // slot's record matched and inserted
-        constexpr uint32_t CB = MB >= 8 ? 8 : 4;
+        // the owner's side: which of its retained hashes a key is (keepm bits)
+        auto match = [&](uint32_t key) -> uint32_t {
+            uint32_t mm = 0;
+#pragma unroll
+            for (int j = 0; j < HCAP; ++j) mm |= (v[j] == key ? 1u : 0u) << j;
+            return mm & (uint32_t)keepm;
+        };
+        uint32_t cov = 0;
+        // two batches of 4 owner rounds: half of the wave's reads each
 #pragma unroll 1
-        for (uint32_t u0 = 0; u0 < 8; u0 += CB) {
-        uint4 xb[CB];
-        uint32_t qb[CB];
-        int hb[CB];
+        for (uint32_t u0 = 0; u0 < 8; u0 += 4) {
+            uint4 xb[4];
+            uint64_t heads[4];
 #pragma unroll
-        for (uint32_t w = 0; w < CB; ++w) {
-            const uint32_t o = 8 * (u0 + w) + (lane >> 3);
-            qb[w] = __shfl(cq, o, 64);
-            hb[w] = __shfl(has_q, o, 64);
-            xb[w] = make_uint4(0, 0, 0, 0);
-            if (hb[w] && qb[w] < clen) xb[w] = ctab[(uint64_t)qb[w] * 8 + slot];
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint32_t o = 8 * (u0 + w) + (lane >> 3);
+                const uint32_t qo = __shfl(cq, o, 64);
+                const int ho = __shfl(has_q, o, 64);
+                xb[w] = make_uint4(0, 0, 0, 0);
+                if (ho && qo < clen) xb[w] = ctab[(uint64_t)qo * 8 + slot];
+            }
+#pragma unroll
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint32_t o = 8 * (u0 + w) + (lane >> 3);
+                const bool head = (xb[w].y >> 22) != 0;  // (empty slots and continuations: 0)
+                heads[w] = __ballot(head);
+                s_keys[o * 8 + slot] = xb[w].x;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // owners of this batch (lanes 8 u0 .. 8 u0 + 31): match the entry's record keys
+            if ((lane >> 5) == (u0 >> 2)) {
+                const uint32_t w = (lane >> 3) & 3u;  // this owner's round in the batch
+                const uint64_t hw = w == 0 ? heads[0] : w == 1 ? heads[1] : w == 2 ? heads[2] : heads[3];
+                const uint32_t hm = (uint32_t)(hw >> (8 * (lane & 7u))) & 0xFFu;
+                const uint4 k0 = *reinterpret_cast<const uint4*>(s_keys + lane * 8);
+                const uint4 k1 = *reinterpret_cast<const uint4*>(s_keys + lane * 8 + 4);
+                const uint32_t kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+                uint32_t hit = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {  // (an entry's keys are distinct: each counted once)
+                    const uint32_t mm = (hm >> q) & 1u ? match(kk[q]) : 0u;
+                    hit |= mm ? (1u << q) : 0u;
+                    cov |= mm;
+                }
+                // the query is settled by its own record, or is a miss (no entry)
+                if (has_q) cov |= match(cq);
+                s_hit[lane] = has_q ? hit : 0u;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the slot lanes insert the matched records' tids into the owners' count tables
+#pragma unroll
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint32_t o = 8 * (u0 + w) + (lane >> 3);
+                const uint4 x = xb[w];
+                const uint32_t n = x.y >> 22;
+                const uint32_t nprev = __shfl_up(n, 1, 64);
+                const uint32_t hm = s_hit[o];
+                const bool hit = (hm >> slot) & 1u;
+                const bool cont = slot > 0 && n == 0 && nprev >= 4 && nprev <= 7;
+                const bool chit = cont && ((hm >> (slot - 1)) & 1u);
+                uint32_t xs[4];
+                bool vs[4];
+                xs[0] = cont ? x.x : x.y & TID_MASK;
+                xs[1] = cont ? x.y : x.z;
+                xs[2] = cont ? x.z : x.w;
+                xs[3] = x.w;
+                vs[0] = (hit && n <= 7) || chit;
+                vs[1] = (hit && n >= 2 && n <= 7) || (chit && nprev >= 5);
+                vs[2] = (hit && n >= 3 && n <= 7) || (chit && nprev >= 6);
+                vs[3] = chit && nprev >= 7;
+                uint32_t olds[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+                    olds[q] = vs[q] ? atomicCAS(colbase + sl * WG + ((o + sl) & 63u), EMPTY, (xs[q] << 8) | 1u) : EMPTY;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t xq = xs[q], sl = Counter<1, WG>::slot_of(xq), ol = olds[q];
+                    if (ol == EMPTY) continue;
+                    if ((ol >> 8) == xq) atomicAdd(colbase + sl * WG + ((o + sl) & 63u), 1u);
+                    else ains_probe(xq, o);
+                }
+                const bool lng = hit && n == CMP_LONG;  // a list longer than 7 (rare): all of it from lists[]
+                if (__any(lng) && lng) {
+                    const uint32_t lo = x.z, len = cp.lists[lo];
+                    for (uint32_t q = 0; q < len; ++q) ains(cp.lists[lo + 1 + q], o);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-#pragma unroll
-        for (uint32_t w = 0; w < CB; ++w) {
-            const uint32_t o = 8 * (u0 + w) + (lane >> 3);  // the owner: this wave's read 8u + g
-            const uint32_t qo = qb[w];
-            const int ho = hb[w];
-            const uint4 x = xb[w];
-            const uint32_t n = x.y >> 22;
-            const uint32_t nprev = __shfl_up(n, 1, 64);
-            // the owner's distinct retained hashes
-            uint32_t ov[HCAP];
-#pragma unroll
-            for (int j = 0; j < HCAP; j += 4) {
-                const uint4 w4 = *reinterpret_cast<const uint4*>(s_vals + o * HCAP + j);
-                ov[j] = w4.x;
-                ov[j + 1] = w4.y;
-                ov[j + 2] = w4.z;
-                ov[j + 3] = w4.w;
-            }
-            const uint32_t okeep = s_keep[o];
-            auto match = [&](uint32_t key) -> uint32_t {
-                uint32_t mm = 0;
-#pragma unroll
-                for (int j = 0; j < HCAP; ++j) mm |= (ov[j] == key ? 1u : 0u) << j;
-                return mm & okeep;
-            };
-            const bool head = ho && n >= 1;
-            const uint32_t mm = head ? match(x.x) : 0u;
-            const bool hit = mm != 0;
-            const bool cont = ho && slot > 0 && n == 0 && nprev >= 4 && nprev <= 7;
-            const bool chit = __shfl_up(hit ? 1 : 0, 1, 64) != 0 && cont;
-            // the inserts: a head's t0..t2, a continuation's t3..t6 (first attempts together)
-            uint32_t xs[4];
-            bool vs[4];
-            xs[0] = cont ? x.x : x.y & TID_MASK;
-            xs[1] = cont ? x.y : x.z;
-            xs[2] = cont ? x.z : x.w;
-            xs[3] = x.w;
-            vs[0] = (hit && n <= 7) || chit;
-            vs[1] = (hit && n >= 2 && n <= 7) || (chit && nprev >= 5);
-            vs[2] = (hit && n >= 3 && n <= 7) || (chit && nprev >= 6);
-            vs[3] = chit && nprev >= 7;
-            uint32_t olds[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
-                olds[q] = vs[q] ? atomicCAS(colbase + sl * WG + ((o + sl) & 63u), EMPTY, (xs[q] << 8) | 1u) : EMPTY;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t xq = xs[q], sl = Counter<1, WG>::slot_of(xq), ol = olds[q];
-                if (ol == EMPTY) continue;
-                if ((ol >> 8) == xq) atomicAdd(colbase + sl * WG + ((o + sl) & 63u), 1u);
-                else ains_probe(xq, o);
-            }
-            const bool lng = hit && n == CMP_LONG;  // a list longer than 7 (rare): all of it from lists[]
-            if (__any(lng) && lng) {
-                const uint32_t lo = x.z, len = cp.lists[lo];
-                for (uint32_t q = 0; q < len; ++q) ains(cp.lists[lo + 1 + q], o);
-            }
-            // counted: the matched hash; slot 0 also settles the query itself (a key the table
-            // lacks is a miss, whatever the entry)
-            const uint32_t done = mm | (ho && slot == 0 ? match(qo) : 0u);
-            if (done) atomicOr(s_cov + o, done);
-        }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        keepm &= ~(uint64_t)s_cov[lane];
+        keepm &= ~(uint64_t)cov;
     }
     // the wave's entry list: every retained hash not counted above
     const uint64_t keep0 = keepm_all;
@@ -4128,10 +4133,8 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // (MB: gather rounds in flight)
     switch (p.hcap * 4 + (chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
-    // (chained tables: every chain-slot load of the lane in flight at once (CB = 8) and 8 rounds
-    // of the remaining entry list, one memory round trip each for a wave)
-    case 67: hipLaunchKernelGGL((k_map1<16, 8, 3>), grid, dim3(WG), lds, st, p, cp); break;
-    case 131: hipLaunchKernelGGL((k_map1<32, 8, 3>), grid, dim3(WG), lds, st, p, cp); break;
+    case 67: hipLaunchKernelGGL((k_map1<16, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
+    case 131: hipLaunchKernelGGL((k_map1<32, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
     case 64: hipLaunchKernelGGL((k_map1<16, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
     case 65: hipLaunchKernelGGL((k_map1<16, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
     case 66: hipLaunchKernelGGL((k_map1<16, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;
