@@ -77,20 +77,14 @@ int skq_index_stats(const skq_index* idx, uint64_t* device_bytes, uint64_t* npos
  * bucket table) and half the free device memory is built; SKQ_PROBE = wide | dir | rank forces
  * one kind. */
 int skq_index_direct(const skq_index* ix);
-/* Partitions of the partitioned map's tables (0: none). With one k slot, ids within 22 bits and
- * wide or compact tables, SKQ_PART=1 at index creation adds per-key-range compact tables small
- * enough for one XCD's L2; skq_map then runs the partitioned map (k_part_a: sketch + the retained
- * hashes grouped by key range; k_part_b: the lookups of one key range per workgroup, on one XCD;
- * k_part_c: the per-read vote), identical results. */
-int skq_index_partitions(const skq_index* ix);
-
 /* skq_index_create plus, for an index of one k whose transcripts are given (seqs[seq_offs[t] ..
  * seq_offs[t+1]), the sequences the tables were built from, sketched at `threshold`), chained
  * tables: per possible key a 128-B entry holding its postings list and those of the keys that
  * follow it along the transcripts (nearest first, whole lists). skq_map then settles a read's
- * retained hashes with about 1.5 entry requests instead of one per hash; results
- * are identical (a record is used only for its exact key). SKQ_CHAIN=0 leaves them out. Other
- * indexes: as skq_index_create. */
+ * retained hashes with one entry request plus one per hash the entry does not hold (2.6 instead
+ * of 6 at cfg3); results are identical (a record is used only for its exact key).
+ * Built only with SKQ_CHAIN=1 in the environment (measured 2 % faster at cfg3, for 27.5 GB);
+ * otherwise, and for other indexes: as skq_index_create. */
 int skq_index_create_chained(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
                              const skq_kmer_table* tables, const uint8_t* seqs, const uint64_t* seq_offs,
                              uint32_t nseq, uint32_t threshold, skq_index** out);

@@ -78,14 +78,6 @@ struct skq_index {
     const uint16_t* wpil[SKQ_MAX_K] = {};
     uint32_t wnb[SKQ_MAX_K] = {}, wseed[SKQ_MAX_K] = {};
     uint64_t dir_bytes = 0;
-    // partitioned tables (one k slot: the partitioned map, k_part_*; skq_internal.h PartParams):
-    // key >> part_shift -> partition, each with its own compact table; beside the probe kind below,
-    // which the slow paths and skq_chain keep using
-    uint32_t* d_pent = nullptr;
-    uint16_t* d_ppil = nullptr;
-    skq::PartDesc* d_pdesc = nullptr;
-    uint32_t part_shift = 0, part_np = 0, part_npx = 0;
-    uint64_t part_bytes = 0;
     // chained tables (one k slot; ChainParams::chain): a 128-B entry per possible key up to the
     // largest, carrying the key's postings list and those of the keys that follow it in the
     // transcripts; k_map1 then settles a read with ~1.5 entry requests instead of one per hash
@@ -142,11 +134,6 @@ struct skq_session {
     uint32_t bin_par = 0;
     uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
     uint32_t* ktab = nullptr;    // multi-k map by passes: per-k count tables (allocated on first use)
-    // the partitioned map's workspace (allocated on first use, for raw capacity part_hcap)
-    uint32_t* part_pairs = nullptr;
-    uint16_t* part_poff = nullptr;
-    uint32_t* part_out = nullptr;
-    uint32_t part_hcap = 0;
     uint8_t* kcnt = nullptr;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
@@ -496,107 +483,6 @@ int build_compact(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
 }
 
 
-// Partitioned tables for the partitioned map (one k slot): the keys split by key >> shift into
-// np <= 256 partitions of ~40k keys (a compact table of ~1.35 MB each: a third of one XCD's 4 MB
-// L2), each placed by its own minimal perfect hash (mph_place) with the compact entry format.
-// The shift also bounds the pair words of k_part_a: shift + 8 lane bits <= 32.
-int build_part(skq_index* ix, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
-               const std::vector<uint32_t>& lists) {
-    const uint64_t m = keys.size();
-    if (m == 0) return 0;
-    uint64_t target = std::max<uint64_t>(1, (m + 39999) / 40000);
-    if (const char* e = std::getenv("SKQ_PART_KEYS")) target = std::max<uint64_t>(1, m / std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)));
-    const uint64_t maxkey = keys.back();  // (ascending)
-    uint32_t shift = 0;
-    while (shift < 24 && (maxkey >> shift) + 1 > target) ++shift;
-    while ((maxkey >> shift) + 1 > skq::PART_MAX_NP) ++shift;
-    if (shift > 24) return 0;
-    const uint32_t np = (uint32_t)(maxkey >> shift) + 1, npx = (np + 7) & ~7u;
-    std::vector<uint64_t> kb(np + 1);
-    for (uint32_t q = 0; q < np; ++q)
-        kb[q] = (uint64_t)(std::lower_bound(keys.begin(), keys.end(), (uint32_t)((uint64_t)q << shift)) - keys.begin());
-    kb[np] = m;
-    std::vector<std::vector<uint32_t>> ent(np);
-    std::vector<std::vector<uint16_t>> pil(np);
-    std::vector<skq::PartDesc> desc(npx);
-    std::vector<int> bad(np, 0);
-    auto build = [&](uint32_t q) {
-        const uint64_t a = kb[q], z = kb[q + 1], mq = z - a;
-        const std::vector<uint32_t> sub(keys.begin() + (ptrdiff_t)a, keys.begin() + (ptrdiff_t)z);
-        const uint64_t nslots = std::max<uint64_t>(mq + 1, (uint64_t)std::ceil((double)mq / 0.95));
-        const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (mq + 4) / 5);
-        std::vector<uint32_t> slot;
-        uint32_t seed = 0x5EED5EEDu ^ (q * 0x9E3779B9u);
-        int tries = 0;
-        while (!mph_place(sub, seed, nslots, nb, pil[q], slot)) {
-            if (++tries == 16) {
-                bad[q] = 1;
-                return;
-            }
-            seed = skq::cmp_mix(seed + 0x9E3779B9u);
-        }
-        ent[q].assign(nslots * 8, 0);
-        for (uint64_t j = 0; j < mq; ++j) {
-            const uint32_t off = vals[a + j], n = lists[off];
-            uint32_t* e = ent[q].data() + (uint64_t)slot[j] * 8;
-            e[0] = sub[j];
-            for (uint32_t u = 0; u < 7 && u < n; ++u) e[1 + u] = lists[off + 1 + u];
-            e[1] |= std::min<uint32_t>(n, skq::CMP_LONG) << 22;
-            if (n > 7) {
-                e[4] |= (off & 0x3FFu) << 22;
-                e[5] |= ((off >> 10) & 0x3FFu) << 22;
-                e[6] |= ((off >> 20) & 0x3FFu) << 22;
-                e[7] |= (off >> 30) << 22;
-            }
-        }
-        desc[q].nslots = (uint32_t)nslots;
-        desc[q].nb = nb;
-        desc[q].seed = seed;
-    };
-    {
-        const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        std::atomic<uint32_t> next{0};
-        std::vector<std::thread> pool;
-        for (uint32_t w = 0; w < P; ++w)
-            pool.emplace_back([&] {
-                for (uint32_t q; (q = next.fetch_add(1)) < np;) build(q);
-            });
-        for (auto& t : pool) t.join();
-    }
-    for (uint32_t q = 0; q < np; ++q)
-        if (bad[q]) return fail(-1, "partitioned table placement failed");
-    uint64_t ns = 0, nbt = 0;
-    for (uint32_t q = 0; q < npx; ++q) {
-        if (q >= np) {  // padding partitions: never served (k_part_b skips them), kept valid
-            desc[q].nslots = 1;
-            desc[q].nb = 1;
-        }
-        desc[q].ent_base = (uint32_t)ns;
-        desc[q].pil_base = (uint32_t)nbt;
-        ns += desc[q].nslots;
-        nbt += desc[q].nb;
-    }
-    if (ns >= (1ull << 32) / 8) return fail(-1, "index too large for partitioned tables");
-    std::vector<uint32_t> all(ns * 8, 0);
-    std::vector<uint16_t> allp(nbt, 0);
-    for (uint32_t q = 0; q < np; ++q) {
-        std::copy(ent[q].begin(), ent[q].end(), all.begin() + (ptrdiff_t)desc[q].ent_base * 8);
-        std::copy(pil[q].begin(), pil[q].end(), allp.begin() + desc[q].pil_base);
-    }
-    if (dev_alloc(&ix->d_pent, all.size()) || dev_alloc(&ix->d_ppil, allp.size()) || dev_alloc(&ix->d_pdesc, desc.size()))
-        return fail(-3, "partitioned table allocation failed");
-    if (hipMemcpy(ix->d_pent, all.data(), all.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ix->d_ppil, allp.data(), allp.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ix->d_pdesc, desc.data(), desc.size() * sizeof(skq::PartDesc), hipMemcpyHostToDevice) != hipSuccess)
-        return fail(-3, "partitioned table upload failed");
-    ix->part_shift = shift;
-    ix->part_np = np;
-    ix->part_npx = npx;
-    ix->part_bytes = all.size() * 4 + allp.size() * 2 + desc.size() * sizeof(skq::PartDesc);
-    return 0;
-}
-
-
 // Chained tables for one k slot (ChainParams::chain). The transcripts are sketched in position
 // order (the index's own hashing: skq::sketch_positions); every retained k-mer's successors within
 // CHAIN_HOPS retained positions in any transcript are candidates for its entry, nearest first
@@ -618,18 +504,15 @@ __global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* e
 
 int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
                 const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
-                uint32_t nseq, uint32_t threshold, bool force) {
+                uint32_t nseq, uint32_t threshold) {
     const uint64_t m = keys.size();
     if (m == 0) return 0;
     const uint64_t len = (uint64_t)keys.back() + 1;
-    // 128 B per possible key: built when it fits half the free memory and, unless forced, when
-    // the keys fill at least 1/128 of their range (200k transcripts: 1/51, 27.5 GB; a 10k-transcript
-    // index would spend 27 GB on 217k keys)
+    // 128 B per possible key, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
     uint64_t budget = 65536ull << 20;
     if (const char* e = std::getenv("SKQ_CHAIN_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || len * 128 > fr / 2 || len * 128 > budget) return 0;
-    if (!force && len > 128 * m) return 0;
     const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // (key, successor, hop) triples, bucketed by key range, one sort per bucket
     constexpr uint32_t NB = 256;
@@ -989,31 +872,16 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
         skq_index_free(ix);
         return rc2;
     }
-    // the partitioned map's tables (one k slot, ids within 22 bits, beside wide or compact tables
-    // for the slow paths): SKQ_PART = 0 turns them off, 1 on
-    {
-        const char* e = std::getenv("SKQ_PART");
-        const bool want = e ? std::atoi(e) != 0 : false;
-        const bool ok = nk == 1 && (ix->mode == 3 || ix->mode == 5) && ix->ntx <= (1u << 22) &&
-                        ix->nlist_words < 0x80000000ull;
-        for (uint32_t t = 0; want && ok && t < ntables; ++t)
-            if (tables[t].k == ks[0])
-                if (int rc2 = build_part(ix, dkeys[t], dvals[t], lists)) {
-                    skq_index_free(ix);
-                    return rc2;
-                }
-    }
-    // chained tables (one k slot, ids within 22 bits, transcripts given): SKQ_CHAIN = 0 turns them
-    // off, 1 builds them whatever the key density (build_chain)
+    // chained tables (one k slot, ids within 22 bits, transcripts given): built only with SKQ_CHAIN
+    // = 1 (A/B at cfg3: 48 % fewer fabric read requests, 2 % faster map, 27.5 GB)
     if (seqs && seq_offs && nk == 1 && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
         ix->mode == 3) {  // (the entry list behind the chain step gathers wide entries)
         const char* e = std::getenv("SKQ_CHAIN");
-        const int cm = e ? std::atoi(e) : -1;
-        if (cm != 0)
+        const int cm = e ? std::atoi(e) : 0;
+        if (cm == 1)
             for (uint32_t t = 0; t < ntables; ++t)
                 if (tables[t].k == ks[0])
-                    if (int rc2 = build_chain(ix, dkeys[t], dvals[t], lists, ks[0], seqs, seq_offs, nseq, threshold,
-                                              cm == 1)) {
+                    if (int rc2 = build_chain(ix, dkeys[t], dvals[t], lists, ks[0], seqs, seq_offs, nseq, threshold)) {
                         skq_index_free(ix);
                         return rc2;
                     }
@@ -1043,9 +911,6 @@ int skq_index_free(skq_index* ix) {
     for (auto& d : ix->d_wpil_t) dev_free(d);
     for (auto& d : ix->d_rank_t) dev_free(d);
     for (auto& d : ix->d_rovf_t) dev_free(d);
-    dev_free(ix->d_pent);
-    dev_free(ix->d_ppil);
-    dev_free(ix->d_pdesc);
     dev_free(ix->d_chain);
     dev_free(ix->d_buckets);
     dev_free(ix->d_lists);
@@ -1056,7 +921,7 @@ int skq_index_free(skq_index* ix) {
 
 int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npostings, uint32_t* max_list) {
     if (!ix) return fail(-1, "null index");
-    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4 + ix->dir_bytes + ix->part_bytes + ix->chain_bytes;
+    if (device_bytes) *device_bytes = ix->nbucket_words * 4 + ix->nlist_words * 4 + ix->dir_bytes + ix->chain_bytes;
     if (npostings) *npostings = ix->npostings;
     if (max_list) *max_list = ix->max_list;
     return 0;
@@ -1085,7 +950,6 @@ int skq_session_slow_counts(skq_session* s, uint32_t* counts) {
 }
 
 int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? ix->mode : 0; }
-int skq_index_partitions(const skq_index* ix) { return ix ? (int)ix->part_np : 0; }
 double skq_index_chained(const skq_index* ix) { return ix && ix->d_chain ? 1.0 + ix->chain_succ : 0.0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
@@ -1176,9 +1040,6 @@ int skq_session_free(skq_session* s) {
     dev_free(s->tx_acc);
     dev_free(s->ktab);
     dev_free(s->kcnt);
-    dev_free(s->part_pairs);
-    dev_free(s->part_poff);
-    dev_free(s->part_out);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -1464,48 +1325,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     hipEvent_t t0{};
     record(s, 0, &t0, st);
     int rc = 0;
-    const skq_index* ix = s->idx;
-    if (ix->nk == 1 && ix->part_np && (sp.hcap == 16 || sp.hcap == 32)) {
-        // the partitioned map (k_part_a / k_part_b / k_part_c)
-        skq::PartParams pp{};
-        pp.ent = ix->d_pent;
-        pp.pil = ix->d_ppil;
-        pp.desc = ix->d_pdesc;
-        pp.shift = ix->part_shift;
-        pp.np = ix->part_np;
-        pp.npx = ix->part_npx;
-        pp.row = (ix->part_npx + 1 + 7) & ~7u;
-        pp.cap = (uint32_t)skq::WG * sp.hcap;
-        pp.bw = 64;
-        if (const char* e = std::getenv("SKQ_PART_BW")) pp.bw = (uint32_t)std::max(1, std::min(256, std::atoi(e)));
-        pp.nbk = (uint32_t)((n_reads + skq::WG - 1) / skq::WG);
-        // bucket strides padded off powers of two (SKQ_PART_PAD=0: unpadded, for A/B)
-        const char* pe = std::getenv("SKQ_PART_PAD");
-        const bool pad = !pe || std::atoi(pe) != 0;
-        pp.pstride = pp.cap + (pad ? 48u : 0u);
-        pp.ostride = 8ull * pp.cap + (pad ? 80u : 0u);
-        if (s->part_hcap < sp.hcap) {  // the workspace, sized for the session's batch at this capacity
-            dev_free(s->part_pairs);
-            dev_free(s->part_poff);
-            dev_free(s->part_out);
-            s->part_hcap = 0;
-            const uint64_t nW = (s->max_reads + skq::WG - 1) / skq::WG;
-            int arc = dev_alloc(&s->part_pairs, nW * (pp.cap + 48ull));
-            if (!arc) arc = dev_alloc(&s->part_poff, nW * pp.row);
-            if (!arc) arc = dev_alloc(&s->part_out, nW * (8ull * pp.cap + 80ull));
-            if (arc) {
-                dev_free(s->part_pairs);
-                dev_free(s->part_poff);
-                dev_free(s->part_out);
-                return arc;
-            }
-            s->part_hcap = sp.hcap;
-        }
-        pp.pairs = s->part_pairs;
-        pp.poff = s->part_poff;
-        pp.out = s->part_out;
-        rc = skq::launch_part(sp, cp, pp, stream);
-    } else if (s->idx->nk == 1) {
+    if (s->idx->nk == 1) {
         rc = skq::launch_map1(sp, cp, stream);
     } else {
         // 2..4 k slots: one k_map1 pass per k slot (each with the raw capacity its k needs), their

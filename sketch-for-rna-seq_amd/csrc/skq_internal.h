@@ -180,47 +180,6 @@ struct ChainParams {
     uint64_t chain_len;
 };
 
-// Partitioned map (one k slot; k_part_a -> k_part_b -> k_part_c): the keys of the
-// k slot's table split by key >> shift into np partitions (padded to npx, a multiple of 8), each
-// with its own compact table (the entry format of ChainParams::wpil's compact tables, placed by
-// a minimal perfect hash over that partition's keys alone), small enough for one XCD's L2.
-//   k_part_a: per workgroup (bucket w of 256 reads): sketch as k_map1, then the retained hashes as
-//             pair words (hash & (2^shift - 1)) | lane << shift, grouped by partition:
-//             pairs[w * pstride + poff[w * row + p] ...], poff[w * row + np] = the bucket's pairs;
-//   k_part_b: per (partition, run of bw buckets), with partition p on the XCD of blocks p mod 8:
-//             every pair looked up in p's table; per (w, p) piece, at out[w * ostride + 8 * poff]:
-//             one header word per pair (lane | F << 8 | tid offset << 12, or PART_MISS) followed by
-//             the tids of the hits (F <= 7 inline; F = 8: one word, the list offset in lists[]);
-//   k_part_c: per bucket: the pieces' tids counted per read in LDS, then filter, order, write and
-//             bin as k_map1.
-struct PartDesc {
-    uint32_t ent_base;  // first slot of the partition's entries (8 words each)
-    uint32_t nslots;
-    uint32_t pil_base;  // first pilot
-    uint32_t nb;        // buckets (pilots)
-    uint32_t seed;
-    uint32_t pad[3];
-};
-constexpr uint32_t PART_MISS = 0xFFFFFFFFu;
-constexpr uint32_t PART_MAX_NP = 256;
-struct PartParams {
-    const uint32_t* ent;
-    const uint16_t* pil;
-    const PartDesc* desc;
-    uint32_t shift, np, npx;
-    uint32_t row;   // u16 words per poff row (>= npx + 1, a multiple of 8)
-    uint32_t cap;   // pair slots per bucket (WG * raw capacity)
-    uint32_t bw;    // buckets per k_part_b workgroup
-    uint32_t nbk;   // buckets (k_part_a / k_part_c workgroups)
-    // words per bucket of pairs (>= cap) and of out (>= 8 * cap): padded past powers of two, so
-    // that one partition's pieces in consecutive buckets do not all map to one L2 channel / set
-    uint32_t pstride;
-    uint64_t ostride;
-    uint32_t* pairs;
-    uint16_t* poff;
-    uint32_t* out;
-};
-
 // records the message returned by skq_last_error(); returns code (skq_capi.hip)
 int set_error(int code, const char* msg);
 // session facts for skq_ingest (skq_capi.hip)
@@ -249,8 +208,6 @@ int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
 // for each k slot (p.kslot; a raw capacity `cap` of 16 or 32 hashes, at most the hashes' layout
 // stride p.hcap); the last (final_pass) merges the per-k tables, filters, orders and bins
 int launch_map1_pass(const SketchParams& p, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream);
-// the partitioned map (k_part_a, k_part_b, k_part_c) for one k slot, raw capacity p.hcap 16 or 32
-int launch_part(const SketchParams& p, const ChainParams& cp, const PartParams& pp, void* stream);
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);

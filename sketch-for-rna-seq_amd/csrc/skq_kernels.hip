@@ -2759,487 +2759,6 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Partitioned map (one k slot; PartParams, skq_internal.h). k_map1's entry gathers
-// are random 32-B requests into a table far larger than any cache (one fabric request each, the
-// kernel's bound). Here the lookups are regrouped by key range so that each partition's compact
-// table is served from one XCD's L2, and what crosses HBM is streamed: the workgroup's pairs
-// (4 B per retained hash) and the hits' tids (one header word + the tids per hit).
-
-__host__ __device__ inline size_t part_a_lds_bytes(uint32_t wc, uint32_t hcap) {
-    return sketch_tab_bytes(1) + (WG / 64) * sketch_codes_bytes(wc) + ((size_t)hcap + 1) * WG * 4 +
-           (PART_MAX_NP + 8) * 4;
-}
-
-// k_part_a: k_map1's staging, validity, rolling hash, sort and de-duplication (the same code
-// path and the same outputs: status, hash_cnt, hashes, slow lists), then the workgroup's retained
-// hashes as pair words grouped by partition (LDS counting sort) and written out coalesced with the
-// bucket's partition offsets.
-template <int HCAP>
-__global__ __launch_bounds__(WG) void k_part_a(SketchParams p, ChainParams cp, PartParams pp) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wv = tid >> 6;
-    const uint32_t wc = p.tile_chunks;
-    const size_t cbytes = sketch_codes_bytes(wc);
-    uint2* s_tab = reinterpret_cast<uint2*>(smem);
-    const uint2* s_seed = s_tab + 16;
-    uint32_t* s_codes = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + wv * cbytes);
-    uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * cbytes);
-    uint32_t* s_hist = s_raw + (HCAP + 1) * WG;
-    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + wv * 64);  // (row 0 of the wave's columns)
-    for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot 0's roll terms, then the seeds
-        const uint64_t v = e < 16 ? p.rolltab[e] : p.rolltab[p.nk * 16 + (e - 16)];
-        s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
-    }
-    for (uint32_t e = tid; e <= PART_MAX_NP; e += WG) s_hist[e] = 0;
-    __syncthreads();
-
-    const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
-    const uint32_t nr = r0 < p.n ? (uint32_t)min((uint64_t)64, p.n - r0) : 0u;  // wave-uniform
-    const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
-    const uintptr_t abase = base & ~(uintptr_t)15;
-    const uint64_t delta = base - abase;
-    uint64_t c0 = 0;
-    uint32_t nch = 0;
-    if (nr) {
-        uint64_t s0, l0, sl, ll;
-        read_extent(p.offs, p.fixed_len, r0, s0, l0);
-        read_extent(p.offs, p.fixed_len, r0 + nr - 1, sl, ll);
-        c0 = (s0 + delta) >> 4;
-        const uint64_t c1 = (sl + ll + delta + 15) >> 4;
-        nch = (uint32_t)min((uint64_t)wc, c1 - c0);
-        const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
-        constexpr uint32_t SU = 10;
-        for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
-            uint4 vv[SU];
-#pragma unroll
-            for (uint32_t u = 0; u < SU; ++u) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + min(cb + u * 64, nch - 1)));
-                vv[u] = make_uint4(x.x, x.y, x.z, x.w);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < SU; ++u) {
-                const uint32_t c = cb + u * 64;
-                const uint4 v = vv[u];
-                const uint32_t cs = c < nch ? c : wc + 1;
-                const uint32_t ta = (v.x >> 1) & 0x03030303u, tb = (v.y >> 1) & 0x03030303u;
-                const uint32_t tc = (v.z >> 1) & 0x03030303u, td = (v.w >> 1) & 0x03030303u;
-                constexpr uint32_t W4 = 0x40100401u;
-                const uint32_t code = __builtin_amdgcn_udot4(ta, W4, 0u, false) |
-                                      (__builtin_amdgcn_udot4(tb, W4, 0u, false) << 8) |
-                                      (__builtin_amdgcn_udot4(tc, W4, 0u, false) << 16) |
-                                      (__builtin_amdgcn_udot4(td, W4, 0u, false) << 24);
-                constexpr uint32_t GTCA = 0x47544341u;
-                const uint32_t x = (__builtin_amdgcn_perm(0u, GTCA, ta) ^ v.x) | (__builtin_amdgcn_perm(0u, GTCA, tb) ^ v.y) |
-                                   (__builtin_amdgcn_perm(0u, GTCA, tc) ^ v.z) | (__builtin_amdgcn_perm(0u, GTCA, td) ^ v.w);
-                s_codes[cs] = code;
-                const uint64_t wbits = __ballot(x != 0);
-                if (lane == 0 && c < nch) s_badw[c >> 6] = wbits;
-            }
-        }
-        if (lane == 0) s_codes[nch] = 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    const bool live = lane < nr;
-    const uint64_t r = live ? r0 + lane : 0;
-    uint64_t start = 0, len = 0;
-    if (live) read_extent(p.offs, p.fixed_len, r, start, len);
-    const uint64_t q0 = start + delta - c0 * 16;
-    bool slow = live && (len > (uint64_t)LFAST || q0 + len > (uint64_t)nch * 16);
-    uint8_t st = SKQ_READ_OK;
-    if (live && !slow) {
-        // is_valid_sequence (src/data_io.cpp:17-34), as in k_map1
-        bool bad = false;
-        if (len) {
-            const uint32_t ca = (uint32_t)(q0 >> 4), cz = (uint32_t)((q0 + len - 1) >> 4);
-            for (uint32_t wd = ca >> 6; wd <= (cz >> 6); ++wd) {
-                uint64_t m = s_badw[wd];
-                const uint32_t lo = wd == (ca >> 6) ? (ca & 63) : 0u, hi = wd == (cz >> 6) ? (cz & 63) : 63u;
-                m &= (hi == 63 ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
-                bad |= m != 0;
-            }
-            if (bad) {
-                bad = false;
-                const uint8_t* rb = p.reads + start;
-                for (uint64_t q = 0; q < len; ++q) {
-                    const uint8_t ch = rb[q];
-                    bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
-                }
-            }
-        }
-        if (bad) st = SKQ_READ_INVALID;
-        else if (len < p.maxk) st = SKQ_READ_SHORT;  // src/main.cpp:136-138
-    }
-
-    uint32_t v[HCAP];
-#pragma unroll
-    for (int j = 0; j < HCAP; ++j) v[j] = 0xFFFFFFFFu;
-    uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
-    const bool hashing = live && !slow && st == SKQ_READ_OK;
-    if (hashing) {
-        // src/sketch.cpp:24-39 through ntHash's rolling forward hash (33-bit lane), as k_map1
-        const uint32_t T = p.threshold;
-        const uint32_t L = (uint32_t)len;
-        const uint32_t k = p.ks[0];
-        auto codes16 = [&](uint32_t q) -> uint32_t {
-            const uint32_t d = q >> 4;
-            return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
-        };
-        uint32_t hlo = 0, hhi = 0;
-        for (uint32_t b = 0; b < k; b += 16) {
-            const uint32_t w = codes16((uint32_t)q0 + b);
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (b + j < k) roll33b(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
-        }
-        uint32_t* raw = s_raw + tid;
-        raw[0] = hlo;
-        uint32_t nraw = hlo <= T ? 1u : 0u;
-        const uint32_t nw = L - k + 1;
-        const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
-        for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
-            const uint32_t win = codes16(qin + w0 - 1);
-            const uint32_t wout = codes16(qout + w0 - 1);
-            const uint32_t jn = nw - w0;
-            uint2 e[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) e[j] = s_tab[((win >> (2 * j)) & 3u) * 4 + ((wout >> (2 * j)) & 3u)];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                roll33b(hlo, hhi, e[j]);
-                const bool rec = hlo <= T && (uint32_t)j < jn;
-                raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
-                nraw += rec ? 1u : 0u;
-            }
-        }
-        if (nraw > HCAP) {
-            slow = true;
-        } else {
-#pragma unroll
-            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
-            bitonic_sort<HCAP>(v);
-            uint32_t* out = p.hashes + r;
-            uint32_t m = 0;
-#pragma unroll
-            for (int j = 0; j < HCAP; ++j) {
-                const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
-                if (keep) {
-                    out[(uint64_t)(m++) * p.n] = v[j];
-                    keepm |= 1ull << j;
-                }
-            }
-            p.hash_cnt[r] = m;
-        }
-    }
-    if (live) {
-        if (slow) {
-            st = ST_SLOW1;
-            list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
-            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
-        } else if (st != SKQ_READ_OK) {
-            p.hash_cnt[r] = 0;
-        }
-        p.status[r] = st;
-        p.pflag[r] = slow ? 1 : 0;
-    }
-
-    // ---- the retained hashes by partition: rank within the partition (LDS atomics), the
-    // partitions' bases (one wave scans), the pair words into LDS in partition order (the raw rows
-    // are dead: every lane sorted its values into registers), out in coalesced stores
-    // (src/sparse_chaining.cpp:51-53: a k the index has no table for is not counted)
-    const bool act = hashing && !slow && cp.tabs[0].present;
-    __syncthreads();
-    const uint32_t shift = pp.shift, mask = (1u << shift) - 1u;
-    uint32_t pr[HCAP];
-#pragma unroll
-    for (int j = 0; j < HCAP; ++j) {
-        pr[j] = ~0u;
-        const uint32_t pt = v[j] >> shift;
-        if (act && ((keepm >> j) & 1ull) && pt < pp.np) {  // (keys past the table's last partition: misses)
-            const uint32_t rank = atomicAdd(&s_hist[pt], 1u);
-            pr[j] = pt | (rank << 8);
-            v[j] = (v[j] & mask) | ((uint32_t)tid << shift);
-        }
-    }
-    __syncthreads();
-    const uint32_t npx = pp.npx;
-    if (tid < 64) {  // exclusive scan of the (<= 256) partition counts, 4 per lane
-        uint32_t c4[4], sum = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t b = 4 * tid + u;
-            c4[u] = b < npx ? s_hist[b] : 0u;
-            sum += c4[u];
-        }
-        const uint32_t incl = wave_incl_scan(sum, tid);
-        uint32_t run = incl - sum;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t b = 4 * tid + u;
-            if (b < npx) s_hist[b] = run;
-            run += c4[u];
-        }
-        if (tid == 63) s_hist[npx] = incl;
-    }
-    __syncthreads();
-    uint32_t* s_stage = s_raw;
-#pragma unroll
-    for (int j = 0; j < HCAP; ++j)
-        if (pr[j] != ~0u) s_stage[s_hist[pr[j] & 255u] + (pr[j] >> 8)] = v[j];
-    __syncthreads();
-    const uint32_t total = s_hist[npx];
-    uint4* dst = reinterpret_cast<uint4*>(pp.pairs + (uint64_t)blockIdx.x * pp.pstride);
-    const uint4* sr = reinterpret_cast<const uint4*>(s_stage);
-    for (uint32_t q = tid; q < (total + 3) / 4; q += WG) dst[q] = sr[q];
-    uint16_t* prow = pp.poff + (uint64_t)blockIdx.x * pp.row;
-    for (uint32_t q = tid; q <= npx; q += WG) prow[q] = (uint16_t)s_hist[q];
-}
-
-// k_part_b: the lookups of one partition for a run of bw buckets. Block b serves partition
-// p = (b mod 8) + 8 * (b / 8 / chunks): blocks b and b + 8 share an XCD (workgroups are dealt
-// round-robin over the 8 XCDs), so each partition's workgroups run on one XCD and its table
-// stays in that XCD's L2 (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"; placement is
-// a speed matter only). R pairs per thread per round, contiguous, one block scan per round for
-// the hits' tid offsets within their pieces.
-template <int R>
-__global__ __launch_bounds__(WG) void k_part_b(PartParams pp) {
-    __shared__ uint32_t s_pre[WG + 1];  // per bucket of the run: first pair (flattened)
-    __shared__ uint32_t s_st[WG];       // per bucket: the partition's offset in the bucket's pairs
-    __shared__ uint32_t s_tb[WG];       // per bucket: tid-word prefix at its first pair
-    __shared__ uint32_t s_scan[WG];
-    const uint32_t t = threadIdx.x;
-    const uint32_t b = blockIdx.x, x = b & 7u, j = b >> 3;
-    const uint32_t nch = (pp.nbk + pp.bw - 1) / pp.bw;
-    const uint32_t p = x + 8u * (j / nch), c = j % nch;
-    if (p >= pp.np) return;  // (block-uniform, before any barrier: a padding partition)
-    const uint32_t w0 = c * pp.bw, nbh = min(pp.bw, pp.nbk - w0);
-    uint32_t cnt = 0;
-    if (t < nbh) {
-        const uint16_t* row = pp.poff + (uint64_t)(w0 + t) * pp.row;
-        const uint32_t a = row[p];
-        cnt = (uint32_t)row[p + 1] - a;
-        s_st[t] = a;
-    }
-    uint32_t M = 0;
-    const uint32_t incl0 = block_incl_scan(cnt, s_scan, M);
-    if (t < nbh) s_pre[t] = incl0 - cnt;
-    if (t == 0) s_pre[nbh] = M;
-    __syncthreads();
-    const PartDesc d = pp.desc[p];
-    const uint32_t shift = pp.shift, mask = (1u << shift) - 1u;
-    const uint64_t ocap = pp.ostride;
-    uint32_t carry = 0;  // tid words of the earlier rounds
-    for (uint32_t base = 0; base < M; base += WG * R) {  // block-uniform
-        uint32_t hdr[R], nw[R], bk[R], loc[R];
-        uint4 e0[R], e1[R];
-        uint32_t mine = 0;
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            const uint32_t i = base + t * R + u;
-            hdr[u] = PART_MISS;
-            nw[u] = 0;
-            bk[u] = 0;
-            loc[u] = ~0u;
-            e0[u] = make_uint4(0, 0, 0, 0);
-            e1[u] = e0[u];
-            if (i < M) {
-                uint32_t lo = 0, hi = nbh;  // the bucket holding pair i: last s_pre[k] <= i
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_pre[mid] <= i) lo = mid;
-                    else hi = mid;
-                }
-                bk[u] = lo;
-                loc[u] = i - s_pre[lo];
-                const uint32_t pw = pp.pairs[(uint64_t)(w0 + lo) * pp.pstride + s_st[lo] + loc[u]];
-                const uint32_t key = (p << shift) | (pw & mask);
-                const uint32_t kh = cmp_key_hash(key, d.seed);
-                const uint32_t pv = pp.pil[d.pil_base + cmp_scale(kh, d.nb)];
-                const uint4* ep = reinterpret_cast<const uint4*>(pp.ent) + 2ull * (d.ent_base + cmp_slot(kh, pv, d.nslots));
-                e0[u] = ep[0];
-                e1[u] = ep[1];
-                const uint32_t F = e0[u].x == key ? e0[u].y >> 22 : 0u;  // (F 0: no key here)
-                if (F) {
-                    hdr[u] = (pw >> shift) | (F << 8);
-                    nw[u] = F >= CMP_LONG ? 1u : F;  // (a longer list: its offset in lists[])
-                }
-            }
-            mine += nw[u];
-        }
-        uint32_t rtot = 0;
-        const uint32_t incl = block_incl_scan(mine, s_scan, rtot);
-        uint32_t run = carry + incl - mine;
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            if (loc[u] == 0) s_tb[bk[u]] = run;  // a piece starts at this pair
-            run += nw[u];
-        }
-        __syncthreads();
-        run = carry + incl - mine;
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            if (loc[u] != ~0u) {
-                const uint32_t bb = bk[u];
-                const uint32_t npc = s_pre[bb + 1] - s_pre[bb];
-                uint32_t* piece = pp.out + (uint64_t)(w0 + bb) * ocap + 8ull * s_st[bb];
-                const uint32_t to = run - s_tb[bb];
-                piece[loc[u]] = hdr[u] == PART_MISS ? PART_MISS : hdr[u] | (to << 12);
-                uint32_t* tp = piece + npc + to;
-                const uint32_t F = hdr[u] == PART_MISS ? 0u : (hdr[u] >> 8) & 15u;
-                if (F >= CMP_LONG) {
-                    tp[0] = cmp_long_off(e1[u]);
-                } else {
-                    const uint32_t w7[7] = {e0[u].y, e0[u].z, e0[u].w, e1[u].x, e1[u].y, e1[u].z, e1[u].w};
-#pragma unroll
-                    for (int q = 0; q < 7; ++q)
-                        if ((uint32_t)q < F) tp[q] = w7[q] & TID_MASK;
-                }
-            }
-            run += nw[u];
-        }
-        carry += rtot;
-        __syncthreads();  // (s_tb, s_scan: the next round)
-    }
-}
-
-// k_part_c: one bucket (the 256 reads of k_part_a's workgroup): every hit's tids from the
-// bucket's pieces into the owning read's LDS count table (k_map1's table: slot sl of read o in
-// column (o + sl) mod 64 of its wave's columns, CAS inserts), then per read the filter, the order
-// and the candidates as k_map1 (src/sparse_chaining.cpp:76-110), then the binning epilogue.
-__global__ __launch_bounds__(WG) void k_part_c(SketchParams p, ChainParams cp, PartParams pp) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[TS * WG];
-    __shared__ uint32_t s_flag[WG];
-    __shared__ uint32_t s_off[PART_MAX_NP + 8];  // the bucket's partition offsets; then the binning counts
-    const uint32_t t = threadIdx.x, w = blockIdx.x;
-    const uint64_t r = (uint64_t)w * WG + t;
-    const bool live = r < p.n;
-    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
-#pragma unroll
-    for (int sl = 0; sl < TS; ++sl) s_cnt[sl * WG + t] = EMPTY;
-    s_flag[t] = 0;
-    const uint16_t* prow = pp.poff + (uint64_t)w * pp.row;
-    for (uint32_t q = t; q <= pp.np; q += WG) s_off[q] = prow[q];
-    __syncthreads();
-    const uint32_t np = pp.np, M = s_off[np];
-    const uint32_t* region = pp.out + (uint64_t)w * pp.ostride;
-    auto tab = [&](uint32_t o, uint32_t sl) -> uint32_t* { return s_cnt + sl * WG + (o & ~63u) + ((o + sl) & 63u); };
-    auto ains_probe = [&](uint32_t x, uint32_t o) {
-        uint32_t sl = Counter<1, WG>::slot_of(x);
-#pragma unroll 1
-        for (int z = 1; z < TS; ++z) {
-            sl = (sl + 1) & (TS - 1);
-            uint32_t* a = tab(o, sl);
-            const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | 1u);
-            if (old == EMPTY) return;
-            if ((old >> 8) == x) {
-                atomicAdd(a, 1u);
-                return;
-            }
-        }
-        atomicOr(s_flag + o, 1u);  // more than TS distinct transcripts
-    };
-    auto ains = [&](uint32_t x, uint32_t o) {
-        uint32_t* a = tab(o, Counter<1, WG>::slot_of(x));
-        const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | 1u);
-        if (old == EMPTY) return;
-        if ((old >> 8) == x) atomicAdd(a, 1u);
-        else ains_probe(x, o);
-    };
-    for (uint32_t i = t; i < M; i += WG) {
-        uint32_t lo = 0, hi = np;  // the piece holding pair i: last s_off[k] <= i
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_off[mid] <= i) lo = mid;
-            else hi = mid;
-        }
-        const uint32_t a = s_off[lo], npc = s_off[lo + 1] - a;
-        const uint32_t* piece = region + 8u * a;
-        const uint32_t h = piece[i - a];
-        if (h == PART_MISS) continue;
-        const uint32_t o = h & 255u, F = (h >> 8) & 15u;
-        const uint32_t* tp = piece + npc + (h >> 12);
-        if (F < CMP_LONG) {
-            uint32_t x[7];
-#pragma unroll
-            for (int q = 0; q < 7; ++q) x[q] = (uint32_t)q < F ? tp[q] : 0u;
-#pragma unroll
-            for (int q = 0; q < 7; ++q)
-                if ((uint32_t)q < F) ains(x[q], o);
-        } else {  // a list longer than 7 (rare): all of it from lists[]
-            const uint32_t lo2 = tp[0], n = cp.lists[lo2];
-            for (uint32_t q = 0; q < n; ++q) ains(cp.lists[lo2 + 1 + q], o);
-        }
-    }
-    __syncthreads();
-    const uint8_t st = live ? p.status[r] : (uint8_t)0xFF;
-    const bool act = live && st == SKQ_READ_OK && cp.tabs[0].present;
-    uint32_t key[TS];
-    uint32_t nc = 0;
-    if (act) {
-        if (s_flag[t] == 0) {
-            // filter and order (src/sparse_chaining.cpp:76-110), as k_map1
-            uint32_t ev[TS], mx = 0;
-#pragma unroll
-            for (int sl = 0; sl < TS; ++sl) {
-                ev[sl] = *tab(t, sl);
-                mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
-            }
-            const double thr = cp.fraction * (double)mx;
-            uint32_t need = 0;
-            if (thr > 0.0) need = thr >= 256.0 ? 256u : (uint32_t)ceil(thr);
-#pragma unroll
-            for (int sl = 0; sl < TS; ++sl) {
-                const uint32_t cnt = ev[sl] & 0xFFu;
-                key[sl] = (ev[sl] != EMPTY && cnt >= need) ? ((1023u - cnt) << 22) | (ev[sl] >> 8) : ~0u;
-            }
-            bitonic_sort<TS>(key);
-            uint32_t* ct = cp.cand_tid + r;
-            uint32_t* cs = cp.cand_score + r;
-#pragma unroll
-            for (int d = 0; d < TS; ++d) {
-                if (key[d] != ~0u) {
-                    ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
-                    cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
-                    ++nc;
-                }
-            }
-            cp.cand_cnt[r] = nc;
-        } else {
-            list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
-            cp.cand_cnt[r] = 0;
-        }
-    } else if (live) {
-        cp.cand_cnt[r] = 0;
-    }
-    const bool bin = cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
-    if (bin) bin_candidates<true>(cp, t, w, nc, key, s_off, s_cnt);
-}
-
-int launch_part(const SketchParams& p, const ChainParams& cp, const PartParams& pp, void* stream) {
-    if (p.n == 0) return 0;
-    if (pp.nbk != (uint32_t)((p.n + WG - 1) / WG) || pp.npx % 8 || pp.np > pp.npx || pp.npx > PART_MAX_NP ||
-        pp.row < pp.npx + 1 || pp.cap != (uint32_t)WG * p.hcap || pp.bw == 0 || pp.bw > (uint32_t)WG ||
-        pp.pstride < pp.cap || pp.pstride % 4 || pp.ostride < 8ull * pp.cap)
-        return -4;
-    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(pp.nbk);
-    const size_t lds = part_a_lds_bytes(p.tile_chunks, p.hcap);
-    switch (p.hcap) {
-    case 16: hipLaunchKernelGGL((k_part_a<16>), grid, dim3(WG), lds, st, p, cp, pp); break;
-    case 32: hipLaunchKernelGGL((k_part_a<32>), grid, dim3(WG), lds, st, p, cp, pp); break;
-    default: return -4;
-    }
-    const uint32_t nch = (pp.nbk + pp.bw - 1) / pp.bw;
-    hipLaunchKernelGGL((k_part_b<4>), dim3(pp.npx * nch), dim3(WG), 0, st, pp);
-    hipLaunchKernelGGL(k_part_c, grid, dim3(WG), 0, st, p, cp, pp);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
 // LDS (global scratch beyond SLOW_CAP), sorted, and counted per transcript run.

@@ -52,7 +52,6 @@ def lib():
             "skq_index_free": (i32, [vp]),
             "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
             "skq_index_direct": (i32, [vp]),
-            "skq_index_partitions": (i32, [vp]),
             "skq_index_chained": (C.c_double, [vp]),
             "skq_index_create_chained": (i32, [i32, u32, u32, vp, u32, vp, vp, vp, u32, u32, C.POINTER(vp)]),
             "skq_session_slow_reads": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
@@ -225,7 +224,6 @@ class Index:
         return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
                     direct=bool(lib().skq_index_direct(self.h)),
                     probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 4: "block", 5: "compact"}[lib().skq_index_direct(self.h)],
-                    partitions=lib().skq_index_partitions(self.h),
                     chained=lib().skq_index_chained(self.h))
 
     def free(self):

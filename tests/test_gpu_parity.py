@@ -18,27 +18,21 @@ SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the 
 CHAINED = False  # build: indexes from sequences get the chained tables (skq_index_create_chained)
 
 
-@pytest.fixture(autouse=True, params=["chain", "part", "part-compact", "compact", "compact-split",
+@pytest.fixture(autouse=True, params=["chain", "compact", "compact-split",
                                       "block", "wide", "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
     """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables,
     block tables and wide direct tables gathered by the map or count kernel, 4-B direct and rank
     tables probed inside the sketch kernel, and the bucket table probed by k_probe
     (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map).
-    "part": the partitioned map (k_part_a/b/c; SKQ_PART=1) over wide tables for the slow paths,
-    "part-compact" over compact tables; indexes it does not apply to (several k) run as wide /
-    compact."""
-    monkeypatch.setenv("SKQ_PART", "0")
+    "chain": wide tables plus the chained tables (SKQ_CHAIN=1, indexes of one k built from
+    sequences); other indexes run as wide."""
     if request.param.startswith("chain"):
         # chained tables (one k, indexes built from sequences) over wide tables
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
         monkeypatch.setenv("SKQ_PROBE", "wide")
-        monkeypatch.setenv("SKQ_CHAIN", "1")  # (small test indexes: whatever the key density)
+        monkeypatch.setenv("SKQ_CHAIN", "1")
         monkeypatch.setattr(sys.modules[__name__], "CHAINED", True)
-    elif request.param.startswith("part"):
-        monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
-        monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "part-compact" else "wide")
-        monkeypatch.setenv("SKQ_PART", "1")
     elif request.param == "bucket":
         monkeypatch.setenv("SKQ_DIRECT_MB", "0")
     elif request.param.endswith("-split"):
@@ -124,14 +118,11 @@ def totals_from(ref, n, ntx):
 def test_probe_mode_is_selected(tx300, probe_mode):
     gi, _ = build([21, 31], tx=tx300)
     st = gi.stats()
-    base = {"part": "wide", "part-compact": "compact", "chain": "wide"}.get(
-        probe_mode, probe_mode.split("-")[0])
+    base = {"chain": "wide"}.get(probe_mode, probe_mode.split("-")[0])
     assert st["probe"] == base
     assert st["device_bytes"] > 0
-    assert st["partitions"] == 0  # (several k: no partitioned tables)
     assert st["chained"] == 0  # (several k: no chained tables)
     gi1, _ = build([31], tx=tx300)
-    assert (gi1.stats()["partitions"] > 0) == probe_mode.startswith("part")
     assert (gi1.stats()["chained"] > 1) == probe_mode.startswith("chain")
 
 
@@ -522,7 +513,7 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     s.check()
     s.enable_timing(False)
     count_launches = s.kernel_time(2)[1]
-    if probe_mode in ("wide", "compact", "part", "part-compact", "chain"):
+    if probe_mode in ("wide", "compact", "chain"):
         assert count_launches == 0 and s.kernel_time(0)[1] == 1
     else:
         assert count_launches == 1

@@ -94,21 +94,19 @@ def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
     return cpu, st, slow
 
 
-@pytest.mark.parametrize("mode", ["map1", "part", "chain"])
+@pytest.mark.parametrize("mode", ["map1", "chain"])
 def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
-    monkeypatch.setenv("SKQ_PART", "1" if mode == "part" else "0")
-    monkeypatch.setenv("SKQ_CHAIN", "1")  # (a 10k-transcript index: below the automatic key density)
+    monkeypatch.setenv("SKQ_CHAIN", "1" if mode == "chain" else "0")
     cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode == "chain")
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
 
 
-@pytest.mark.parametrize("mode", ["map1", "part", "chain"])
+@pytest.mark.parametrize("mode", ["map1", "chain"])
 def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
-    """part: the partitioned map (k_part_a/b/c); chain: k_map1 over the chained tables."""
-    monkeypatch.setenv("SKQ_PART", "1" if mode == "part" else "0")
+    """chain: k_map1 over the chained tables (SKQ_CHAIN=1)."""
+    monkeypatch.setenv("SKQ_CHAIN", "1" if mode == "chain" else "0")
     cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode == "chain")
-    assert (st["partitions"] > 50) == (mode == "part"), st
     assert (st["chained"] > 2) == (mode == "chain"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert st["max_list"] >= 10  # GENCODE-scale postings (long lists take the inline overflow)

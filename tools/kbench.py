@@ -32,19 +32,19 @@ tx = synth.transcriptome(a.ntx, seed=1)
 tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
 indexes, sessions = {}, {}
 for pm in a.probes.split(","):
-    # "<kind>/part": that probe kind plus the partitioned map's tables (SKQ_PART=1); "<kind>/chain":
-    # plus the chained tables (the transcripts handed to the index)
+    # "<kind>/chain": that probe kind plus the chained tables (SKQ_CHAIN=1, the transcripts handed
+    # to the index)
     kind, _, part = pm.partition("/")
     if kind == "auto":
         os.environ.pop("SKQ_PROBE", None)
     else:
         os.environ["SKQ_PROBE"] = kind
-    os.environ["SKQ_PART"] = "1" if part == "part" else "0"
+    os.environ["SKQ_CHAIN"] = "1" if part == "chain" else "0"
     tb = time.time()
     indexes[pm] = skq.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs) if part == "chain" else None)
     print(pm, indexes[pm].stats(), "built in %.1fs" % (time.time() - tb), flush=True)
 os.environ.pop("SKQ_PROBE", None)
-os.environ.pop("SKQ_PART", None)
+os.environ.pop("SKQ_CHAIN", None)
 bases, _, _ = synth.reads(tx, a.reads, a.len, seed=1000, err=0.001)
 dev = torch.device("cuda", 0)
 d = torch.from_numpy(bases).to(dev)
