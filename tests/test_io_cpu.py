@@ -123,15 +123,15 @@ def test_legacy_index_unknown_names_and_parallel_lookups(tmp_path):
 
 
 def test_sidecar_matches_the_legacy_file_and_is_stamped(tmp_path):
-    """index mode writes <index>.skq next to the legacy file; skq_index_open reads the same tables
-    and names from it, and falls back to the legacy file once the stamp no longer matches."""
+    """index mode writes <index>.skq next to the legacy file; skq_index_open reads the same tables,
+    names and sequences from it, and falls back to the legacy file once the stamp no longer matches."""
     out = tmp_path / "e.idx"
     subprocess.run([CLI, "-k", "31,25", "-o", "index", os.path.join(EDGE, "e.fa"), str(out)], check=True,
                    capture_output=True, timeout=120)
     assert os.path.exists(str(out) + ".skq")
     ks, names, seqs, tabs = skq.legacy_index_read(out)
     ks2, names2, seqs2, tabs2, side = skq.index_open(out)
-    assert side and ks2 == ks and names2 == names and all(s == b"" for s in seqs2)
+    assert side and ks2 == ks and names2 == names and seqs2 == seqs
     for k in ks:
         for a, b in zip(tabs[k], tabs2[k]):
             np.testing.assert_array_equal(a, b)
