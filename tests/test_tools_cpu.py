@@ -36,14 +36,18 @@ def test_traffic_sums_multi_k_passes(tmp_path):
     _write(str(tmp_path / "W"), "WRITE_SIZE", [(d, n, gg, v / 8) for d, n, gg, v in rows])
     out = tmp_path / "t.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "traffic.py"), "cfg5", str(tmp_path / "F"),
-                    str(tmp_path / "W"), str(out)], check=True, capture_output=True)
+                    str(tmp_path / "W"), str(out), "k_map1 x3 passes=450"], check=True, capture_output=True)
     k = json.load(open(out))["kernels"]
     mp = k["k_map1 x3 passes"]
     assert mp["dispatches"] == [2, 2]
-    assert mp["fetch_bytes_per_read"] == 2 * 7.0 * 1024  # (1 + 2 + 4) kB per read, doubled
+    # calibrated (profiles/r3_fetch_calibration.json): FETCH_SIZE as tallied (64 B per request) plus
+    # half the streamed bytes (streamed requests move 128 B)
+    assert mp["fetch_size_bytes_per_read"] == 7.0 * 1024  # (1 + 2 + 4) kB per read
+    assert mp["fetch_bytes_per_read"] == 7.0 * 1024 + 225
     assert mp["write_bytes_per_read"] == 7.0 / 8 * 1024
-    # the per-launch figure: the median over the full-size dispatches
-    assert k["k_map1"]["fetch_bytes_per_read"] == 2 * 2.0 * 1024
+    assert mp["hbm_bytes_per_read"] == 7.0 * 1024 + 225 + 7.0 / 8 * 1024
+    # the per-launch figure: the median over the full-size dispatches (no streamed bytes given)
+    assert k["k_map1"]["fetch_bytes_per_read"] == 2.0 * 1024
     assert "k_bin_sum" in k
 
 
@@ -53,7 +57,9 @@ def test_traffic_one_k_map_has_no_pass_entry(tmp_path):
     _write(str(tmp_path / "W"), "WRITE_SIZE", rows)
     out = tmp_path / "t.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "traffic.py"), "cfg3", str(tmp_path / "F"),
-                    str(tmp_path / "W"), str(out)], check=True, capture_output=True)
-    k = json.load(open(out))["kernels"]
+                    str(tmp_path / "W"), str(out), "k_map1=150"], check=True, capture_output=True)
+    t = json.load(open(out))
+    k = t["kernels"]
     assert list(k) == ["k_map1"]
-    assert k["k_map1"]["hbm_bytes_per_read"] == 3 * 2.0 * 1024
+    assert k["k_map1"]["hbm_bytes_per_read"] == 2 * 2.0 * 1024 + 75
+    assert "r3_fetch_calibration" in t["calibration"]
