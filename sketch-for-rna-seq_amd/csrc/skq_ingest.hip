@@ -299,6 +299,10 @@ struct DevArray {
     }
 };
 
+// chunk slots: the reader fills one while the device copies another and the consumer parses and
+// maps a third (pread, H2D and the map overlap; two slots serialised the pread with the copy)
+constexpr int NSLOT = 3;
+
 struct Slot {
     uint8_t* host = nullptr;   // pinned
     uint64_t host_cap = 0;
@@ -306,6 +310,7 @@ struct Slot {
     uint64_t dev_cap = 0;
     hipEvent_t h2d{}, consumed{};
     bool consumed_pending = false;
+    bool h2d_pending = false;  // the host buffer is still being copied to the device
     int state = 0;             // 0 free, 1 ready (copy issued), 2 in use by the consumer
     uint64_t file_off = 0, own = 0, len = 0;
 };
@@ -327,7 +332,7 @@ struct skq_ingest {
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
-    Slot slot[2];
+    Slot slot[NSLOT];
     uint64_t produced = 0, consumed_chunks = 0;
     bool eof = false, stop = false;
     std::string io_err;
@@ -398,7 +403,7 @@ void reader_main(skq_ingest* g) {
     uint64_t off = g->lo;
     std::string err;
     for (uint64_t c = 0; off < g->hi; ++c) {
-        Slot& sl = g->slot[c & 1];
+        Slot& sl = g->slot[c % NSLOT];
         {
             std::unique_lock<std::mutex> lk(g->mu);
             g->cv.wait(lk, [&] { return g->stop || sl.state == 0; });
@@ -407,6 +412,10 @@ void reader_main(skq_ingest* g) {
         if (sl.consumed_pending) {  // the consumer's kernels are done with the device buffer
             (void)hipEventSynchronize(sl.consumed);
             sl.consumed_pending = false;
+        }
+        if (sl.h2d_pending) {  // (the host buffer's last copy: done before it is refilled)
+            (void)hipEventSynchronize(sl.h2d);
+            sl.h2d_pending = false;
         }
         // read until the own region ends at a newline (or EOF) and the halo line is complete
         const uint64_t lim = g->hi - off;  // bytes of the range left (hi is a line start or EOF)
@@ -477,8 +486,8 @@ void reader_main(skq_ingest* g) {
             err = "chunk upload failed";
             break;
         }
-        // the pinned buffer is reused only after this copy: wait for it before the next fill
-        (void)hipEventSynchronize(sl.h2d);
+        // (the consumer's stream waits for sl.h2d; this host buffer is refilled only after it)
+        sl.h2d_pending = true;
         sl.file_off = off;
         sl.own = own;
         sl.len = len;
@@ -663,7 +672,7 @@ int skq_ingest_map(skq_ingest* g, uint32_t threshold, double fraction, int accum
             g->cv.notify_all();
             g->cur = -1;
         }
-        const int c = (int)(g->consumed_chunks & 1);
+        const int c = (int)(g->consumed_chunks % NSLOT);
         {
             std::unique_lock<std::mutex> lk(g->mu);
             g->cv.wait(lk, [&] { return g->slot[c].state == 1 || (g->eof && g->produced == g->consumed_chunks); });
