@@ -42,6 +42,8 @@ def _args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: min(16, affinity CPUs): the box's CPU share per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the 1-thread CPU timing")
+    ap.add_argument("--io-threads", type=int, default=12, help="end to end: FASTQ pread threads per GPU")
+    ap.add_argument("--chunk-mb", type=int, default=32, help="end to end: FASTQ chunk (MiB)")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the FASTQ-file -> EM leg reported beside the kernel path")
     ap.add_argument("--dist-backend", default="nccl",
@@ -160,7 +162,7 @@ def parity_check(gpu, gtot, cpu, nk):
     return bad
 
 
-def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, rank=0, world=1, dev=None, batch=2_000_000):
+def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, rank=0, world=1, dev=None, batch=2_000_000, io_cfg=(8, 64)):
     """quant as the CLI runs it, beside the kernel-path metric (never `value`): the job's reads as
     ONE FASTQ file in memory (/dev/shm when there is room, else the page cache; each rank writes
     its shard's records at its own offset) -> split at line starts into one part per rank
@@ -216,7 +218,7 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, rank=0, world=1, dev=No
         emr = {}
 
         def run():
-            g = skq.Ingest(es, path, chunk_bytes=64 << 20, io_threads=8, part=part)
+            g = skq.Ingest(es, path, chunk_bytes=io_cfg[1] << 20, io_threads=io_cfg[0], part=part)
             em = skq.EMSet(ntx, device=dev.index if dev is not None else 0)
             tot = 0
             while True:
@@ -273,6 +275,7 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, rank=0, world=1, dev=No
                                               " with RCCL all-reduces" if world > 1 else ""),
                     reads=got_all, fastq_GB=need / 1e9,
                     fastq_in="/dev/shm" if tmpdir else "page cache (%s)" % os.path.dirname(path), seconds=dt,
+                    io_threads=io_cfg[0], chunk_mb=io_cfg[1],
                     reads_per_s=got_all / dt, pass_reads_per_s=[got_all / t for t in times],
                     check="totals equal the in-HBM map's, all reads kept" if ok else "MISMATCH", **emr)
     finally:
@@ -457,7 +460,8 @@ def main(args):
     e2e = None
     if not args.no_end_to_end:
         try:
-            e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp, rank, world, dev)
+            e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp, rank, world, dev,
+                             io_cfg=(args.io_threads, args.chunk_mb))
         except (OSError, skq.SkqError) as ex:  # (e.g. no room for the FASTQ file): the metric line still prints
             e2e = {"error": "%s: %s" % (type(ex).__name__, ex)}
         log("end to end: %s" % json.dumps(e2e))

@@ -51,7 +51,7 @@ void print_help(const std::string& prog) {
               << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
               << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_DEVICES (GPU list for quant,\n"
               << "             e.g. 0,1,2,3 or all), SKQ_BATCH (reads per batch), SKQ_CHUNK_MB (FASTQ MiB\n"
-              << "             per device chunk, default 64), SKQ_REDUCE (rccl | host: how the EM sums\n"
+              << "             per device chunk, default 32), SKQ_REDUCE (rccl | host: how the EM sums\n"
               << "             reduce over devices; rccl on one device runs the sharded EM over a\n"
               << "             one-rank RCCL communicator).\n";
 }
@@ -110,7 +110,7 @@ struct Part {
         check(skq_session_create(ix, batch, 256, &s), "session");
         uint64_t chunk = 0;
         if (const char* e = std::getenv("SKQ_CHUNK_MB")) chunk = std::strtoull(e, nullptr, 10) << 20;
-        check(skq_ingest_open_range(s, reads_path.c_str(), lo, hi, state, chunk, 8, &q), "FASTQ");
+        check(skq_ingest_open_range(s, reads_path.c_str(), lo, hi, state, chunk, 0, &q), "FASTQ");
         // every record's candidates stay on the device, appended batch by batch to the EM set
         check(skq_em_create(dev, ntx, &em), "EM");
         const uint32_t thr = skq_threshold((double)kSketchSize);

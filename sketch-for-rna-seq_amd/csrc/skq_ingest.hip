@@ -599,8 +599,8 @@ int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_
     g->s = s;
     g->device = skq::session_device(s);
     g->max_reads = skq::session_max_reads(s);
-    g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (64ull << 20), 1u << 12);  // (64 MiB: tools/ingest_bench.py sweep)
-    g->io_threads = io_threads > 0 ? io_threads : 8;  // 4 preads: 37 M reads/s end to end, 8: 53 M (profiles/r2_ingest_threads.log)
+    g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (32ull << 20), 1u << 12);  // (32 MiB, 12 preads: profiles/r3_ingest_sweep.log)
+    g->io_threads = io_threads > 0 ? io_threads : 12;  // 4 preads: 37 M reads/s end to end, 8: 53 M (profiles/r2_ingest_threads.log); 12 with 32-MiB chunks: 75 M (profiles/r3_ingest_sweep.log)
     g->fd = ::open(path, O_RDONLY);
     if (g->fd < 0) {
         delete g;

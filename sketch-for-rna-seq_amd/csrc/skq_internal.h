@@ -85,6 +85,9 @@ struct SketchParams {
     uint32_t* ovf1;
     uint32_t ovf_word;  // the control word counting ovf1 (k_sketch_slow: C_OVF1, or C_OVF3 behind k_slow_wave)
     uint32_t kslot;     // k_map1 pass mode: the k slot this pass sketches and counts
+    // k_map1's per-wave LDS region (bytes) and the offset of its per-read overflow flags in it,
+    // set by the launcher (map1_layout)
+    uint32_t map_wave_bytes, map_flag_at;
     // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to

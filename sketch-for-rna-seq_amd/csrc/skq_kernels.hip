@@ -19,6 +19,10 @@
 //                  transcripts, > 4 k slots). One workgroup per listed read, sorting in LDS; they walk device-side
 //                  work lists with a fixed grid, so no host round trip is needed.
 #include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include <utility>
 
@@ -1949,18 +1953,32 @@ constexpr uint32_t MAP_P = 384;
 // chained tables: the wave's entries' record keys ([64][8]) and hit masks ([64]) before the
 // per-read overflow flags
 __host__ __device__ inline size_t chn_flag_at(uint32_t) { return (size_t)64 * 8 * 4 + 256; }
-__host__ __device__ inline size_t map1_wave_bytes(uint32_t wc, bool chn = false, uint32_t hcap = 16) {
+// the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
+// lanes (u8; compact tables: u32 slot | lane << 26) — or the chained step's keys (tab: 0 wide,
+// 1 block, 2 compact, 3 chained). SKQ_MAP1_LOOSE=1: the round-2 layout (the flags after an 8-B
+// per-entry list whatever the tables), for A/B.
+inline size_t map1_flag_at(int tab, uint32_t hcap) {
+    static const bool loose = [] {
+        const char* e = std::getenv("SKQ_MAP1_LOOSE");
+        return e && std::atoi(e) != 0;
+    }();
+    if (tab == 3) return chn_flag_at(hcap);
+    if (tab == 2 || loose) return (size_t)MAP_P * 8;
+    return ((size_t)MAP_P * 5 + 15) & ~(size_t)15;
+}
+inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
     const size_t a = sketch_codes_bytes(wc);
-    // the list: hashes, then owning lanes (u8; compact tables: u32 slot | lane << 26), then the
-    // per-read overflow flags (chained tables: chn_flag_at)
-    const size_t b = (chn ? chn_flag_at(hcap) : (size_t)MAP_P * 8) + 64 * 4;
+    const size_t b = map1_flag_at(tab, hcap) + 64 * 4;
     const size_t c = (size_t)(WG + 1) * 4;
     const size_t m = a > b ? a : b;
     return ((m > c ? m : c) + 15) & ~(size_t)15;
 }
 
-size_t map1_lds_bytes(uint32_t wave_chunks, uint32_t hcap, bool chn = false) {
-    return sketch_tab_bytes(1) + (WG / 64) * map1_wave_bytes(wave_chunks, chn, hcap) + ((size_t)hcap + 1) * WG * 4;
+// sets p.map_wave_bytes / p.map_flag_at; returns the launch's LDS bytes
+size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
+    p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
+    p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
+    return sketch_tab_bytes(1) + (WG / 64) * (size_t)p.map_wave_bytes + ((size_t)hcap + 1) * WG * 4;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -1998,7 +2016,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t lane = tid & 63, wv = tid >> 6;
     MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
-    const size_t wave_bytes = map1_wave_bytes(wc, CHN, HCAP);
+    const size_t wave_bytes = p.map_wave_bytes;
     uint2* s_tab = reinterpret_cast<uint2*>(smem);
     const uint2* s_seed = s_tab + 16;
     unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
@@ -2196,7 +2214,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t cq = CHN && act && nraw_out ? s_raw[tid] : 0u;
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
-    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + (CHN ? chn_flag_at(HCAP) : MAP_P * 8));  // per read: > TS transcripts
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + p.map_flag_at);  // per read: > TS transcripts
     s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
@@ -3644,32 +3662,56 @@ int launch_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* cont
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream) {
-    if (p.n == 0) return 0;
-    const dim3 grid((unsigned)((p.n + WG - 1) / WG));
+// SKQ_MAP1_OCC=1: print each k_map1 launch shape's resident workgroups per CU once (stderr)
+static void map1_report_occupancy(const void* kern, size_t lds) {
+    static const bool on = [] {
+        const char* e = std::getenv("SKQ_MAP1_OCC");
+        return e && std::atoi(e) != 0;
+    }();
+    if (!on) return;
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, size_t>> seen;
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& x : seen)
+        if (x.first == kern && x.second == lds) return;
+    seen.emplace_back(kern, lds);
+    int nb = -1;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, WG, lds);
+    std::fprintf(stderr, "[skq] k_map1 %p: %zu B LDS, %d workgroups per CU\n", kern, lds, nb);
+}
+
+int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
+    if (p0.n == 0) return 0;
+    const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
     const bool chn = cp.chain != nullptr;
-    const size_t lds = map1_lds_bytes(p.tile_chunks, p.hcap, chn);
+    SketchParams p = p0;
+    const size_t lds = map1_layout(p, chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0, p.hcap);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    using K = void (*)(SketchParams, ChainParams);
+    K kern = nullptr;
     // (MB: gather rounds in flight)
     switch (p.hcap * 4 + (chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
-    case 67: hipLaunchKernelGGL((k_map1<16, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
-    case 131: hipLaunchKernelGGL((k_map1<32, 4, 3>), grid, dim3(WG), lds, st, p, cp); break;
-    case 64: hipLaunchKernelGGL((k_map1<16, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
-    case 65: hipLaunchKernelGGL((k_map1<16, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
-    case 66: hipLaunchKernelGGL((k_map1<16, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;
-    case 128: hipLaunchKernelGGL((k_map1<32, 4, 0>), grid, dim3(WG), lds, st, p, cp); break;
-    case 129: hipLaunchKernelGGL((k_map1<32, 4, 1>), grid, dim3(WG), lds, st, p, cp); break;
-    case 130: hipLaunchKernelGGL((k_map1<32, 4, 2>), grid, dim3(WG), lds, st, p, cp); break;
+    case 67: kern = k_map1<16, 4, 3>; break;
+    case 131: kern = k_map1<32, 4, 3>; break;
+    case 64: kern = k_map1<16, 4, 0>; break;
+    case 65: kern = k_map1<16, 4, 1>; break;
+    case 66: kern = k_map1<16, 4, 2>; break;
+    case 128: kern = k_map1<32, 4, 0>; break;
+    case 129: kern = k_map1<32, 4, 1>; break;
+    case 130: kern = k_map1<32, 4, 2>; break;
     default: return -4;
     }
+    map1_report_occupancy(reinterpret_cast<const void*>(kern), lds);
+    hipLaunchKernelGGL(kern, grid, dim3(WG), lds, st, p, cp);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_map1_pass(const SketchParams& p, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
-    if (p.n == 0) return 0;
-    if ((cp.wide != 1 && cp.wide != 3) || cap > p.hcap) return -4;
-    const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    const size_t lds = map1_lds_bytes(p.tile_chunks, cap);
+int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
+    if (p0.n == 0) return 0;
+    if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap) return -4;
+    const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
+    SketchParams p = p0;
+    const size_t lds = map1_layout(p, cp.wide == 3 ? 2 : 0, cap);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (cap * 8 + (cp.wide == 3 ? 2 : 0) + (final_pass ? 1 : 0)) {
     case 128: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;

@@ -492,7 +492,7 @@ class FastqReader:
 class Ingest:
     """FASTQ parsed on the GPU (skq_ingest_*): batches of records mapped through `session`."""
 
-    def __init__(self, session, path, chunk_bytes=0, io_threads=8, part=None):
+    def __init__(self, session, path, chunk_bytes=0, io_threads=0, part=None):
         """part = (lo, hi, entry_state): only the records whose header starts in [lo, hi)
         (fastq_split), numbered from 0."""
         self.session = session  # keeps the session alive
