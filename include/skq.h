@@ -128,8 +128,14 @@ uint32_t skq_threshold(double fraction);
 
 /* Device-resident results of the last call (valid until the next call on the session), in
  * structure-of-arrays layout (n = n_reads of the call, so a wave's accesses are contiguous):
- * hashes: read r, k slot i: c = hash_cnt[i*n + r]; if c <= hcap the sorted set is
- *   hashes[(i*hcap + j)*n + r] for j < c; otherwise it is hash_ext[hashes[i*hcap*n + r] + j].
+ * hashes, hash_layout 0 (padded rows; skq_sketch, multi-k maps): read r, k slot i:
+ *   c = hash_cnt[i*n + r]; if c <= hcap the sorted set is hashes[(i*hcap + j)*n + r] for j < c;
+ *   otherwise it is hash_ext[hashes[i*hcap*n + r] + j].
+ * hashes, hash_layout 1 (per-wave packed; the single-k skq_map, whose kernel then writes whole
+ *   64-B lines): c = hash_cnt[r]; if c & 0x80000000 the set is a run in hash_ext at
+ *   x = c & 0x7FFFFFFF: hash_ext[x] hashes at hash_ext[x + 1 ..]; otherwise its c hashes are at
+ *   hashes[(r & ~63)*hcap + o .. + c), o = the summed counts of reads (r & ~63) .. r - 1 that are
+ *   not runs. skq_session_export gives either layout as flat arrays.
  * candidates (sorted by score desc, tid asc): c = cand_cnt[r]; if c <= ccap candidate j is
  *   (cand_tid[j*n + r], cand_score[j*n + r]); otherwise the (tid, score) pairs are at
  *   cand_ext[2*(cand_tid[r] + j)], cand_ext[2*(cand_tid[r] + j) + 1].
@@ -150,6 +156,7 @@ typedef struct {
     const uint32_t* cand_ext;
     const uint64_t* tx_reads; /* per transcript: reads listing it as a candidate (accumulated) */
     const uint64_t* tx_score; /* per transcript: sum of those reads' scores (accumulated)      */
+    uint32_t hash_layout;     /* 0: padded rows, 1: per-wave packed (above)                     */
     /* (batches of 512k+ reads finish their totals on the session's own side stream, which the
      * launch stream does not wait for: skq_session_results blocks the host until that work is
      * done, so tx_reads / tx_score are current once the caller's stream is synchronized too;

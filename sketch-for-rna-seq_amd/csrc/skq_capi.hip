@@ -106,6 +106,7 @@ struct skq_session {
     bool have_sketch = false;
     bool probed = false;       // the last skq_sketch also filled lofs/pflag (fused probe)
     bool have_chain = false;   // candidates belong to the current batch
+    bool hash_packed = false;  // hashes in the per-wave packed layout (single-k fused map)
     uint8_t* status = nullptr;
     uint32_t* hash_cnt = nullptr;
     uint32_t* hashes = nullptr;
@@ -147,6 +148,8 @@ struct skq_session {
     // side stream for the totals (k_bin_sum runs beside the slow paths), created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork{}, ev_join[2]{};  // ev_join[b]: k_bin_sum of the last batch of parity b
+    hipEvent_t ev_early{};               // the early k_slow_wave (multi-k passes) is done
+    bool early_pending = false;
     bool join_rec[2] = {false, false};
 };
 
@@ -185,6 +188,16 @@ uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold, double s
     if (need <= 16) return 16;
     if (need <= 32) return 32;
     return 64;
+}
+
+// the multi-k passes' raw capacity: the mean retained windows of the pass's k plus this many
+// standard deviations (reads beyond it take k_slow_wave); SKQ_PASS_SIGMAS overrides (A/B)
+double pass_sigmas() {
+    static const double v = [] {
+        const char* e = std::getenv("SKQ_PASS_SIGMAS");
+        return e ? std::atof(e) : 3.0;
+    }();
+    return v;
 }
 
 void record(skq_session* s, int kind, hipEvent_t* start, hipStream_t st) {
@@ -1017,6 +1030,7 @@ int skq_session_free(skq_session* s) {
         (void)hipEventDestroy(s->ev_fork);
         (void)hipEventDestroy(s->ev_join[0]);
         (void)hipEventDestroy(s->ev_join[1]);
+        (void)hipEventDestroy(s->ev_early);
     }
     dev_free(s->status);
     dev_free(s->hash_cnt);
@@ -1106,6 +1120,7 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     s->n_reads = n_reads;
     s->have_sketch = true;
     s->have_chain = false;
+    s->hash_packed = false;
     s->probed = ix->direct;
     s->x_hashes = nullptr;
     s->x_offs = nullptr;
@@ -1141,6 +1156,17 @@ static int wait_totals(skq_session* s, hipStream_t st) {
 // with atomics (commuting with the slow paths' direct adds). For batches of 512k+ reads it runs on
 // the session's side stream and nothing on the launch stream waits for it: it overlaps the slow
 // paths and the next batch's map kernel, which bins into the other buffer (wait_bins).
+// the side stream (totals binning, the early k_slow_wave) and its events
+static int ensure_side(skq_session* s) {
+    if (s->side) return 0;
+    HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_join[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_join[1], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_early, hipEventDisableTiming));
+    return 0;
+}
+
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
                       hipStream_t st) {
     // (small batches: the extra stream hand-offs cost more than the overlap gains; with the
@@ -1148,12 +1174,7 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
     const bool fork = accumulate && p.slow_totals && p.n >= (1u << 19);
     hipEvent_t t0{};
     if (fork) {
-        if (!s->side) {
-            HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&s->ev_join[0], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&s->ev_join[1], hipEventDisableTiming));
-        }
+        if (int rc = ensure_side(s)) return rc;
         HIP_TRY(hipEventRecord(s->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
         record(s, 3, &t0, s->side);
@@ -1166,6 +1187,10 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
     }
     if (sp && (p.wide == 1 || p.wide == 3) && p.nk <= (uint32_t)skq::NK_FAST) {
         // the fused map's slow reads: the wave path first, the general paths for what it leaves
+        if (s->early_pending) {  // (its marks on the list are read by the late launch)
+            HIP_TRY(hipStreamWaitEvent(st, s->ev_early, 0));
+            s->early_pending = false;
+        }
         if (int rc = skq::launch_slow_wave(*sp, p, s->ovf3, s->ovf4, st))
             return fail(-3, rc == -4 ? "slow path: unsupported tables" : "slow-path launch failed");
         skq::SketchParams sp2 = *sp;
@@ -1209,6 +1234,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.status = status;
     p.hash_cnt = hash_cnt;
     p.hashes = hashes;
+    p.hpack = hashes == s->hashes && s->hash_packed ? 1u : 0u;
     p.hash_ext = s->hash_ext;
     p.hash_offs = hash_offs;
     p.present = present;
@@ -1297,6 +1323,16 @@ static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t f
     return (ix->mode == 3 || ix->mode == 5) && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32);
 }
 
+// the early k_slow_wave (multi-k passes, large batches): opt-in, SKQ_EARLY_SLOW=1 (from 512k
+// reads) or 2 (any batch; tests). Off by default: the passes run at the fabric's request ceiling,
+// so the overlapped slow wave's requests slow them by as much as it saves (profiles/r3_early_slow.log)
+static bool early_slow(const skq::ChainParams& cp) {
+    const char* e = std::getenv("SKQ_EARLY_SLOW");
+    const int mode = e ? std::atoi(e) : 0;
+    return mode != 0 && cp.nk > 1 && (cp.wide == 1 || cp.wide == 3) && cp.nk <= (uint32_t)skq::NK_FAST &&
+           (mode == 2 || cp.n >= (1u << 19));
+}
+
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
                      uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction, int accumulate,
                      void* stream) {
@@ -1315,6 +1351,9 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         }
     }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
+    // one k slot: the hashes in the per-wave packed layout (whole lines written; skq.h)
+    s->hash_packed = s->idx->nk == 1;
+    sp.hpack = s->hash_packed ? 1u : 0u;
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
         return rc;
@@ -1336,8 +1375,20 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
             pi.kslot = i;
             const uint32_t ml = d_offs ? max_len : fixed_len;
             const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(ml, s->max_len), skq::LFAST));
-            rc = skq::launch_map1_pass(pi, cp, std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, 3.0)),
+            rc = skq::launch_map1_pass(pi, cp, std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, pass_sigmas())),
                                        i + 1 == nk, stream);
+            if (!rc && i == 0 && early_slow(cp)) {
+                // the first pass's slow reads (ST_SLOW1) on the side stream while the others run:
+                // the list's length now, then the early k_slow_wave over that much of it
+                HIP_TRY(hipMemcpyAsync(s->ctrl + skq::C_SNAP, s->ctrl + skq::C_OVF2, 4, hipMemcpyDeviceToDevice, st));
+                if (int e = ensure_side(s)) return e;
+                HIP_TRY(hipEventRecord(s->ev_fork, st));
+                HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+                if (skq::launch_slow_wave(sp, cp, s->ovf3, s->ovf4, s->side, true))
+                    return fail(-3, "slow-path launch failed");
+                HIP_TRY(hipEventRecord(s->ev_early, s->side));
+                s->early_pending = true;
+            }
         }
     }
     if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
@@ -1392,6 +1443,7 @@ int skq_session_results(skq_session* s, skq_results* o) {
     o->hash_cnt = s->hash_cnt;
     o->hashes = s->hashes;
     o->hash_ext = s->hash_ext;
+    o->hash_layout = s->hash_packed ? 1u : 0u;
     o->cand_cnt = s->cand_cnt;
     o->cand_tid = s->cand_tid;
     o->cand_score = s->cand_score;
@@ -1448,6 +1500,15 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
             HIP_TRY(hipMemcpy(st.data(), s->status, n, hipMemcpyDeviceToHost));
         }
     }
+    std::vector<uint32_t> xo;  // packed layout: the read's hash_ext run ([count, hashes...]) or ~0u
+    if (s->have_sketch && s->hash_packed) {
+        xo.assign(n, ~0u);
+        for (uint64_t r = 0; r < n; ++r)
+            if (hc[r] & skq::HASH_EXT) {
+                xo[r] = hc[r] & ~skq::HASH_EXT;
+                HIP_TRY(hipMemcpy(&hc[r], s->hash_ext + xo[r], 4, hipMemcpyDeviceToHost));
+            }
+    }
     uint64_t th = 0, tc = 0;
     for (uint64_t v : hc) th += v;
     for (uint64_t v : cc) tc += v;
@@ -1458,24 +1519,41 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     if (hash_offs || hashes) {
         if (s->have_sketch) {
             const uint32_t hcap = s->hcap;
-            std::vector<uint32_t> pad((uint64_t)nk * hcap * n);  // [i][j][r]
+            std::vector<uint32_t> pad((uint64_t)nk * hcap * n);  // padded: [i][j][r]; packed: per wave
             if (n) HIP_TRY(hipMemcpy(pad.data(), s->hashes, pad.size() * 4, hipMemcpyDeviceToHost));
             uint64_t at = 0;
-            for (uint64_t r = 0; r < n; ++r)
-                for (uint32_t i = 0; i < nk; ++i) {
-                    const uint64_t e = r * nk + i;
-                    const uint32_t c = hc[(uint64_t)i * n + r];
-                    if (hash_offs) hash_offs[e] = at;
-                    if (hashes) {
-                        if (c <= hcap) {
-                            for (uint32_t j = 0; j < c; ++j) hashes[at + j] = pad[((uint64_t)i * hcap + j) * n + r];
-                        } else {
-                            HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + pad[(uint64_t)i * hcap * n + r], c * 4ull,
-                                              hipMemcpyDeviceToHost));
-                        }
+            if (s->hash_packed) {  // (one k slot) sets in lane order per wave; runs in hash_ext
+                uint64_t woff = 0;
+                for (uint64_t r = 0; r < n; ++r) {
+                    if ((r & 63) == 0) woff = 0;
+                    const uint32_t c = hc[r];
+                    if (xo[r] != ~0u) {
+                        if (hashes && c)
+                            HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + xo[r] + 1, c * 4ull, hipMemcpyDeviceToHost));
+                    } else {
+                        if (hashes) std::copy_n(pad.data() + (r & ~63ull) * hcap + woff, c, hashes + at);
+                        woff += c;
                     }
+                    if (hash_offs) hash_offs[r] = at;
                     at += c;
                 }
+            } else {
+                for (uint64_t r = 0; r < n; ++r)
+                    for (uint32_t i = 0; i < nk; ++i) {
+                        const uint64_t e = r * nk + i;
+                        const uint32_t c = hc[(uint64_t)i * n + r];
+                        if (hash_offs) hash_offs[e] = at;
+                        if (hashes) {
+                            if (c <= hcap) {
+                                for (uint32_t j = 0; j < c; ++j) hashes[at + j] = pad[((uint64_t)i * hcap + j) * n + r];
+                            } else {
+                                HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + pad[(uint64_t)i * hcap * n + r], c * 4ull,
+                                                  hipMemcpyDeviceToHost));
+                            }
+                        }
+                        at += c;
+                    }
+            }
             if (hash_offs) hash_offs[n * nk] = at;
         } else if (hash_offs) {
             for (uint64_t e = 0; e <= n * nk; ++e) hash_offs[e] = 0;

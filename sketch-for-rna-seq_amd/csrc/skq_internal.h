@@ -21,6 +21,8 @@ constexpr uint64_t MAX_BATCH = (1ull << 24) - 1;  // packed per-batch totals hol
 
 // status flags above SKQ_STATUS_MASK (internal)
 constexpr uint8_t ST_SLOW1 = 0x10;  // sketch handled by the slow path
+constexpr uint32_t HASH_EXT = 0x80000000u;  // packed hash layout: hash_cnt marks a hash_ext run
+constexpr uint8_t ST_EARLY = 0x20;  // done by the early k_slow_wave (ST_SLOW1 kept until the late one)
 
 // control block (u32 words): the sketch half (words 0-7) is zeroed before every sketch, the
 // chain half (words 8-15) before every chain.
@@ -34,6 +36,7 @@ enum Ctrl : int {
     C_BUMP_S = 10,  // u64 (words 10-11): chain scratch u64 words used
     C_BUMP_C = 12,  // u64 (words 12-13): cand_ext pairs used
     C_OVF4 = 14,    // second-level chain list (k_slow_wave -> k_chain_slow)
+    C_SNAP = 15,    // the chain list's length after the first multi-k pass (the early k_slow_wave's)
     C_WORDS = 16
 };
 enum Err : uint32_t {
@@ -88,6 +91,10 @@ struct SketchParams {
     // k_map1's per-wave LDS region (bytes) and the offset of its per-read overflow flags in it,
     // set by the launcher (map1_layout)
     uint32_t map_wave_bytes, map_flag_at;
+    // hpack: the per-wave packed hash layout (single-k map; skq.h "hash layouts"): read r's
+    // hashes follow those of the reads before it in its wave, from hashes + (r & ~63) * hcap,
+    // except runs in hash_ext, marked hash_cnt[r] = HASH_EXT | offset ([count, hashes...])
+    uint32_t hpack;
     // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
@@ -118,6 +125,7 @@ struct ChainParams {
     const uint32_t* hashes;    // padded (session) or flat (explicit offsets)
     const uint32_t* hash_ext;
     const uint64_t* hash_offs; // null => padded layout
+    uint32_t hpack;            // 1: per-wave packed layout (SketchParams::hpack)
     const uint8_t* present;    // null => all k present
     const uint32_t* buckets;
     const uint32_t* lists;    // [n, tid...] per distinct postings list
@@ -216,7 +224,8 @@ int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
 // the wave slow path behind k_map1 and its passes (wide or compact tables, <= 4 k slots; -4 otherwise):
 // the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
-int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);
+int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream,
+                     bool early = false);
 int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
 // per-transcript totals of the batch's final candidates into p.tx_acc (k_bin + k_bin_sum), then
 // launch_fold_totals adds them into p.tx_reads / p.tx_score with atomics (commuting with the slow

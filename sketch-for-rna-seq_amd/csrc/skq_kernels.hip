@@ -24,6 +24,7 @@
 #include <mutex>
 #include <vector>
 
+#include <type_traits>
 #include <utility>
 
 #include <algorithm>
@@ -592,34 +593,48 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     const uint32_t incl = block_incl_scan(mine, s_scan, u);
                     uint32_t* dst = slot;
                     uint64_t dstride = p.n;
-                    if (u > p.hcap) {
+                    if (u > p.hcap || p.hpack) {  // (packed layout: always a run, [count, hashes...])
+                        const uint32_t need = u + (p.hpack ? 1u : 0u);
                         if (t == 0) {
                             s_at = ~0ull;
-                            const unsigned long long at = atomicAdd(bump, (unsigned long long)u);
-                            if (at + u <= p.hash_ext_cap) s_at = at;
+                            const unsigned long long at = atomicAdd(bump, (unsigned long long)need);
+                            if (at + need <= p.hash_ext_cap && at < HASH_EXT) s_at = at;
                             else atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         }
                         __syncthreads();
                         if (s_at == ~0ull) continue;  // uniform
-                        dst = p.hash_ext + s_at;
+                        dst = p.hash_ext + s_at + (p.hpack ? 1u : 0u);
                         dstride = 1;
-                        if (t == 0) slot[0] = (uint32_t)s_at;
+                        if (t == 0) {
+                            if (p.hpack) p.hash_ext[s_at] = u;
+                            else slot[0] = (uint32_t)s_at;
+                        }
                     }
                     uint32_t o = incl - mine;
                     for (uint32_t x = a; x < b; ++x)
                         if (x == 0 || s_buf[x] != s_buf[x - 1]) dst[(uint64_t)(o++) * dstride] = s_buf[x];
-                    if (t == 0) p.hash_cnt[(uint64_t)i * p.n + r] = u;
+                    if (t == 0) p.hash_cnt[(uint64_t)i * p.n + r] = p.hpack ? (HASH_EXT | (uint32_t)s_at) : u;
                 } else if (t == 0) {  // more windows than LDS holds: serial, in place
                     serial_sort(ext, m);
                     uint32_t u = 0;
                     for (uint32_t x = 0; x < m; ++x)
                         if (x == 0 || ext[x] != ext[u - 1]) ext[u++] = ext[x];
-                    if (u <= p.hcap) {
-                        for (uint32_t x = 0; x < u; ++x) slot[(uint64_t)x * p.n] = ext[x];
+                    if (p.hpack) {  // the run behind its count (nw > u: not every window is retained)
+                        if (u + 1 > nw || s_at >= HASH_EXT) {
+                            atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
+                        } else {
+                            for (uint32_t x = u; x > 0; --x) ext[x] = ext[x - 1];
+                            ext[0] = u;
+                            p.hash_cnt[(uint64_t)i * p.n + r] = HASH_EXT | (uint32_t)s_at;
+                        }
                     } else {
-                        slot[0] = (uint32_t)s_at;
+                        if (u <= p.hcap) {
+                            for (uint32_t x = 0; x < u; ++x) slot[(uint64_t)x * p.n] = ext[x];
+                        } else {
+                            slot[0] = (uint32_t)s_at;
+                        }
+                        p.hash_cnt[(uint64_t)i * p.n + r] = u;
                     }
-                    p.hash_cnt[(uint64_t)i * p.n + r] = u;
                 }
             }
         }
@@ -636,13 +651,26 @@ __device__ __forceinline__ uint32_t hash_count(const ChainParams& p, uint64_t r,
     // one load from a selected index (a load in each arm of the branch would be waited for at
     // the join, before the loads that follow could issue)
     const uint64_t at = p.hash_offs ? r * p.nk + i : (uint64_t)i * p.n + r;
-    return p.hash_cnt[at];
+    const uint32_t c = p.hash_cnt[at];
+    if (p.hpack && (c & HASH_EXT)) return p.hash_ext[c & ~HASH_EXT];  // (packed: a run in hash_ext)
+    return c;
 }
 
 __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint64_t r, uint32_t i,
                                                      uint32_t cnt, uint64_t& stride) {
     stride = 1;
     if (p.hash_offs) return p.hashes + p.hash_offs[r * p.nk + i];
+    if (p.hpack) {  // (single k slot) after the sets of the wave's earlier reads, or a hash_ext run
+        const uint32_t c = p.hash_cnt[r];
+        if (c & HASH_EXT) return p.hash_ext + (c & ~HASH_EXT) + 1;
+        const uint64_t r0 = r & ~63ull;
+        uint32_t off = 0;
+        for (uint64_t q = r0; q < r; ++q) {
+            const uint32_t cq = p.hash_cnt[q];
+            off += (cq & HASH_EXT) ? 0u : cq;
+        }
+        return p.hashes + r0 * p.hcap + off;
+    }
     const uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * p.n + r;
     if (cnt <= p.hcap) {
         stride = p.n;
@@ -1949,10 +1977,16 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // (the per-chunk bad bits sit in row 0 of the wave's raw columns, dead until hashing starts; the
 // binning counts in wave 0's region, dead once every wave has counted; HCAP + 1 raw rows, the
 // last one the sink of windows past the capacity)
-constexpr uint32_t MAP_P = 384;
-// chained tables: the wave's entries' record keys ([64][8]) and hit masks ([64]) before the
-// per-read overflow flags
-__host__ __device__ inline size_t chn_flag_at(uint32_t) { return (size_t)64 * 8 * 4 + 256; }
+// (MAP_P: 8 per read; at 384 — the mean of cfg3's ~6.0 distinct hashes per read x 64 — half of
+// the waves listed their hashes in two passes, the second one a dependent reload and gather
+// round; profiles/r3_map_p.log)
+constexpr uint32_t MAP_P = 512;
+// chained tables: the wave's entries' record keys ([64][8]) and hit masks ([64]), dead once the
+// entry list is written, then (after the list) the per-read overflow flags
+__host__ __device__ inline size_t chn_flag_at(uint32_t) {
+    const size_t keys = (size_t)64 * 8 * 4 + 256, list = ((size_t)MAP_P * 5 + 15) & ~(size_t)15;
+    return keys > list ? keys : list;
+}
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
 // lanes (u8; compact tables: u32 slot | lane << 26) — or the chained step's keys (tab: 0 wide,
 // 1 block, 2 compact, 3 chained). SKQ_MAP1_LOOSE=1: the round-2 layout (the flags after an 8-B
@@ -2131,33 +2165,59 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             const uint32_t d = q >> 4;
             return __builtin_amdgcn_alignbit(s_codes[d + 1], s_codes[d], (q & 15) * 2);
         };
+        // first window (NtHash::init): the seeds of 16 bases read before their serial rolls
         uint32_t hlo = 0, hhi = 0;
         for (uint32_t b = 0; b < k; b += 16) {
             const uint32_t w = codes16((uint32_t)q0 + b);
+            uint2 e[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (b + j < k) roll33b(hlo, hhi, s_seed[(w >> (2 * j)) & 3u]);
+            for (int j = 0; j < 16; ++j) e[j] = s_seed[(w >> (2 * j)) & 3u];
+            if (b + 16 <= k) {  // (uniform)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) roll33b(hlo, hhi, e[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (b + j < k) roll33b(hlo, hhi, e[j]);
+            }
         }
         uint32_t* raw = s_raw + tid;
         raw[0] = hlo;
         uint32_t nraw = hlo <= T ? 1u : 0u;  // src/sketch.cpp:33-35
         const uint32_t nw = L - k + 1;
         const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
-        for (uint32_t w0 = 1; w0 < nw; w0 += 16) {
-            const uint32_t win = codes16(qin + w0 - 1);
-            const uint32_t wout = codes16(qout + w0 - 1);
-            const uint32_t jn = nw - w0;
+        // windows 1..nw-1, 16 per block (in-base at w + k - 1, out-base at w - 1). A window's roll
+        // term sits at byte (in << 5 | out << 3) of s_tab: with A the in-bases' 2-bit codes
+        // shifted up by 2 and B the out-bases', the nibbles of ce = A:B (even windows) and
+        // co = B:A (odd windows) hold (in, out) pairs, so a term's offset is one shift and one
+        // mask. Every window's value goes to raw slot min(nraw, HCAP) (HCAP: a spare slot); full
+        // blocks skip the window-count test.
+        const unsigned char* tabb = reinterpret_cast<const unsigned char*>(s_tab);
+        auto block = [&](uint32_t w0, uint32_t jn, auto full) {
+            const uint32_t A = codes16(qin + w0 - 1), B = codes16(qout + w0 - 1);
+            const uint32_t A2 = A << 2;
+            const uint32_t ce = (A2 & 0xCCCCCCCCu) | (B & 0x33333333u);
+            const uint32_t co = (A2 & 0x33333333u) | (B & 0xCCCCCCCCu);
+            uint32_t off[16];
+            off[0] = (ce << 3) & 0x78u;
+            off[1] = (co << 1) & 0x78u;
+#pragma unroll
+            for (int j = 2; j < 15; ++j) off[j] = ((j & 1 ? co : ce) >> (2 * j - 3)) & 0x78u;
+            off[15] = ((A >> 30) << 5) | ((B >> 30) << 3);
             uint2 e[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) e[j] = s_tab[((win >> (2 * j)) & 3u) * 4 + ((wout >> (2 * j)) & 3u)];
+            for (int j = 0; j < 16; ++j) e[j] = *reinterpret_cast<const uint2*>(tabb + off[j]);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 roll33b(hlo, hhi, e[j]);
-                const bool rec = hlo <= T && (uint32_t)j < jn;
+                const bool rec = hlo <= T && (decltype(full)::value || (uint32_t)j < jn);
                 raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
                 nraw += rec ? 1u : 0u;
             }
-        }
+        };
+        uint32_t w0 = 1;
+        for (; w0 + 16 <= nw; w0 += 16) block(w0, 16u, std::true_type{});
+        if (w0 < nw) block(w0, nw - w0, std::false_type{});
         if (nraw > HCAP) {
             slow = true;
         } else {
@@ -2171,16 +2231,31 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             for (int j = 0; j < HCAP; ++j) {
                 const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
                 if (keep) {
-                    out[(uint64_t)(m++) * p.n] = v[j];
+                    if (PASS || !p.hpack) out[(uint64_t)m * p.n] = v[j];
+                    ++m;
                     keepm |= 1ull << j;
                 }
             }
             p.hash_cnt[(uint64_t)ks * p.n + r] = m;
         }
     }
+    // packed layout (uniform): the wave's sets one after another in lane order, from the wave's
+    // region — whole 64-B lines, where the padded rows leave most lines partly written (the
+    // kernel's write requests share the fabric's request budget with its gathers)
+    uint32_t hoff = 0;  // (packed) this read's first hash in the wave's region
+    if (!PASS && p.hpack) {
+        const uint32_t mw = (uint32_t)__builtin_popcountll(keepm);
+        hoff = wave_incl_scan(mw, lane) - mw;
+        uint32_t* out = p.hashes + (r - lane) * p.hcap + hoff;
+        uint32_t rank = 0;
+#pragma unroll
+        for (int j = 0; j < HCAP; ++j)
+            if ((keepm >> j) & 1ull) out[rank++] = v[j];
+    }
     if (live && !sk_prev) {
         if (slow) {
             st = ST_SLOW1;
+            if (!PASS && p.hpack) p.hash_cnt[r] = 0;  // (none packed: the slow path marks its run)
             if (!pf_prev) {
                 list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
                 list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
@@ -2402,7 +2477,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 if ((keepm >> j) & 1ull) {
                     const uint32_t e = off + d;
                     if (e >= pb && e < pb + MAP_P) {
-                        s_h[e - pb] = p.hashes[((uint64_t)ks * p.hcap + rank) * p.n + r];
+                        s_h[e - pb] = !PASS && p.hpack ? p.hashes[(r - lane) * p.hcap + hoff + rank]
+                                                       : p.hashes[((uint64_t)ks * p.hcap + rank) * p.n + r];
                         if (CMP) s_x[e - pb] = lane << 26;
                         else s_own[e - pb] = (uint8_t)lane;
                     }
@@ -2726,7 +2802,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     }
                     cp.cand_cnt[r] = nc;
                 }
-            } else if (live) {
+            } else if (live && !sk_prev) {  // (sk_prev: k_slow_wave writes them, maybe already has)
                 cp.cand_cnt[r] = 0;
             }
         }
@@ -2976,8 +3052,17 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+//
+// Early mode (multi-k passes): launched on a side stream right after the first pass, over the list
+// as that pass left it (C_SNAP), it takes the reads that pass sent to the slow path (ST_SLOW1)
+// while the other passes run — they skip such reads. It keeps ST_SLOW1 in their status (the
+// passes still read it), adding ST_EARLY, and marks their list entries (bit 31); the late launch
+// after the last pass skips marked entries, clearing the flags of the ones done here.
+constexpr uint32_t SW_DONE = 0x80000000u;
+
 template <int NK, bool CMP>
-__global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp, uint32_t* ovf3, uint32_t* ovf4) {
+__global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp, uint32_t* ovf3, uint32_t* ovf4,
+                                                  uint32_t early) {
     __shared__ uint32_t s_h[NK][SW_H + 1];
     __shared__ uint32_t s_tid[SW_T], s_c[SW_T];
     __shared__ uint64_t s_key[SW_T];
@@ -2988,7 +3073,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                                             // below are chains of dependent lookups: LDS, not global)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
     const uint32_t lane = threadIdx.x;
-    const uint32_t cnt = min(cp.ctrl[C_OVF2], cp.ovf_cap);
+    const uint32_t cnt = min(cp.ctrl[early ? C_SNAP : C_OVF2], cp.ovf_cap);
     if (blockIdx.x >= cnt) return;  // (uniform) nothing listed for this workgroup
     unsigned long long* bump_h = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(cp.ctrl + C_BUMP_C);
@@ -2997,8 +3082,18 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
     const uint64_t* seed = s_rt + NK * 16;
     const uint64_t n = cp.n;
     for (uint32_t jr = blockIdx.x; jr < cnt; jr += gridDim.x) {
-        const uint32_t r = cp.ovf2[jr];
+        const uint32_t e = cp.ovf2[jr];
+        if (e & SW_DONE) {  // (late launch) done by the early one
+            const uint32_t r = e & ~SW_DONE;
+            if (lane == 0 && (p.status[r] & ST_EARLY)) p.status[r] &= SKQ_STATUS_MASK;
+            continue;
+        }
+        const uint32_t r = e;
         const uint8_t st0 = p.status[r];
+        if (early) {
+            if (!(st0 & ST_SLOW1)) continue;  // (a chain-overflow read: it needs every pass)
+            if (lane == 0) cp.ovf2[jr] = r | SW_DONE;
+        }
         bool hashed = false;  // (uniform) the read's retained sets are in s_h / s_m
         uint8_t st = st0 & SKQ_STATUS_MASK;
         if (st0 & ST_SLOW1) {
@@ -3099,24 +3194,29 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                     }
                     if (lane == 0) s_m[i] = 0;
                     // out: <= hcap in the padded slots, else a bump-allocated run in hash_ext
+                    // (packed layout: always a run, [count, hashes...], marked in hash_cnt)
                     uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * n + r;
                     uint32_t* dst = slot;
                     uint64_t dstride = n;
-                    if (u_all > p.hcap) {
+                    if (u_all > p.hcap || p.hpack) {
+                        const uint32_t need = u_all + (p.hpack ? 1u : 0u);
                         if (lane == 0) {
-                            const unsigned long long at = atomicAdd(bump_h, (unsigned long long)u_all);
-                            s_at = at + u_all <= p.hash_ext_cap ? at : ~0ull;
+                            const unsigned long long at = atomicAdd(bump_h, (unsigned long long)need);
+                            s_at = at + need <= p.hash_ext_cap && at < HASH_EXT ? at : ~0ull;
                             if (s_at == ~0ull) atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         }
                         wave_sync();
                         if (s_at == ~0ull) continue;  // (error recorded; hash_cnt stays 0)
-                        dst = p.hash_ext + s_at;
+                        dst = p.hash_ext + s_at + (p.hpack ? 1u : 0u);
                         dstride = 1;
-                        if (lane == 0) slot[0] = (uint32_t)s_at;
+                        if (lane == 0) {
+                            if (p.hpack) p.hash_ext[s_at] = u_all;
+                            else slot[0] = (uint32_t)s_at;
+                        }
                     }
                     for (uint32_t x = lane; x < u_all; x += 64) dst[(uint64_t)x * dstride] = s_h[i][x];
                     if (lane == 0) {
-                        p.hash_cnt[(uint64_t)i * n + r] = u_all;
+                        p.hash_cnt[(uint64_t)i * n + r] = p.hpack ? (HASH_EXT | (uint32_t)s_at) : u_all;
                         s_m[i] = u_all;
                     }
                 }
@@ -3128,7 +3228,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                 }
                 continue;
             }
-            if (lane == 0) p.status[r] = st;
+            if (lane == 0) p.status[r] = early ? (uint8_t)(st | ST_SLOW1 | ST_EARLY) : st;
             hashed = true;
         }
         if (st != SKQ_READ_OK) {
@@ -3582,7 +3682,8 @@ int launch_count(const ChainParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream) {
+int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream,
+                     bool early) {
     if (cp.n == 0) return 0;
     if (cp.wide != 1 && cp.wide != 3) return -4;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -3592,20 +3693,20 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
     const bool cmp = cp.wide == 3;
     switch (cp.nk) {
     case 1:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<1, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
-        else hipLaunchKernelGGL((k_slow_wave<1, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<1, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        else hipLaunchKernelGGL((k_slow_wave<1, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
         break;
     case 2:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<2, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
-        else hipLaunchKernelGGL((k_slow_wave<2, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<2, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        else hipLaunchKernelGGL((k_slow_wave<2, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
         break;
     case 3:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<3, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
-        else hipLaunchKernelGGL((k_slow_wave<3, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<3, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        else hipLaunchKernelGGL((k_slow_wave<3, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
         break;
     case 4:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<4, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
-        else hipLaunchKernelGGL((k_slow_wave<4, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<4, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        else hipLaunchKernelGGL((k_slow_wave<4, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
         break;
     default: return -4;
     }

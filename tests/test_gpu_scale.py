@@ -113,17 +113,24 @@ def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-def test_cfg5_multi_k_200k_transcripts(tx200k):
-    cpu, _, _ = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501)
+@pytest.mark.parametrize("slow", ["late", "early"])
+def test_cfg5_multi_k_200k_transcripts(tx200k, slow, monkeypatch):
+    """early: the first pass's slow reads on the side stream while the other passes run
+    (SKQ_EARLY_SLOW, opt-in; forced here at any batch size), late: all of them after the last
+    pass (the default)."""
+    monkeypatch.setenv("SKQ_EARLY_SLOW", "2" if slow == "early" else "0")
+    cpu, _, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501)
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
+    assert sl[0] > 100  # the k = 21 pass's capacity sends reads to the slow path
 
 
-@pytest.mark.parametrize("n,seed", [(10_000_000, 1000), (12_500_000, 1003)], ids=["cfg3_10M", "cfg4_rank3_12.5M"])
-def test_full_batch_totals(tx200k, n, seed):
-    """The bench's own batches, one skq_map each: cfg3 (10M x 150 bp, rank 0) and cfg4's per-GPU
-    shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it): per-transcript totals
-    equal the oracle's over the same reads as FASTQ text."""
-    ks, L = [31], 150
+@pytest.mark.parametrize("n,seed,ks", [(10_000_000, 1000, [31]), (12_500_000, 1003, [31]), (2_000_000, 1000, [21, 25, 31])],
+                         ids=["cfg3_10M", "cfg4_rank3_12.5M", "cfg5_2M"])
+def test_full_batch_totals(tx200k, n, seed, ks):
+    """The bench's own batches, one skq_map each: cfg3 (10M x 150 bp, rank 0), cfg4's per-GPU
+    shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it) and 2M reads of cfg5's
+    (multi-k passes): per-transcript totals equal the oracle's over the same reads as FASTQ text."""
+    L = 150
     tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
     index = skq.Index(ks, tx200k.ntx, tables)
     bases, _, _ = synth.reads(tx200k, n, L, seed=seed, err=0.001)  # bench.py's batch of rank seed - 1000

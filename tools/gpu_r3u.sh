@@ -1,0 +1,12 @@
+#!/bin/bash
+# whole GPU suite, then kbench
+set -o pipefail
+t=${1:-r3u}
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+root=$(pwd)
+cd /tmp && export TMPDIR=/tmp && cd "$root"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/${t}_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/${t}_tests.log; exit 1; }
+tail -2 gpurun_out/${t}_tests.log
+timeout -k 10 300 python -u tools/kbench.py --rounds ${ROUNDS:-7} ${KB_ARGS:-} > gpurun_out/${t}_kb.log 2>&1 || { echo "kbench failed"; tail -20 gpurun_out/${t}_kb.log; exit 1; }
+grep -h "wall" gpurun_out/${t}_kb.log | tail -6
