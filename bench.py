@@ -384,7 +384,9 @@ def main(args):
     # (2..4 k slots: one k_map1 pass per k slot, the last merging, timed together as one map)
     fused_name = "k_map1" if nk == 1 else "k_map1 x%d passes" % nk
     if map1:  # the fused kernel: read in, one lookup per hash, postings, hashes + candidates out
-        b_kern = {fused_name: L + 1 + 4 * nk + 4 * h + 8 * h + b_chain, "totals": b_kern["totals"]}
+        # (one k slot: the candidates leave packed, tid | score << 22 in one word; include/skq.h)
+        b_chain_m = b_chain - (4 * Cn if nk == 1 else 0)
+        b_kern = {fused_name: L + 1 + 4 * nk + 4 * h + 8 * h + b_chain_m, "totals": b_kern["totals"]}
     b_path = L + 8 * h + 4 * P + 4 * h + 8 * Cn         # SURVEY.md §8d formula
     names = (fused_name if map1 else "k_sketch", "k_probe", count_name, "totals")
     avg = {name: ms / cnt for name, (ms, cnt) in zip(names, kt) if cnt}

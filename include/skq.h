@@ -136,9 +136,14 @@ uint32_t skq_threshold(double fraction);
  *   x = c & 0x7FFFFFFF: hash_ext[x] hashes at hash_ext[x + 1 ..]; otherwise its c hashes are at
  *   hashes[(r & ~63)*hcap + o .. + c), o = the summed counts of reads (r & ~63) .. r - 1 that are
  *   not runs. skq_session_export gives either layout as flat arrays.
- * candidates (sorted by score desc, tid asc): c = cand_cnt[r]; if c <= ccap candidate j is
- *   (cand_tid[j*n + r], cand_score[j*n + r]); otherwise the (tid, score) pairs are at
- *   cand_ext[2*(cand_tid[r] + j)], cand_ext[2*(cand_tid[r] + j) + 1].
+ * candidates (sorted by score desc, tid asc), cand_layout 0 (padded rows): c = cand_cnt[r]; if
+ *   c <= ccap candidate j is (cand_tid[j*n + r], cand_score[j*n + r]); otherwise the (tid, score)
+ *   pairs are at cand_ext[2*(cand_tid[r] + j)], cand_ext[2*(cand_tid[r] + j) + 1].
+ * candidates, cand_layout 1 (per-wave packed; the single-k skq_map): c = cand_cnt[r]; if
+ *   c & 0x80000000 they are a run of pairs at x = c & 0x7FFFFFFF: cand_ext[2x] of them, pair j at
+ *   cand_ext[2(x + 1 + j)], cand_ext[2(x + 1 + j) + 1]; otherwise candidate j is the word
+ *   cand_tid[(r & ~63)*ccap + o + j] = tid | score << 22, o = the summed counts of reads
+ *   (r & ~63) .. r - 1 that are not runs (cand_score unused).
  * After skq_chain_sketches, hash_cnt/hashes are not the session's (the caller's inputs). */
 typedef struct {
     uint64_t n_reads;
@@ -157,6 +162,7 @@ typedef struct {
     const uint64_t* tx_reads; /* per transcript: reads listing it as a candidate (accumulated) */
     const uint64_t* tx_score; /* per transcript: sum of those reads' scores (accumulated)      */
     uint32_t hash_layout;     /* 0: padded rows, 1: per-wave packed (above)                     */
+    uint32_t cand_layout;     /* 0: padded rows, 1: per-wave packed (above)                     */
     /* (batches of 512k+ reads finish their totals on the session's own side stream, which the
      * launch stream does not wait for: skq_session_results blocks the host until that work is
      * done, so tx_reads / tx_score are current once the caller's stream is synchronized too;

@@ -107,6 +107,7 @@ struct skq_session {
     bool probed = false;       // the last skq_sketch also filled lofs/pflag (fused probe)
     bool have_chain = false;   // candidates belong to the current batch
     bool hash_packed = false;  // hashes in the per-wave packed layout (single-k fused map)
+    bool cand_packed = false;  // candidates likewise
     uint8_t* status = nullptr;
     uint32_t* hash_cnt = nullptr;
     uint32_t* hashes = nullptr;
@@ -1286,6 +1287,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
         *prep = p;
         return 0;
     }
+    s->cand_packed = false;  // (the chain kernels write the padded rows)
     HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
     if (int rc = wait_bins(s, st)) return rc;
     hipEvent_t t0{};
@@ -1357,6 +1359,9 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
         return rc;
+    // candidates packed too, unless the totals would be binned from the padded rows (k_bin)
+    s->cand_packed = s->hash_packed && (!accumulate || cp.slow_totals);
+    cp.cpack = s->cand_packed ? 1u : 0u;
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
@@ -1444,6 +1449,7 @@ int skq_session_results(skq_session* s, skq_results* o) {
     o->hashes = s->hashes;
     o->hash_ext = s->hash_ext;
     o->hash_layout = s->hash_packed ? 1u : 0u;
+    o->cand_layout = s->cand_packed ? 1u : 0u;
     o->cand_cnt = s->cand_cnt;
     o->cand_tid = s->cand_tid;
     o->cand_score = s->cand_score;
@@ -1499,6 +1505,15 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
             HIP_TRY(hipMemcpy(hc.data(), s->hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(st.data(), s->status, n, hipMemcpyDeviceToHost));
         }
+    }
+    std::vector<uint32_t> cx;  // packed candidates: the read's cand_ext run (pair offset) or ~0u
+    if (s->have_chain && s->cand_packed) {
+        cx.assign(n, ~0u);
+        for (uint64_t r = 0; r < n; ++r)
+            if (cc[r] & skq::CAND_EXT) {
+                cx[r] = cc[r] & ~skq::CAND_EXT;
+                HIP_TRY(hipMemcpy(&cc[r], s->cand_ext + 2ull * cx[r], 4, hipMemcpyDeviceToHost));
+            }
     }
     std::vector<uint32_t> xo;  // packed layout: the read's hash_ext run ([count, hashes...]) or ~0u
     if (s->have_sketch && s->hash_packed) {
@@ -1565,12 +1580,31 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
             HIP_TRY(hipMemcpy(t.data(), s->cand_tid, t.size() * 4, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(sc.data(), s->cand_score, sc.size() * 4, hipMemcpyDeviceToHost));
         }
-        uint64_t at = 0;
+        uint64_t at = 0, woff = 0;
         std::vector<uint32_t> ext;
         for (uint64_t r = 0; r < n; ++r) {
             if (cand_offs) cand_offs[r] = at;
             const uint32_t c = cc[r];
-            if (c <= (uint32_t)skq::CCAP) {
+            if (s->cand_packed) {  // per wave in lane order (tid | score << 22), or a run
+                if ((r & 63) == 0) woff = 0;
+                if (cx[r] != ~0u) {
+                    ext.resize(2ull * c);
+                    if (c)
+                        HIP_TRY(hipMemcpy(ext.data(), s->cand_ext + 2ull * (cx[r] + 1), ext.size() * 4,
+                                          hipMemcpyDeviceToHost));
+                    for (uint32_t j = 0; j < c; ++j) {
+                        if (cand_tid) cand_tid[at + j] = ext[2 * j];
+                        if (cand_score) cand_score[at + j] = ext[2 * j + 1];
+                    }
+                } else {
+                    for (uint32_t j = 0; j < c; ++j) {
+                        const uint32_t e = t[(r & ~63ull) * skq::CCAP + woff + j];
+                        if (cand_tid) cand_tid[at + j] = e & 0x3FFFFFu;
+                        if (cand_score) cand_score[at + j] = e >> 22;
+                    }
+                    woff += c;
+                }
+            } else if (c <= (uint32_t)skq::CCAP) {
                 for (uint32_t j = 0; j < c; ++j) {
                     if (cand_tid) cand_tid[at + j] = t[(uint64_t)j * n + r];
                     if (cand_score) cand_score[at + j] = sc[(uint64_t)j * n + r];

@@ -101,18 +101,53 @@ inline int key_bits(uint32_t maxkey) { return std::max(1, 32 - __builtin_clz(max
 
 // ---- appending ----------------------------------------------------------------------------------
 
-// session results (SoA, ext overflow) -> counts of a batch
-__global__ void k_em_cnt(uint64_t n, const uint32_t* cand_cnt, uint64_t* cnt) {
+// session results -> counts of a batch (padded rows with ext overflow, or the packed layout's
+// runs: cand_cnt = 0x80000000 | pair offset of [count, 0], skq.h)
+__global__ void k_em_cnt(uint64_t n, uint32_t packed, const uint32_t* cand_cnt, const uint32_t* cand_ext,
+                         uint64_t* cnt) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < n) cnt[r] = cand_cnt[r];
+    if (r < n) {
+        const uint32_t c = cand_cnt[r];
+        cnt[r] = packed && (c & 0x80000000u) ? cand_ext[2ull * (c & 0x7FFFFFFFu)] : c;
+    }
     if (r == n) cnt[n] = 0;
 }
 
-// copies read r's candidates to tid[offs[r]..], score[offs[r]..] (offs absolute)
-__global__ void k_em_gather(uint64_t n, uint32_t ccap, const uint32_t* cand_cnt, const uint32_t* cand_tid,
-                            const uint32_t* cand_score, const uint32_t* cand_ext, const uint64_t* offs,
-                            uint32_t* tid, uint32_t* score) {
+// copies read r's candidates to tid[offs[r]..], score[offs[r]..] (offs absolute); packed layout:
+// a wave (64 consecutive reads from a multiple of 64: EWG is) scans its counts for the offsets
+__global__ void k_em_gather(uint64_t n, uint32_t ccap, uint32_t packed, const uint32_t* cand_cnt,
+                            const uint32_t* cand_tid, const uint32_t* cand_score, const uint32_t* cand_ext,
+                            const uint64_t* offs, uint32_t* tid, uint32_t* score) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (packed) {
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t c = r < n ? cand_cnt[r] : 0u;
+        const bool run = (c & 0x80000000u) != 0;
+        const uint32_t m = run ? 0u : c;
+        uint32_t incl = m;  // inclusive scan over the wave
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (r >= n) return;
+        const uint64_t o = offs[r];
+        if (run) {
+            const uint32_t* e = cand_ext + 2ull * (c & 0x7FFFFFFFu);
+            const uint32_t k = e[0];
+            for (uint32_t j = 0; j < k; ++j) {
+                tid[o + j] = e[2 * (j + 1)];
+                score[o + j] = e[2 * (j + 1) + 1];
+            }
+        } else {
+            const uint32_t* w = cand_tid + (r - lane) * ccap + (incl - m);
+            for (uint32_t j = 0; j < m; ++j) {
+                tid[o + j] = w[j] & 0x3FFFFFu;
+                score[o + j] = w[j] >> 22;
+            }
+        }
+        return;
+    }
     if (r >= n) return;
     const uint32_t c = cand_cnt[r];
     const uint64_t o = offs[r];
@@ -487,7 +522,7 @@ int skq_em_add_session(skq_em_set* em, skq_session* s, void* stream) {
     if (em->n) EHIP(hipMemcpy(&base, em->offs.p + em->n, 8, hipMemcpyDeviceToHost));
     Buf<uint64_t> cnt;
     EHIP(cnt.reserve(n + 1));
-    k_em_cnt<<<blocks(n + 1, EWG), EWG, 0, st>>>(n, res.cand_cnt, cnt.p);
+    k_em_cnt<<<blocks(n + 1, EWG), EWG, 0, st>>>(n, res.cand_layout, res.cand_cnt, res.cand_ext, cnt.p);
     EHIP(hipGetLastError());
     uint64_t* dst = em->offs.p + em->n;  // exclusive sum of n + 1 counts over [n .. n + n]
     if (int rc = cub_call(em, [&](void* t, size_t& b) {
@@ -501,8 +536,9 @@ int skq_em_add_session(skq_em_set* em, skq_session* s, void* stream) {
     EHIP(hipStreamSynchronize(st));
     EHIP(em->tid.reserve(end + 1, base));
     EHIP(em->score.reserve(end + 1, base));
-    k_em_gather<<<blocks(n, EWG), EWG, 0, st>>>(n, res.ccap, res.cand_cnt, res.cand_tid, res.cand_score,
-                                                res.cand_ext, dst, em->tid.p, em->score.p);
+    static_assert(EWG % 64 == 0, "k_em_gather's packed scan: whole waves of aligned reads");
+    k_em_gather<<<blocks(n, EWG), EWG, 0, st>>>(n, res.ccap, res.cand_layout, res.cand_cnt, res.cand_tid,
+                                                res.cand_score, res.cand_ext, dst, em->tid.p, em->score.p);
     EHIP(hipGetLastError());
     EHIP(hipStreamSynchronize(st));
     em->n += n;

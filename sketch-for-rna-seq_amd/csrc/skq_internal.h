@@ -22,6 +22,7 @@ constexpr uint64_t MAX_BATCH = (1ull << 24) - 1;  // packed per-batch totals hol
 // status flags above SKQ_STATUS_MASK (internal)
 constexpr uint8_t ST_SLOW1 = 0x10;  // sketch handled by the slow path
 constexpr uint32_t HASH_EXT = 0x80000000u;  // packed hash layout: hash_cnt marks a hash_ext run
+constexpr uint32_t CAND_EXT = 0x80000000u;  // packed candidate layout: cand_cnt marks a cand_ext run
 constexpr uint8_t ST_EARLY = 0x20;  // done by the early k_slow_wave (ST_SLOW1 kept until the late one)
 
 // control block (u32 words): the sketch half (words 0-7) is zeroed before every sketch, the
@@ -126,6 +127,11 @@ struct ChainParams {
     const uint32_t* hash_ext;
     const uint64_t* hash_offs; // null => padded layout
     uint32_t hpack;            // 1: per-wave packed layout (SketchParams::hpack)
+    // cpack: candidates in the per-wave packed layout (single-k map; skq.h "candidate layouts"):
+    // read r's, as tid | score << 22, follow those of the reads before it in its wave, from
+    // cand_tid + (r & ~63) * CCAP, except runs in cand_ext, marked cand_cnt[r] = CAND_EXT | pair
+    // offset (pair [count, 0], then the (tid, score) pairs)
+    uint32_t cpack;
     const uint8_t* present;    // null => all k present
     const uint32_t* buckets;
     const uint32_t* lists;    // [n, tid...] per distinct postings list

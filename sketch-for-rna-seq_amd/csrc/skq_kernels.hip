@@ -656,6 +656,9 @@ __device__ __forceinline__ uint32_t hash_count(const ChainParams& p, uint64_t r,
     return c;
 }
 
+// COOP: every lane of the wave calls it for the same read (the packed layout's offset is then one
+// load per lane and a wave sum instead of up to 63 loads in a row)
+template <bool COOP = false>
 __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint64_t r, uint32_t i,
                                                      uint32_t cnt, uint64_t& stride) {
     stride = 1;
@@ -665,9 +668,17 @@ __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint6
         if (c & HASH_EXT) return p.hash_ext + (c & ~HASH_EXT) + 1;
         const uint64_t r0 = r & ~63ull;
         uint32_t off = 0;
-        for (uint64_t q = r0; q < r; ++q) {
-            const uint32_t cq = p.hash_cnt[q];
-            off += (cq & HASH_EXT) ? 0u : cq;
+        if constexpr (COOP) {
+            const uint64_t q = r0 + (threadIdx.x & 63u);
+            const uint32_t cq = q < r ? p.hash_cnt[q] : 0u;
+            off = (cq & HASH_EXT) ? 0u : cq;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) off += (uint32_t)__shfl_xor(off, d, 64);
+        } else {
+            for (uint64_t q = r0; q < r; ++q) {
+                const uint32_t cq = p.hash_cnt[q];
+                off += (cq & HASH_EXT) ? 0u : cq;
+            }
         }
         return p.hashes + r0 * p.hcap + off;
     }
@@ -1979,7 +1990,7 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // last one the sink of windows past the capacity)
 // (MAP_P: 8 per read; at 384 — the mean of cfg3's ~6.0 distinct hashes per read x 64 — half of
 // the waves listed their hashes in two passes, the second one a dependent reload and gather
-// round; profiles/r3_map_p.log)
+// round; profiles/r3_map1_writes.log)
 constexpr uint32_t MAP_P = 512;
 // chained tables: the wave's entries' record keys ([64][8]) and hit masks ([64]), dead once the
 // entry list is written, then (after the list) the per-read overflow flags
@@ -2831,8 +2842,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
                 for (int d = 0; d < TS; ++d) {
                     if (key[d] != ~0u) {
-                        ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
-                        cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                        if (!cp.cpack) {
+                            ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
+                            cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                        }
                         ++nc;
                     }
                 }
@@ -2843,6 +2856,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
         } else if (live) {
             cp.cand_cnt[r] = 0;
+        }
+        if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
+            const uint32_t coff = wave_incl_scan(nc, lane) - nc;
+            uint32_t* out = cp.cand_tid + (r - lane) * CCAP + coff;
+#pragma unroll
+            for (int d = 0; d < TS; ++d)
+                if ((uint32_t)d < nc) out[d] = (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22);
         }
     }
     MAP1_STAMP(4);
@@ -2876,7 +2896,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
             if (!p.tabs[i].present || (p.present && !p.present[r * p.nk + i])) continue;
             const uint32_t hc = hash_count(p, r, i);
             uint64_t hstride;
-            const uint32_t* hs = hash_list(p, r, i, hc, hstride);
+            const uint32_t* hs = hash_list<true>(p, r, i, hc, hstride);
             uint32_t mine = 0;
             for (uint32_t h = t; h < hc; h += WG) {
                 const uint32_t* pp;
@@ -2914,7 +2934,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
             if (!p.tabs[i].present || (p.present && !p.present[r * p.nk + i])) continue;
             const uint32_t hc = hash_count(p, r, i);
             uint64_t hstride;
-            const uint32_t* hs = hash_list(p, r, i, hc, hstride);
+            const uint32_t* hs = hash_list<true>(p, r, i, hc, hstride);
             for (uint32_t h = t; h < hc; h += WG) {
                 const uint32_t* pp;
                 uint32_t np;
@@ -2975,12 +2995,18 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
         uint32_t* ct = p.cand_tid + r;
         uint32_t* cs = p.cand_score + r;
         uint64_t stride = p.n;
-        if (nc > (uint32_t)CCAP) {
+        if (nc > (uint32_t)CCAP || p.cpack) {  // (packed layout: always a run, behind a [count, 0] pair)
+            const uint32_t hd = p.cpack ? 1u : 0u;
             if (t == 0) {
-                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)nc);
-                if (at + nc <= p.cand_ext_cap) {
+                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)(nc + hd));
+                if (at + nc + hd <= p.cand_ext_cap && at < CAND_EXT) {
                     s_at = at;
-                    p.cand_tid[r] = (uint32_t)at;
+                    if (p.cpack) {
+                        p.cand_ext[2 * at] = nc;
+                        p.cand_ext[2 * at + 1] = 0;
+                    } else {
+                        p.cand_tid[r] = (uint32_t)at;
+                    }
                 } else {
                     atomicOr(&p.ctrl[C_ERR2], (uint32_t)E_CAND_EXT);
                     s_at = ~0ull;
@@ -2991,7 +3017,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
                 if (t == 0) p.cand_cnt[r] = 0;
                 continue;
             }
-            ct = p.cand_ext + 2 * s_at;
+            ct = p.cand_ext + 2 * (s_at + hd);
             cs = ct + 1;
             stride = 2;
         }
@@ -3005,7 +3031,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
                 atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
             }
         }
-        if (t == 0) p.cand_cnt[r] = nc;
+        if (t == 0) p.cand_cnt[r] = p.cpack ? (CAND_EXT | (uint32_t)s_at) : nc;
     }
 }
 
@@ -3243,7 +3269,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                 const uint32_t hc = hash_count(cp, r, i);
                 if (hc > SW_H) fits = false;
                 uint64_t hs;
-                const uint32_t* hp = hash_list(cp, r, i, hc, hs);
+                const uint32_t* hp = hash_list<true>(cp, r, i, hc, hs);
                 for (uint32_t x = lane; x < hc && x < SW_H; x += 64) s_h[i][x] = hp[x * hs];
                 if (lane == 0) s_m[i] = hc;
             }
@@ -3357,12 +3383,18 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
         uint32_t* ct = cp.cand_tid + r;
         uint32_t* cs = cp.cand_score + r;
         uint64_t stride = n;
-        if (nc > (uint32_t)CCAP) {
+        if (nc > (uint32_t)CCAP || cp.cpack) {  // (packed layout: always a run, behind a [count, 0] pair)
+            const uint32_t hd = cp.cpack ? 1u : 0u;
             if (lane == 0) {
-                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)nc);
-                if (at + nc <= cp.cand_ext_cap) {
+                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)(nc + hd));
+                if (at + nc + hd <= cp.cand_ext_cap && at < CAND_EXT) {
                     s_at = at;
-                    cp.cand_tid[r] = (uint32_t)at;
+                    if (cp.cpack) {
+                        cp.cand_ext[2 * at] = nc;
+                        cp.cand_ext[2 * at + 1] = 0;
+                    } else {
+                        cp.cand_tid[r] = (uint32_t)at;
+                    }
                 } else {
                     atomicOr(&cp.ctrl[C_ERR2], (uint32_t)E_CAND_EXT);
                     s_at = ~0ull;
@@ -3373,7 +3405,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                 if (lane == 0) cp.cand_cnt[r] = 0;
                 continue;
             }
-            ct = cp.cand_ext + 2 * s_at;
+            ct = cp.cand_ext + 2 * (s_at + hd);
             cs = ct + 1;
             stride = 2;
         }
@@ -3387,7 +3419,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                 atomicAdd(reinterpret_cast<unsigned long long*>(&cp.tx_score[tid]), (unsigned long long)score);
             }
         }
-        if (lane == 0) cp.cand_cnt[r] = nc;
+        if (lane == 0) cp.cand_cnt[r] = cp.cpack ? (CAND_EXT | (uint32_t)s_at) : nc;
     }
 }
 

@@ -33,7 +33,8 @@ class _Results(C.Structure):
     _fields_ = [("n_reads", C.c_uint64), ("nk", C.c_uint32), ("hcap", C.c_uint32), ("ccap", C.c_uint32),
                 ("ntx", C.c_uint32)] + [(n, C.c_void_p) for n in (
                     "status", "hash_cnt", "hashes", "hash_ext", "cand_cnt", "cand_tid", "cand_score",
-                    "cand_ext", "tx_reads", "tx_score")] + [("hash_layout", C.c_uint32)]
+                    "cand_ext", "tx_reads", "tx_score")] + [("hash_layout", C.c_uint32),
+                                                               ("cand_layout", C.c_uint32)]
 
 
 def lib():
