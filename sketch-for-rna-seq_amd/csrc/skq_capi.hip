@@ -71,8 +71,6 @@ struct skq_index {
     const uint32_t* rovf[SKQ_MAX_K] = {};
     uint32_t* d_wdir_t[SKQ_MAX_K] = {};
     const uint32_t* wdir[SKQ_MAX_K] = {};
-    uint32_t* d_wovf_t[SKQ_MAX_K] = {};
-    const uint32_t* wovf[SKQ_MAX_K] = {};
     // compact tables: per distinct k, the pilots; per k slot, the view
     uint16_t* d_wpil_t[SKQ_MAX_K] = {};
     const uint16_t* wpil[SKQ_MAX_K] = {};
@@ -85,8 +83,8 @@ struct skq_index {
     uint64_t chain_len = 0;
     uint64_t chain_bytes = 0;
     double chain_succ = 0;  // mean successor records per entry (stats)
-    // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 4 = block tables,
-    // 5 = compact tables
+    // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 5 = compact tables
+    // (4 was the block tables, retired in round 3: compact tables are smaller and faster)
     int mode = 0;
     bool direct = false;  // every slot with a table has a direct table: the sketch probes
 };
@@ -310,74 +308,6 @@ int build_wide(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, co
             }
     ix->direct = true;
     ix->mode = 3;
-    return 0;
-}
-
-// Block tables: for each distinct k, one 64-B block per 32 possible keys (2 B per key: 429 MB per
-// k at (double)0.05f): [bitmap, overflow base, entry A, entry B]. The first two keys of a block
-// carry their list inline ([n, t0..t5], or [0x80000000 | list offset, t0..t5] when longer), so a
-// retained hash costs the chain one 64-B line and no key compare (the bitmap tells a miss); the
-// 3rd+ key of a block (~1 % of keys at 5 %) keeps its list offset in the overflow array.
-int build_block(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, const std::vector<uint32_t>* dkeys,
-                const std::vector<uint32_t>* dvals, const std::vector<uint32_t>& lists) {
-    hipStream_t st = nullptr;
-    uint64_t need = 0;
-    for (uint32_t t = 0; t < ntables; ++t) {
-        const uint64_t m = dkeys[t].size();
-        if (m == 0) continue;
-        const uint64_t nb = ((uint64_t)dkeys[t].back() >> 5) + 1;
-        std::vector<uint32_t> bidx, content, ovf;
-        for (uint64_t j = 0; j < m; ++j) {
-            const uint32_t key = dkeys[t][j], off = dvals[t][j];
-            if (bidx.empty() || bidx.back() != key >> 5) {
-                bidx.push_back(key >> 5);
-                content.resize(content.size() + 16, 0);
-                content[content.size() - 15] = (uint32_t)ovf.size();
-            }
-            uint32_t* c = content.data() + content.size() - 16;
-            const uint32_t rank = __builtin_popcount(c[0]);
-            c[0] |= 1u << (key & 31);
-            if (rank >= 2) {
-                ovf.push_back(off);
-                continue;
-            }
-            uint32_t* e = c + 2 + 7 * rank;
-            const uint32_t n = lists[off];
-            if (off >= 0x80000000u) return fail(-1, "index too large for block tables");
-            e[0] = n <= 6 ? n : (0x80000000u | off);
-            for (uint32_t q = 0; q < 6 && q < n; ++q) e[1 + q] = lists[off + 1 + q];
-        }
-        ovf.push_back(0);
-        uint32_t *db = nullptr, *dc = nullptr;
-        const uint64_t nz = bidx.size();
-        if (dev_alloc(&ix->d_wdir_t[t], nb * 16) || dev_alloc(&ix->d_wovf_t[t], ovf.size()) ||
-            dev_alloc(&db, nz) || dev_alloc(&dc, nz * 16)) {
-            dev_free(db);
-            dev_free(dc);
-            return fail(-3, "block table allocation failed");
-        }
-        if (hipMemsetAsync(ix->d_wdir_t[t], 0, nb * 64, st) != hipSuccess ||
-            hipMemcpy(ix->d_wovf_t[t], ovf.data(), ovf.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(db, bidx.data(), nz * 4, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(dc, content.data(), nz * 64, hipMemcpyHostToDevice) != hipSuccess ||
-            skq::launch_blk_scatter(ix->d_wdir_t[t], db, dc, nz, st) || hipStreamSynchronize(st) != hipSuccess) {
-            dev_free(db);
-            dev_free(dc);
-            return fail(-3, "block table build failed");
-        }
-        dev_free(db);
-        dev_free(dc);
-        need += nb * 64 + ovf.size() * 4;
-        for (uint32_t i = 0; i < ix->nk; ++i)
-            if (tables[t].k == ix->ks[i]) {
-                ix->wdir[i] = ix->d_wdir_t[t];
-                ix->wovf[i] = ix->d_wovf_t[t];
-                ix->dir_len[i] = nb;
-            }
-    }
-    ix->dir_bytes = need;
-    ix->direct = true;
-    ix->mode = 4;
     return 0;
 }
 
@@ -663,8 +593,9 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
 // Probe structure, for ids that fit k_count3: wide tables when they fit SKQ_DIRECT_MB (default
 // 49152 MiB) and half the free device memory, else compact tables (a few % of the wide tables'
 // size); otherwise 4-B direct tables when they fit, else the bucket table alone.
-// SKQ_PROBE = wide | compact | block | dir | rank forces one kind (A/B measurements and the
-// parity tests, which run every kind).
+// SKQ_PROBE = wide | compact | dir | rank | bucket forces one kind (A/B measurements and the
+// parity tests, which run every kind; anything else is an error). Dir and rank tables serve
+// transcript ids past 2^22, which the wide and compact entries cannot hold.
 int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
                  const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals,
                  const std::vector<uint32_t>& lists) {
@@ -672,6 +603,15 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     if (const char* e = std::getenv("SKQ_DIRECT_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     if (budget == 0) return 0;
     const char* force = std::getenv("SKQ_PROBE");
+    if (force && *force) {
+        static const char* kinds[] = {"wide", "compact", "dir", "rank", "bucket"};
+        bool known = false;
+        for (const char* k : kinds) known |= !std::strcmp(force, k);
+        if (!known) return fail(-1, std::string("SKQ_PROBE: unknown probe kind ") + force);
+        if (!std::strcmp(force, "bucket")) return 0;
+    } else {
+        force = nullptr;
+    }
     if (force && !std::strcmp(force, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
     uint64_t need = 0, len[SKQ_MAX_K] = {};
     for (uint32_t t = 0; t < ntables; ++t) {
@@ -683,10 +623,6 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     if (need == 0) return 0;
     const bool ids_ok = ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull;
     auto forced = [&](const char* kind) { return force && !std::strcmp(force, kind); };
-    if (forced("block")) {
-        if (!ids_ok || need / 2 > budget || need / 2 > fr / 2) return 0;
-        return build_block(ix, ntables, tables, dkeys, dvals, lists);
-    }
     const bool wide_ok = ids_ok && need * 8 <= budget && need * 8 <= fr / 2;
     if (wide_ok && (!force || forced("wide"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
     if (forced("wide")) return 0;  // forced but does not fit: bucket table
@@ -921,7 +857,6 @@ int skq_index_free(skq_index* ix) {
     DeviceGuard g(ix->device);
     for (auto& d : ix->d_dir_t) dev_free(d);
     for (auto& d : ix->d_wdir_t) dev_free(d);
-    for (auto& d : ix->d_wovf_t) dev_free(d);
     for (auto& d : ix->d_wpil_t) dev_free(d);
     for (auto& d : ix->d_rank_t) dev_free(d);
     for (auto& d : ix->d_rovf_t) dev_free(d);
@@ -998,6 +933,7 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
         return rc;
     }
     // totals buckets: at most WG buckets of at most 2^14 ids (the LDS histogram), else direct
+    if (const char* e = std::getenv("SKQ_BIN_BITS")) s->bin_bits = (uint32_t)std::max(8, std::min(14, std::atoi(e)));  // (A/B)
     while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
     s->bin_nb = s->bin_bits <= 14 ? (uint32_t)(((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits) : 0u;
     const uint64_t nW = (max_reads + skq::WG - 1) / skq::WG;
@@ -1262,13 +1198,12 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
     p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
     // wide tables: the count kernel reads the sketch's hashes and gathers the entries itself
-    p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 4 ? 2 : ix->mode == 5 ? 3 : 0;
+    p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 5 ? 3 : 0;
     if (p.wide) {
         p.lofs = const_cast<uint32_t*>(hashes);
         for (uint32_t i = 0; i < ix->nk; ++i) {
             p.wdir[i] = ix->wdir[i];
             p.wdir_len[i] = ix->dir_len[i];
-            p.wovf[i] = ix->wovf[i];
             p.wpil[i] = ix->wpil[i];
             p.wnb[i] = ix->wnb[i];
             p.wseed[i] = ix->wseed[i];
@@ -1311,7 +1246,7 @@ int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
                       fraction, accumulate, s->probed, stream);
 }
 
-// Fused map: k_map1 (compact, wide or block tables, one k slot, a raw capacity of 16 or 32) or
+// Fused map: k_map1 (compact or wide tables, one k slot, a raw capacity of 16 or 32) or
 // k_map1 passes (compact or wide tables, 2..4 k slots); anything else takes the two-kernel path (a caller
 // can always ask for that path itself with skq_sketch + skq_chain)
 static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t fixed_len, uint32_t max_len,

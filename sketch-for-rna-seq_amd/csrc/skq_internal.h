@@ -171,11 +171,6 @@ struct ChainParams {
     // [n, t0..t6] for lists of n <= 7 transcripts, [0x80000000 | list offset, t0..t6] for longer
     // ones (the rest at lists[offset + 8..]), n = 0 for no key; h >= wdir_len[i] is a miss.
     // wide = 1: lofs holds the sketch's hashes themselves (k_count3 only)
-    // Block tables (wide = 2): block h >> 5 of k slot i is 16 words at wdir[i] + 16 * (h >> 5):
-    // [bitmap of its 32 keys, overflow base, entry A (7 words), entry B (7 words)]; the first two
-    // keys of a block (by key order) have entries [n, t0..t5] (n <= 6) or [0x80000000 | list
-    // offset, t0..t5]; the 3rd+ key's list offset is wovf[i][overflow base + rank - 2].
-    // wdir_len = blocks.
     // Compact tables (wide = 3): the same 8-word entries, one per key, placed by a minimal
     // perfect hash (cmp_slot below) in wdir_len[i] slots; wpil[i] holds one 16-bit pilot per
     // bucket of keys (wnb[i] buckets, hash seed wseed[i]). Entry: [key, t0 | F << 22, t1 .. t6],
@@ -187,7 +182,6 @@ struct ChainParams {
     int wide;
     const uint32_t* wdir[SKQ_MAX_K];
     uint64_t wdir_len[SKQ_MAX_K];
-    const uint32_t* wovf[SKQ_MAX_K];
     // chained tables (k_map1 TAB = 3, one k slot): a 128-B entry per possible key
     // (chain_len of them, 8 uint4 each): word 0 = payload words used (0: no key), then records
     // [key, n << 22 | t0, t1 .. t(n-1)] (n <= 7) or [key, 8 << 22, list offset], the entry's own
@@ -241,8 +235,6 @@ int launch_bin(const ChainParams& p, int binned, void* stream);
 // whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)
 bool count_bins(const ChainParams& p);
 int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n, void* stream);
-// block tables: blk[bidx[j]] = content[j] (16 words each)
-int launch_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* content, uint64_t n, void* stream);
 // fills wide entries wdir[keys[j]] from the postings lists at lists[vals[j]]
 int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
                         uint64_t n, void* stream);

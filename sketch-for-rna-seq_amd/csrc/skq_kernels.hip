@@ -1355,8 +1355,7 @@ __device__ __forceinline__ void wide_chunk(Counter<NK, PS>& c, const ChainParams
 
 // one read of k_count3: writes its candidates (and cand_cnt) and returns their number, the
 // first nc of key[] holding them in output order. MODE: 0 = lofs hold list offsets (k_probe or
-// the fused dir/rank probe), 1 = wide tables, 2 = block tables, 3 = compact tables (lofs hold
-// the hashes).
+// the fused dir/rank probe), 1 = wide tables, 3 = compact tables (lofs hold the hashes).
 // Wide tables are gathered by lane pairs (wide_chunk), so in MODE 1 every lane of the wave runs
 // the gather loops, reads past n and inactive reads with no hashes.
 template <int NK, int MODE>
@@ -1398,7 +1397,6 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
         const uint32_t cnt = act && pres ? cnts[i] : 0u;
         const uint32_t cmax = COOP ? max(cnt, pair_swap(cnt)) : cnt;  // the pair's trip count
         const uint32_t* lo_i = p.lofs + (uint64_t)i * p.lcap * p.n + rr;
-        constexpr bool blocks = MODE == 2;
         const uint32_t* wd = p.wdir[i];
         const uint64_t wlen = p.wdir_len[i];
         for (uint32_t j0 = 0; j0 < cmax; j0 += 8) {
@@ -1436,59 +1434,6 @@ __device__ __forceinline__ uint32_t count_read(const ChainParams& p, uint64_t r,
 #pragma unroll
                     for (int u = 0; u < 8; ++u) dl[u] = (j0 + u < cnt && xs[u] < wlen) ? xs[u] << 3 : ~0u;
                     wide_chunk<NK, WG, false>(c, p, wd, dl, xs, t & 1u, i);
-                }
-                continue;
-            }
-            if (blocks) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) dl[u] = (j0 + u < cnt && (xs[u] >> 5) < wlen) ? xs[u] : ~0u;
-#pragma unroll
-                for (int u0 = 0; u0 < 8; u0 += 4) {
-                    if (u0 && !__any(j0 + u0 < cmax)) break;
-                    // one 64-B block per hash, all four in flight; the bitmap says whether the
-                    // key exists and its rank in the block
-                    uint4 b[4][4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const bool v = dl[u0 + u] != ~0u;
-                        const uint4* e = reinterpret_cast<const uint4*>(wd + (v ? (uint64_t)(dl[u0 + u] >> 5) * 16 : 0ull));
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) b[u][q] = e[q];
-                    }
-                    uint32_t tail_lo[4], tail_q0[4];
-                    bool tail[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t x = dl[u0 + u];
-                        const uint32_t bm = b[u][0].x, bit = x & 31u;
-                        const bool hit = x != ~0u && ((bm >> bit) & 1u);
-                        const uint32_t rank = __builtin_popcount(bm & ((1u << bit) - 1u));
-                        const bool a = rank == 0;
-                        const uint32_t meta = a ? b[u][0].z : b[u][2].y;
-                        const uint32_t w1 = a ? b[u][0].w : b[u][2].z, w2 = a ? b[u][1].x : b[u][2].w;
-                        const uint32_t w3 = a ? b[u][1].y : b[u][3].x, w4 = a ? b[u][1].z : b[u][3].y;
-                        const uint32_t w5 = a ? b[u][1].w : b[u][3].z, w6 = a ? b[u][2].x : b[u][3].w;
-                        const bool inl = hit && rank < 2;
-                        const uint32_t n = inl ? ((meta & 0x80000000u) ? 7u : meta) : 0u;
-                        c.insert(w1, 1, i, n > 0);
-                        c.insert(w2, 1, i, n > 1);
-                        c.insert(w3, 1, i, n > 2);
-                        c.insert(w4, 1, i, n > 3);
-                        c.insert(w5, 1, i, n > 4);
-                        c.insert(w6, 1, i, n > 5);
-                        tail[u] = hit && (rank >= 2 || (meta & 0x80000000u));
-                        tail_lo[u] = rank >= 2 ? b[u][0].y + rank - 2 : (meta & 0x7FFFFFFFu);
-                        tail_q0[u] = rank >= 2 ? 0u : 6u;
-                    }
-                    // 3rd+ keys of a block (their list from the overflow array) and lists longer
-                    // than 6 (the rest of the list): rare, one at a time
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (__any(tail[u]) && tail[u]) {
-                            const uint32_t lo = tail_q0[u] == 0 ? p.wovf[i][tail_lo[u]] : tail_lo[u];
-                            const uint32_t len = p.lists[lo];
-                            for (uint32_t q = tail_q0[u]; q < len; ++q) c.insert(p.lists[lo + 1 + q], 1, i, true);
-                        }
                 }
                 continue;
             }
@@ -2000,7 +1945,7 @@ __host__ __device__ inline size_t chn_flag_at(uint32_t) {
 }
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
 // lanes (u8; compact tables: u32 slot | lane << 26) — or the chained step's keys (tab: 0 wide,
-// 1 block, 2 compact, 3 chained). SKQ_MAP1_LOOSE=1: the round-2 layout (the flags after an 8-B
+// 2 compact, 3 chained). SKQ_MAP1_LOOSE=1: the round-2 layout (the flags after an 8-B
 // per-entry list whatever the tables), for A/B.
 inline size_t map1_flag_at(int tab, uint32_t hcap) {
     static const bool loose = [] {
@@ -2041,7 +1986,7 @@ size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
             cp.stamps[((uint64_t)blockIdx.x * (WG / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// TAB: 0 = wide tables, 1 = block tables, 2 = compact tables. PASS: one k slot (p.kslot) of a
+// TAB: 0 = wide tables, 2 = compact tables, 3 = chained tables over wide ones. PASS: one k slot (p.kslot) of a
 // multi-k map: the entries of the read's count table at that k that meet that k's need go out to
 // cp.ktab / cp.kcnt with the need (a transcript short of one k slot's need fails the multi-k
 // filter whatever the other k slots hold), with no candidates or binning; a read any pass lists
@@ -2051,7 +1996,7 @@ size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
 // binned as in the one-k map.
 template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
-    constexpr bool BLK = TAB == 1, CMP = TAB == 2, CHN = TAB == 3;
+    constexpr bool CMP = TAB == 2, CHN = TAB == 3;
     static_assert(PASS || !FINAL, "the final pass is a pass");
     static_assert(!(CHN && PASS), "chained tables serve one k slot");
     const uint32_t ks = PASS ? p.kslot : 0u;
@@ -2524,74 +2469,6 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         constexpr int R = MB;  // rounds of 32 entries in flight together
-        if constexpr (BLK) {
-            // block tables (DESIGN.md "Index"): one 64-B block per hash, the even lane loading
-            // words 0-7 (bitmap, overflow base, entry A's meta and t0..t4), the odd lane words
-            // 8-15 (A's t5, entry B); four swaps give each lane what its half of the inserts
-            // needs (even: t0..t2 of the key's entry, odd: t3..t5)
-            // lane pair q walks entries [q * S, (q + 1) * S): the 32 entries of one round lie S apart,
-            // mostly in different reads' count tables (fewer LDS atomics on one address)
-            const uint32_t S = (ne + 31) >> 5;
-            for (uint32_t e0 = 0; e0 < S; e0 += R) {
-                uint4 b0[R], b1[R];
-                uint32_t own[R], hh[R];
-                bool ok[R];
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    const uint32_t e = (lane >> 1) * S + e0 + u;
-                    const bool in = e0 + u < S && e < ne;
-                    hh[u] = s_h[in ? e : 0];
-                    own[u] = s_own[in ? e : 0];
-                    ok[u] = in && (hh[u] >> 5) < wlen;
-                    const uint4* bp =
-                        reinterpret_cast<const uint4*>(wd + (ok[u] ? (uint64_t)(hh[u] >> 5) * 16 : 0ull) + (odd ? 8u : 0u));
-                    b0[u] = bp[0];
-                    b1[u] = bp[1];
-                }
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    const uint32_t r1 = pair_swap(odd ? b0[u].y : b0[u].x);  // even: B.meta, odd: bitmap
-                    const uint32_t r2 = pair_swap(odd ? b0[u].z : b0[u].z);  // even: B.t0, odd: A.meta
-                    const uint32_t r3 = pair_swap(odd ? b0[u].w : b1[u].z);  // even: B.t1, odd: A.t3
-                    const uint32_t r4 = pair_swap(odd ? b1[u].x : b1[u].w);  // even: B.t2, odd: A.t4
-                    const uint32_t bm = odd ? r1 : b0[u].x, bit = hh[u] & 31u;
-                    const bool hit = ok[u] && ((bm >> bit) & 1u);
-                    const uint32_t rank = __builtin_popcount(bm & ((1u << bit) - 1u));
-                    const bool a = rank == 0;
-                    const uint32_t meta = a ? (odd ? r2 : b0[u].z) : (odd ? b0[u].y : r1);
-                    const uint32_t x0 = a ? (odd ? r3 : b0[u].w) : (odd ? b1[u].y : r2);
-                    const uint32_t x1 = a ? (odd ? r4 : b1[u].x) : (odd ? b1[u].z : r3);
-                    const uint32_t x2 = a ? (odd ? b0[u].x : b1[u].y) : (odd ? b1[u].w : r4);
-                    const bool inl = hit && rank < 2;
-                    const uint32_t n = inl ? ((meta & 0x80000000u) ? 6u : meta) : 0u;
-                    const uint32_t qb = odd ? 3u : 0u;
-                    const uint32_t xs[3] = {x0, x1, x2};
-                    uint32_t olds[3];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
-                        olds[q] = n > qb + q ? atomicCAS(colbase + sl * WG + ((own[u] + sl) & 63u), EMPTY, (xs[q] << 8) | 1u)
-                                             : EMPTY;
-                    }
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const uint32_t x = xs[q], sl = Counter<1, WG>::slot_of(x), o = olds[q];
-                        if (o == EMPTY) continue;
-                        if ((o >> 8) == x) atomicAdd(colbase + sl * WG + ((own[u] + sl) & 63u), 1u);
-                        else ains_probe(x, own[u]);
-                    }
-                    // 3rd+ keys of a block (list from the overflow array) and lists longer than
-                    // 6 (the rest of the list): rare, the even lane, one at a time
-                    const bool tail = !odd && hit && (rank >= 2 || (meta & 0x80000000u));
-                    if (__any(tail) && tail) {
-                        const uint32_t lo = rank >= 2 ? cp.wovf[0][b0[u].y + rank - 2] : (meta & 0x7FFFFFFFu);
-                        const uint32_t len = cp.lists[lo];
-                        for (uint32_t q = rank >= 2 ? 0u : 6u; q < len; ++q) ains(cp.lists[lo + 1 + q], own[u]);
-                    }
-                }
-            }
-            continue;
-        }
         // lane pair q walks entries [q * S, (q + 1) * S): the 32 entries of one round lie S apart,
         // mostly in different reads' count tables (fewer LDS atomics on one address)
         const uint32_t S = (ne + 31) >> 5;
@@ -3699,7 +3576,6 @@ int launch_count(const ChainParams& p, void* stream) {
             return hipGetLastError() == hipSuccess ? 0 : -2;
         }
         if (p.wide == 1) go(std::integral_constant<int, 1>{});
-        else if (p.wide == 2) go(std::integral_constant<int, 2>{});
         else if (p.wide == 3) go(std::integral_constant<int, 3>{});
         else go(std::integral_constant<int, 0>{});
         return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -3751,15 +3627,6 @@ int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-__global__ void k_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* content, uint64_t n) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const uint4* c = reinterpret_cast<const uint4*>(content) + j * 4;
-    uint4* d = reinterpret_cast<uint4*>(blk) + (uint64_t)bidx[j] * 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = c[q];
-}
-
 // wide entry for key keys[j]: [n, t0..t6] (n <= 7) or [0x80000000 | list offset, t0..t6]
 __global__ void k_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
                                uint64_t n) {
@@ -3788,13 +3655,6 @@ int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_blk_scatter(uint32_t* blk, const uint32_t* bidx, const uint32_t* content, uint64_t n, void* stream) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_blk_scatter, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0,
-                       reinterpret_cast<hipStream_t>(stream), blk, bidx, content, n);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
 // SKQ_MAP1_OCC=1: print each k_map1 launch shape's resident workgroups per CU once (stderr)
 static void map1_report_occupancy(const void* kern, size_t lds) {
     static const bool on = [] {
@@ -3818,19 +3678,18 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
     const bool chn = cp.chain != nullptr;
     SketchParams p = p0;
-    const size_t lds = map1_layout(p, chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0, p.hcap);
+    if (!chn && cp.wide != 1 && cp.wide != 3) return -4;
+    const size_t lds = map1_layout(p, chn ? 3 : cp.wide == 3 ? 2 : 0, p.hcap);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     using K = void (*)(SketchParams, ChainParams);
     K kern = nullptr;
     // (MB: gather rounds in flight)
-    switch (p.hcap * 4 + (chn ? 3 : cp.wide == 2 ? 1 : cp.wide == 3 ? 2 : 0)) {
+    switch (p.hcap * 4 + (chn ? 3 : cp.wide == 3 ? 2 : 0)) {
     case 67: kern = k_map1<16, 4, 3>; break;
     case 131: kern = k_map1<32, 4, 3>; break;
     case 64: kern = k_map1<16, 4, 0>; break;
-    case 65: kern = k_map1<16, 4, 1>; break;
     case 66: kern = k_map1<16, 4, 2>; break;
     case 128: kern = k_map1<32, 4, 0>; break;
-    case 129: kern = k_map1<32, 4, 1>; break;
     case 130: kern = k_map1<32, 4, 2>; break;
     default: return -4;
     }

@@ -224,7 +224,7 @@ class Index:
         _check(lib().skq_index_stats(self.h, C.byref(b), C.byref(n), C.byref(m)))
         return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
                     direct=bool(lib().skq_index_direct(self.h)),
-                    probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 4: "block", 5: "compact"}[lib().skq_index_direct(self.h)],
+                    probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 5: "compact"}[lib().skq_index_direct(self.h)],
                     chained=lib().skq_index_chained(self.h))
 
     def free(self):

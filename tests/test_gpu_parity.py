@@ -19,11 +19,11 @@ CHAINED = False  # build: indexes from sequences get the chained tables (skq_ind
 
 
 @pytest.fixture(autouse=True, params=["chain", "compact", "compact-split",
-                                      "block", "wide", "wide-split", "dir", "rank", "bucket"])
+                                      "wide", "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
-    """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables,
-    block tables and wide direct tables gathered by the map or count kernel, 4-B direct and rank
-    tables probed inside the sketch kernel, and the bucket table probed by k_probe
+    """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables
+    and wide direct tables gathered by the map or count kernel, 4-B direct and rank tables
+    (transcript ids past 2^22) probed inside the sketch kernel, and the bucket table probed by k_probe
     (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map).
     "chain": wide tables plus the chained tables (SKQ_CHAIN=1, indexes of one k built from
     sequences); other indexes run as wide."""
@@ -345,7 +345,7 @@ def test_list_lengths_around_the_inline_limit():
 
 def test_crowded_blocks():
     # hand-built index: below each real key, up to 3 extra keys in its 32-key block (ranks 2+ of
-    # a block table take the overflow array), with lists of 1..9 transcripts
+    # a rank table's block take its overflow array), with lists of 1..9 transcripts
     rng = np.random.default_rng(6)
     src = synth.transcriptome(30, seed=18)
     seqs = [src.seq(t) for t in range(src.ntx)]
