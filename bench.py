@@ -412,6 +412,13 @@ def main(args):
         requests = {"random_per_read": h, "achieved": rps, "ceiling": GATHER_CEIL_GPS, "unit": "G/s",
                     "frac": rps / GATHER_CEIL_GPS,
                     "ceiling_source": "tools/micro/gather_bench: random pair-cooperative 32-B gathers, 8 GiB table"}
+        if traffic is not None:  # every memory-side request of the launch, from the calibrated PMC passes
+            kt_ = json.load(open(tf))["kernels"][kname]
+            per = kt_["fetch_size_bytes_per_read"] / 64.0 + kt_["write_bytes_per_read"] / 64.0
+            requests.update(all_per_read=per, all_achieved=n * per / (avg[kname] * 1e-3) / 1e9,
+                            all_note="read + write requests per read from profiles/traffic_%s.json (FETCH_SIZE "
+                                     "and WRITE_SIZE tally 64 B per request); random-gather rates measured: "
+                                     "46-49 G/s from HBM, 54-56 G/s from the Infinity Cache (DESIGN.md §5)" % cname)
     total_reads = n * world * args.steps
     value = total_reads / elapsed
 

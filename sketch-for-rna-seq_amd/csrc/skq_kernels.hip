@@ -1945,15 +1945,11 @@ __host__ __device__ inline size_t chn_flag_at(uint32_t) {
 }
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
 // lanes (u8; compact tables: u32 slot | lane << 26) — or the chained step's keys (tab: 0 wide,
-// 2 compact, 3 chained). SKQ_MAP1_LOOSE=1: the round-2 layout (the flags after an 8-B
-// per-entry list whatever the tables), for A/B.
+// 2 compact, 3 chained). (Round 3 measured 6 workgroups per CU against 5 with the list packed
+// tighter: no change, profiles/r3_ingest_sweep.log.)
 inline size_t map1_flag_at(int tab, uint32_t hcap) {
-    static const bool loose = [] {
-        const char* e = std::getenv("SKQ_MAP1_LOOSE");
-        return e && std::atoi(e) != 0;
-    }();
     if (tab == 3) return chn_flag_at(hcap);
-    if (tab == 2 || loose) return (size_t)MAP_P * 8;
+    if (tab == 2) return (size_t)MAP_P * 8;
     return ((size_t)MAP_P * 5 + 15) & ~(size_t)15;
 }
 inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
