@@ -1964,7 +1964,9 @@ inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
 size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
     p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
     p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
-    return sketch_tab_bytes(1) + (WG / 64) * (size_t)p.map_wave_bytes + ((size_t)hcap + 1) * WG * 4;
+    // (+ the binning epilogue's bucket counters, their own so they are zeroed up front)
+    return sketch_tab_bytes(1) + (WG / 64) * (size_t)p.map_wave_bytes + ((size_t)hcap + 1) * WG * 4 +
+           (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -2009,12 +2011,14 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
     uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * wave_bytes);
     uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + wv * 64);  // (row 0 of the wave's columns)
-    uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1));
+    uint32_t* s_bc = s_raw + (HCAP + 1) * WG;  // the binning's bucket counters (map1_layout)
     const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
     for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot ks's roll terms, then the seeds
         const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
     }
+    if (bin)
+        for (uint32_t e = tid; e <= (uint32_t)WG; e += WG) s_bc[e] = 0;
     __syncthreads();
 
     const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
@@ -2741,7 +2745,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(4);
     // (bin_candidates places entries only after its barriers, when every wave's count tables
     // are dead)
-    if (bin) bin_candidates<true>(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
+    if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
     MAP1_STAMP(5);
 }
 
