@@ -128,18 +128,20 @@ uint32_t skq_threshold(double fraction);
 
 /* Device-resident results of the last call (valid until the next call on the session), in
  * structure-of-arrays layout (n = n_reads of the call, so a wave's accesses are contiguous):
- * hashes, hash_layout 0 (padded rows; skq_sketch, multi-k maps): read r, k slot i:
- *   c = hash_cnt[i*n + r]; if c <= hcap the sorted set is hashes[(i*hcap + j)*n + r] for j < c;
- *   otherwise it is hash_ext[hashes[i*hcap*n + r] + j].
- * hashes, hash_layout 1 (per-wave packed; the single-k skq_map, whose kernel then writes whole
- *   64-B lines): c = hash_cnt[r]; if c & 0x80000000 the set is a run in hash_ext at
- *   x = c & 0x7FFFFFFF: hash_ext[x] hashes at hash_ext[x + 1 ..]; otherwise its c hashes are at
- *   hashes[(r & ~63)*hcap + o .. + c), o = the summed counts of reads (r & ~63) .. r - 1 that are
- *   not runs. skq_session_export gives either layout as flat arrays.
+ * hashes, hash_layout 0 (padded rows; skq_sketch): read r, k slot i: c = hash_cnt[i*n + r]; if
+ *   c <= hcap the sorted set is hashes[(i*hcap + j)*n + r] for j < c; otherwise it is
+ *   hash_ext[hashes[i*hcap*n + r] + j].
+ * hashes, hash_layout 1 (per-wave packed; skq_map's fused kernels, which then write whole 64-B
+ *   lines): c = hash_cnt[i*n + r]; if c & 0x80000000 the set is a run in hash_ext at
+ *   x = c & 0x7FFFFFFF: hash_ext[x] hashes at hash_ext[x + 2 ..] (hash_ext[x + 1]: the read's
+ *   share of the wave's region, kept from the pass that sketched it before a slow path did);
+ *   otherwise its c hashes are at hashes[i*hcap*n + (r & ~63)*hcap + o .. + c), o = the summed
+ *   shares (counts, or the runs' shares) of reads (r & ~63) .. r - 1 at k slot i.
+ *   skq_session_export gives either layout as flat arrays.
  * candidates (sorted by score desc, tid asc), cand_layout 0 (padded rows): c = cand_cnt[r]; if
  *   c <= ccap candidate j is (cand_tid[j*n + r], cand_score[j*n + r]); otherwise the (tid, score)
  *   pairs are at cand_ext[2*(cand_tid[r] + j)], cand_ext[2*(cand_tid[r] + j) + 1].
- * candidates, cand_layout 1 (per-wave packed; the single-k skq_map): c = cand_cnt[r]; if
+ * candidates, cand_layout 1 (per-wave packed; skq_map's fused kernels): c = cand_cnt[r]; if
  *   c & 0x80000000 they are a run of pairs at x = c & 0x7FFFFFFF: cand_ext[2x] of them, pair j at
  *   cand_ext[2(x + 1 + j)], cand_ext[2(x + 1 + j) + 1]; otherwise candidate j is the word
  *   cand_tid[(r & ~63)*ccap + o + j] = tid | score << 22, o = the summed counts of reads

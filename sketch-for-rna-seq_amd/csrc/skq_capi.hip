@@ -913,8 +913,8 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     s->max_len = std::max<uint32_t>(max_len, 1);
     s->ovf_cap = (uint32_t)max_reads;  // any read may take a slow path (e.g. > 4 k slots)
     const uint32_t Lc = std::min<uint32_t>(s->max_len, skq::LFAST);
-    s->hash_ext_cap = std::max<uint64_t>(1ull << 24, (uint64_t)s->ovf_cap * 4);
-    s->cand_ext_cap = 1ull << 22;
+    s->hash_ext_cap = std::max<uint64_t>(1ull << 24, (uint64_t)s->ovf_cap * 4) + (uint64_t)skq::SW_GRID * skq::SW_HCH;
+    s->cand_ext_cap = (1ull << 22) + (uint64_t)skq::SW_GRID * skq::SW_CCH;
     s->scratch_cap = 1ull << 24;
     const uint32_t hcap0 = pick_hcap(Lc, ix->mink, skq_threshold((double)0.05f));
     int rc = 0;
@@ -1029,7 +1029,7 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     p.hash_cnt = s->hash_cnt;
     p.hashes = s->hashes;
     p.hash_ext = s->hash_ext;
-    p.hash_ext_cap = s->hash_ext_cap;
+    p.hash_ext_cap = s->hash_ext_cap - (uint64_t)skq::SW_GRID * skq::SW_HCH;  // (the rest: k_slow_wave's stretches)
     p.ctrl = s->ctrl;
     p.ovf1 = s->ovf1;
     p.ovf_word = skq::C_OVF1;
@@ -1182,7 +1182,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.cand_tid = s->cand_tid;
     p.cand_score = s->cand_score;
     p.cand_ext = s->cand_ext;
-    p.cand_ext_cap = s->cand_ext_cap;
+    p.cand_ext_cap = s->cand_ext_cap - (uint64_t)skq::SW_GRID * skq::SW_CCH;  // (the rest: k_slow_wave's stretches)
     p.scratch = s->scratch;
     p.scratch_cap = s->scratch_cap;
     p.tx_acc = s->tx_acc;
@@ -1266,8 +1266,10 @@ static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t f
 static bool early_slow(const skq::ChainParams& cp) {
     const char* e = std::getenv("SKQ_EARLY_SLOW");
     const int mode = e ? std::atoi(e) : 0;
-    return mode != 0 && cp.nk > 1 && (cp.wide == 1 || cp.wide == 3) && cp.nk <= (uint32_t)skq::NK_FAST &&
-           (mode == 2 || cp.n >= (1u << 19));
+    // (not with the packed layout: a later pass writes the slow reads' zero shares of its region
+    // while the early wave would be rewriting their count words)
+    return mode != 0 && !cp.hpack && cp.nk > 1 && (cp.wide == 1 || cp.wide == 3) &&
+           cp.nk <= (uint32_t)skq::NK_FAST && (mode == 2 || cp.n >= (1u << 19));
 }
 
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
@@ -1288,8 +1290,9 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         }
     }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
-    // one k slot: the hashes in the per-wave packed layout (whole lines written; skq.h)
-    s->hash_packed = s->idx->nk == 1;
+    // the hashes (and the multi-k passes' per-k tables) in the per-wave packed layout (whole
+    // lines written; skq.h)
+    s->hash_packed = true;
     sp.hpack = s->hash_packed ? 1u : 0u;
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
@@ -1450,13 +1453,19 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
                 HIP_TRY(hipMemcpy(&cc[r], s->cand_ext + 2ull * cx[r], 4, hipMemcpyDeviceToHost));
             }
     }
-    std::vector<uint32_t> xo;  // packed layout: the read's hash_ext run ([count, hashes...]) or ~0u
+    // packed layout: per (k slot, read) the hash_ext run ([count, region share, hashes...]) or ~0u,
+    // and the read's share of its wave's region
+    std::vector<uint32_t> xo, sh;
     if (s->have_sketch && s->hash_packed) {
-        xo.assign(n, ~0u);
-        for (uint64_t r = 0; r < n; ++r)
-            if (hc[r] & skq::HASH_EXT) {
-                xo[r] = hc[r] & ~skq::HASH_EXT;
-                HIP_TRY(hipMemcpy(&hc[r], s->hash_ext + xo[r], 4, hipMemcpyDeviceToHost));
+        xo.assign(hc.size(), ~0u);
+        sh = hc;
+        for (uint64_t e = 0; e < hc.size(); ++e)
+            if (hc[e] & skq::HASH_EXT) {
+                xo[e] = hc[e] & ~skq::HASH_EXT;
+                uint32_t h2[2];
+                HIP_TRY(hipMemcpy(h2, s->hash_ext + xo[e], 8, hipMemcpyDeviceToHost));
+                hc[e] = h2[0];
+                sh[e] = h2[1];
             }
     }
     uint64_t th = 0, tc = 0;
@@ -1472,20 +1481,24 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
             std::vector<uint32_t> pad((uint64_t)nk * hcap * n);  // padded: [i][j][r]; packed: per wave
             if (n) HIP_TRY(hipMemcpy(pad.data(), s->hashes, pad.size() * 4, hipMemcpyDeviceToHost));
             uint64_t at = 0;
-            if (s->hash_packed) {  // (one k slot) sets in lane order per wave; runs in hash_ext
-                uint64_t woff = 0;
+            if (s->hash_packed) {  // per k slot, sets in lane order per wave; runs in hash_ext
+                std::vector<uint64_t> woff(nk, 0);
                 for (uint64_t r = 0; r < n; ++r) {
-                    if ((r & 63) == 0) woff = 0;
-                    const uint32_t c = hc[r];
-                    if (xo[r] != ~0u) {
-                        if (hashes && c)
-                            HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + xo[r] + 1, c * 4ull, hipMemcpyDeviceToHost));
-                    } else {
-                        if (hashes) std::copy_n(pad.data() + (r & ~63ull) * hcap + woff, c, hashes + at);
-                        woff += c;
+                    if ((r & 63) == 0) std::fill(woff.begin(), woff.end(), 0);
+                    for (uint32_t i = 0; i < nk; ++i) {
+                        const uint64_t e = (uint64_t)i * n + r;
+                        const uint32_t c = hc[e];
+                        if (xo[e] != ~0u) {
+                            if (hashes && c)
+                                HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + xo[e] + 2, c * 4ull, hipMemcpyDeviceToHost));
+                        } else if (hashes) {
+                            std::copy_n(pad.data() + (uint64_t)i * hcap * n + (r & ~63ull) * hcap + woff[i], c,
+                                        hashes + at);
+                        }
+                        woff[i] += sh[e];
+                        if (hash_offs) hash_offs[r * nk + i] = at;
+                        at += c;
                     }
-                    if (hash_offs) hash_offs[r] = at;
-                    at += c;
                 }
             } else {
                 for (uint64_t r = 0; r < n; ++r)

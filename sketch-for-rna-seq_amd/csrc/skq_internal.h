@@ -22,6 +22,12 @@ constexpr uint64_t MAX_BATCH = (1ull << 24) - 1;  // packed per-batch totals hol
 // status flags above SKQ_STATUS_MASK (internal)
 constexpr uint8_t ST_SLOW1 = 0x10;  // sketch handled by the slow path
 constexpr uint32_t HASH_EXT = 0x80000000u;  // packed hash layout: hash_cnt marks a hash_ext run
+// k_slow_wave's workgroups (a fixed grid) and the stretch of hash_ext / cand_ext each owns past the
+// capacity the bump allocators see (SketchParams::hash_ext_cap, ChainParams::cand_ext_cap), so
+// its runs take no shared atomic until a workgroup's stretch is used up
+constexpr uint32_t SW_GRID = 4096;
+constexpr uint32_t SW_HCH = 2048;  // hash_ext words per workgroup
+constexpr uint32_t SW_CCH = 128;   // cand_ext pairs per workgroup
 constexpr uint32_t CAND_EXT = 0x80000000u;  // packed candidate layout: cand_cnt marks a cand_ext run
 constexpr uint8_t ST_EARLY = 0x20;  // done by the early k_slow_wave (ST_SLOW1 kept until the late one)
 
@@ -92,9 +98,10 @@ struct SketchParams {
     // k_map1's per-wave LDS region (bytes) and the offset of its per-read overflow flags in it,
     // set by the launcher (map1_layout)
     uint32_t map_wave_bytes, map_flag_at;
-    // hpack: the per-wave packed hash layout (single-k map; skq.h "hash layouts"): read r's
-    // hashes follow those of the reads before it in its wave, from hashes + (r & ~63) * hcap,
-    // except runs in hash_ext, marked hash_cnt[r] = HASH_EXT | offset ([count, hashes...])
+    // hpack: the per-wave packed hash layout (fused maps; skq.h "hash layouts"): read r's set
+    // at k slot i follows those of the reads before it in its wave, from hashes + i * hcap * n +
+    // (r & ~63) * hcap, except runs in hash_ext, marked hash_cnt = HASH_EXT | offset ([count,
+    // region share, hashes...]); the multi-k passes' per-k tables (ktab) likewise, TS per read
     uint32_t hpack;
     // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
@@ -127,7 +134,7 @@ struct ChainParams {
     const uint32_t* hash_ext;
     const uint64_t* hash_offs; // null => padded layout
     uint32_t hpack;            // 1: per-wave packed layout (SketchParams::hpack)
-    // cpack: candidates in the per-wave packed layout (single-k map; skq.h "candidate layouts"):
+    // cpack: candidates in the per-wave packed layout (fused maps; skq.h "candidate layouts"):
     // read r's, as tid | score << 22, follow those of the reads before it in its wave, from
     // cand_tid + (r & ~63) * CCAP, except runs in cand_ext, marked cand_cnt[r] = CAND_EXT | pair
     // offset (pair [count, 0], then the (tid, score) pairs)

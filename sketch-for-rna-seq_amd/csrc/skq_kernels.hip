@@ -507,6 +507,14 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
     if (p.fuse) p.pflag[r] = (slow || p.nk > (uint32_t)NK_FAST) ? 1 : 0;
 }
 
+// packed layout: the hashes entry `at` (k slot i, read r: i * n + r) occupies in its wave's region
+// — its count, or for a hash_ext run the share its header keeps (a read a pass sketched, that a
+// slow path re-sketched later, keeps its place in the region)
+__device__ __forceinline__ uint32_t packed_share(const uint32_t* hash_cnt, const uint32_t* hash_ext, uint64_t at) {
+    const uint32_t c = hash_cnt[at];
+    return (c & HASH_EXT) ? hash_ext[(c & ~HASH_EXT) + 1] : c;
+}
+
 // Slow sketch path: one workgroup per listed read. Windows are split into one contiguous
 // segment per thread (each thread rebuilds its segment's first hash, then rolls); retained
 // hashes land in LDS (and in a bump-allocated global region beyond SLOW_CAP), then are sorted
@@ -538,7 +546,10 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
         __syncthreads();
         const uint8_t st = p.nthash ? SKQ_READ_OK
                                     : s_bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
-        for (uint32_t i = t; i < p.nk; i += WG) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
+        // (packed layout: each k slot's count word is replaced when its run is written, the old
+        // one still giving the read's share of the wave's region)
+        if (!p.hpack)
+            for (uint32_t i = t; i < p.nk; i += WG) p.hash_cnt[(uint64_t)i * p.n + r] = 0;
         if (st == SKQ_READ_OK) {
             for (uint32_t i = 0; i < p.nk; ++i) {
                 const uint32_t k = p.ks[i];
@@ -593,8 +604,8 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     const uint32_t incl = block_incl_scan(mine, s_scan, u);
                     uint32_t* dst = slot;
                     uint64_t dstride = p.n;
-                    if (u > p.hcap || p.hpack) {  // (packed layout: always a run, [count, hashes...])
-                        const uint32_t need = u + (p.hpack ? 1u : 0u);
+                    if (u > p.hcap || p.hpack) {  // (packed layout: always a run, [count, share, hashes...])
+                        const uint32_t need = u + (p.hpack ? 2u : 0u);
                         if (t == 0) {
                             s_at = ~0ull;
                             const unsigned long long at = atomicAdd(bump, (unsigned long long)need);
@@ -603,11 +614,15 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                         }
                         __syncthreads();
                         if (s_at == ~0ull) continue;  // uniform
-                        dst = p.hash_ext + s_at + (p.hpack ? 1u : 0u);
+                        dst = p.hash_ext + s_at + (p.hpack ? 2u : 0u);
                         dstride = 1;
                         if (t == 0) {
-                            if (p.hpack) p.hash_ext[s_at] = u;
-                            else slot[0] = (uint32_t)s_at;
+                            if (p.hpack) {
+                                p.hash_ext[s_at + 1] = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
+                                p.hash_ext[s_at] = u;
+                            } else {
+                                slot[0] = (uint32_t)s_at;
+                            }
                         }
                     }
                     uint32_t o = incl - mine;
@@ -619,11 +634,12 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     uint32_t u = 0;
                     for (uint32_t x = 0; x < m; ++x)
                         if (x == 0 || ext[x] != ext[u - 1]) ext[u++] = ext[x];
-                    if (p.hpack) {  // the run behind its count (nw > u: not every window is retained)
-                        if (u + 1 > nw || s_at >= HASH_EXT) {
+                    if (p.hpack) {  // the run behind its header (nw > u + 1: not every window is retained)
+                        if (u + 2 > nw || s_at >= HASH_EXT) {
                             atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         } else {
-                            for (uint32_t x = u; x > 0; --x) ext[x] = ext[x - 1];
+                            for (uint32_t x = u; x > 0; --x) ext[x + 1] = ext[x - 1];
+                            ext[1] = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
                             ext[0] = u;
                             p.hash_cnt[(uint64_t)i * p.n + r] = HASH_EXT | (uint32_t)s_at;
                         }
@@ -663,24 +679,21 @@ __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint6
                                                      uint32_t cnt, uint64_t& stride) {
     stride = 1;
     if (p.hash_offs) return p.hashes + p.hash_offs[r * p.nk + i];
-    if (p.hpack) {  // (single k slot) after the sets of the wave's earlier reads, or a hash_ext run
-        const uint32_t c = p.hash_cnt[r];
-        if (c & HASH_EXT) return p.hash_ext + (c & ~HASH_EXT) + 1;
+    if (p.hpack) {  // after the sets of the wave's earlier reads in k slot i's region, or a hash_ext run
+        const uint64_t ci = (uint64_t)i * p.n;
+        const uint32_t c = p.hash_cnt[ci + r];
+        if (c & HASH_EXT) return p.hash_ext + (c & ~HASH_EXT) + 2;
         const uint64_t r0 = r & ~63ull;
         uint32_t off = 0;
         if constexpr (COOP) {
             const uint64_t q = r0 + (threadIdx.x & 63u);
-            const uint32_t cq = q < r ? p.hash_cnt[q] : 0u;
-            off = (cq & HASH_EXT) ? 0u : cq;
+            off = q < r ? packed_share(p.hash_cnt, p.hash_ext, ci + q) : 0u;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) off += (uint32_t)__shfl_xor(off, d, 64);
         } else {
-            for (uint64_t q = r0; q < r; ++q) {
-                const uint32_t cq = p.hash_cnt[q];
-                off += (cq & HASH_EXT) ? 0u : cq;
-            }
+            for (uint64_t q = r0; q < r; ++q) off += packed_share(p.hash_cnt, p.hash_ext, ci + q);
         }
-        return p.hashes + r0 * p.hcap + off;
+        return p.hashes + ci * p.hcap + r0 * p.hcap + off;
     }
     const uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * p.n + r;
     if (cnt <= p.hcap) {
@@ -2187,7 +2200,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             for (int j = 0; j < HCAP; ++j) {
                 const bool keep = (uint32_t)j < nraw && (j == 0 || v[j] != v[j - 1]);
                 if (keep) {
-                    if (PASS || !p.hpack) out[(uint64_t)m * p.n] = v[j];
+                    if (!p.hpack) out[(uint64_t)m * p.n] = v[j];
                     ++m;
                     keepm |= 1ull << j;
                 }
@@ -2198,11 +2211,11 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // packed layout (uniform): the wave's sets one after another in lane order, from the wave's
     // region — whole 64-B lines, where the padded rows leave most lines partly written (the
     // kernel's write requests share the fabric's request budget with its gathers)
-    uint32_t hoff = 0;  // (packed) this read's first hash in the wave's region
-    if (!PASS && p.hpack) {
+    uint32_t hoff = 0;  // (packed) this read's first hash in the wave's region of k slot ks
+    if (p.hpack) {
         const uint32_t mw = (uint32_t)__builtin_popcountll(keepm);
         hoff = wave_incl_scan(mw, lane) - mw;
-        uint32_t* out = p.hashes + (r - lane) * p.hcap + hoff;
+        uint32_t* out = p.hashes + (uint64_t)ks * p.hcap * p.n + (r - lane) * p.hcap + hoff;
         uint32_t rank = 0;
 #pragma unroll
         for (int j = 0; j < HCAP; ++j)
@@ -2211,7 +2224,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     if (live && !sk_prev) {
         if (slow) {
             st = ST_SLOW1;
-            if (!PASS && p.hpack) p.hash_cnt[r] = 0;  // (none packed: the slow path marks its run)
+            if (p.hpack) p.hash_cnt[(uint64_t)ks * p.n + r] = 0;  // (none packed: the slow path marks its run)
             if (!pf_prev) {
                 list_push(p.ctrl, C_OVF1, C_ERR1, p.ovf1, p.ovf_cap, (uint32_t)r, E_OVF1_FULL);
                 list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
@@ -2222,6 +2235,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         p.status[r] = st;
         // (a later skq_chain on these results reads it; pass mode: listed for the slow path)
         if (!PASS || ks == 0 || slow) p.pflag[r] = slow ? 1 : 0;
+    } else if (live && p.hpack) {  // (pass mode, slow since an earlier pass: no share of this region)
+        p.hash_cnt[(uint64_t)ks * p.n + r] = 0;
     }
     MAP1_STAMP(2);
     // every lane of the wave has left the hashing loop: the staged codes become the parked lists
@@ -2433,8 +2448,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 if ((keepm >> j) & 1ull) {
                     const uint32_t e = off + d;
                     if (e >= pb && e < pb + MAP_P) {
-                        s_h[e - pb] = !PASS && p.hpack ? p.hashes[(r - lane) * p.hcap + hoff + rank]
-                                                       : p.hashes[((uint64_t)ks * p.hcap + rank) * p.n + r];
+                        s_h[e - pb] = p.hpack ? p.hashes[(uint64_t)ks * p.hcap * p.n + (r - lane) * p.hcap + hoff + rank]
+                                              : p.hashes[((uint64_t)ks * p.hcap + rank) * p.n + r];
                         if (CMP) s_x[e - pb] = lane << 26;
                         else s_own[e - pb] = (uint8_t)lane;
                     }
@@ -2562,6 +2577,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     if constexpr (PASS) {
         bool listed = pf_prev != 0;  // listed for the slow path by this or an earlier pass
         uint8_t* kneed = cp.kcnt + (uint64_t)p.nk * cp.n;
+        uint32_t kev[TS];  // (a pass before the last) the entries meeting this k slot's need, or EMPTY
+        uint32_t km = 0;
+#pragma unroll
+        for (int sl = 0; sl < TS; ++sl) kev[sl] = EMPTY;
         if (act) {
             if (s_flag[lane] != 0) {  // more than TS transcripts at this k: the slow chain path
                 if (!listed) list_push(cp.ctrl, C_OVF2, C_ERR2, cp.ovf2, cp.ovf_cap, (uint32_t)r, E_OVF2_FULL);
@@ -2569,23 +2588,45 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 listed = true;
                 if (!FINAL) cp.kcnt[(uint64_t)ks * cp.n + r] = 0;
             } else if (!FINAL) {  // the entries meeting this k slot's need, front-packed, and the need
-                uint32_t ev[TS], mx = 0;
+                uint32_t mx = 0;
 #pragma unroll
                 for (int sl = 0; sl < TS; ++sl) {
-                    ev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
-                    mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
+                    kev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
+                    mx = max(mx, kev[sl] != EMPTY ? kev[sl] & 0xFFu : 0u);
                 }
                 const uint32_t need = need_of(mx);
-                uint32_t m = 0;
 #pragma unroll
-                for (int sl = 0; sl < TS; ++sl)
-                    if (ev[sl] != EMPTY && (ev[sl] & 0xFFu) >= need) cp.ktab[((uint64_t)ks * TS + m++) * cp.n + r] = ev[sl];
-                cp.kcnt[(uint64_t)ks * cp.n + r] = (uint8_t)m;
+                for (int sl = 0; sl < TS; ++sl) {
+                    if (kev[sl] != EMPTY && (kev[sl] & 0xFFu) < need) kev[sl] = EMPTY;
+                    if (kev[sl] != EMPTY) {
+                        if (!cp.hpack) cp.ktab[((uint64_t)ks * TS + km) * cp.n + r] = kev[sl];
+                        ++km;
+                    }
+                }
+                cp.kcnt[(uint64_t)ks * cp.n + r] = (uint8_t)km;
                 kneed[(uint64_t)ks * cp.n + r] = (uint8_t)min(need, 255u);
             }
         } else if (live && !FINAL) {  // (a k slot the index lacks does not filter)
             cp.kcnt[(uint64_t)ks * cp.n + r] = 0;
             kneed[(uint64_t)ks * cp.n + r] = 0;
+        }
+        if (!FINAL && cp.hpack) {  // (uniform) packed: the wave's kept entries in lane order
+            const uint32_t ko = wave_incl_scan(km, lane) - km;
+            uint32_t* out = cp.ktab + (uint64_t)ks * TS * cp.n + (r - lane) * TS + ko;
+            uint32_t rank = 0;
+#pragma unroll
+            for (int sl = 0; sl < TS; ++sl)
+                if (kev[sl] != EMPTY) out[rank++] = kev[sl];
+        }
+        // (last pass, packed) where each earlier pass's entries of this read start in its region
+        uint32_t koff[NK_FAST - 1] = {};
+        if (FINAL && cp.hpack) {  // (uniform)
+#pragma unroll
+            for (int i = 0; i < NK_FAST - 1; ++i)
+                if ((uint32_t)i < ks) {
+                    const uint32_t c = live ? cp.kcnt[(uint64_t)i * cp.n + r] : 0u;
+                    koff[i] = wave_incl_scan(c, lane) - c;
+                }
         }
         if constexpr (FINAL) {
             // the transcripts over the k slots, in registers: slot s holds tid ut[s] (EMPTY: free)
@@ -2624,7 +2665,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     for (int i = 0; i < NK_FAST - 1; ++i)
 #pragma unroll
                         for (int u = 0; u < 8; ++u)
-                            eb[i][u] = j0 + u < mk[i] ? cp.ktab[((uint64_t)i * TS + j0 + u) * cp.n + r] : EMPTY;
+                            eb[i][u] = j0 + u < mk[i]
+                                           ? (cp.hpack ? cp.ktab[(uint64_t)i * TS * cp.n + (r - lane) * TS + koff[i] + j0 + u]
+                                                       : cp.ktab[((uint64_t)i * TS + j0 + u) * cp.n + r])
+                                           : EMPTY;
 #pragma unroll
                     for (int i = 0; i < NK_FAST - 1; ++i)
 #pragma unroll
@@ -2683,8 +2727,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
                     for (int d = 0; d < TS; ++d) {
                         if (key[d] != ~0u) {
-                            ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
-                            cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                            if (!cp.cpack) {
+                                ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
+                                cs[(uint64_t)d * cp.n] = 1023u - (key[d] >> 22);
+                            }
                             ++nc;
                         }
                     }
@@ -2692,6 +2738,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 }
             } else if (live && !sk_prev) {  // (sk_prev: k_slow_wave writes them, maybe already has)
                 cp.cand_cnt[r] = 0;
+            }
+            if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
+                const uint32_t coff = wave_incl_scan(nc, lane) - nc;
+                uint32_t* out = cp.cand_tid + (r - lane) * CCAP + coff;
+#pragma unroll
+                for (int d = 0; d < TS; ++d)
+                    if ((uint32_t)d < nc) out[d] = (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22);
             }
         }
     } else {
@@ -2980,6 +3033,31 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
     if (blockIdx.x >= cnt) return;  // (uniform) nothing listed for this workgroup
     unsigned long long* bump_h = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(cp.ctrl + C_BUMP_C);
+    // runs are cut from chunks this workgroup takes from the shared bump counters: one atomic
+    // per chunk instead of one per run (tens of thousands of runs per batch at cfg5 serialise on
+    // one counter otherwise). (lane 0 only; ~0ull: the region is exhausted, error recorded)
+    __shared__ unsigned long long s_hcur, s_hend, s_ccur, s_cend;
+    if (lane == 0) {  // first this workgroup's own stretches (past the bump allocators' capacity)
+        s_hcur = p.hash_ext_cap + (uint64_t)blockIdx.x * SW_HCH;
+        // (the early launch takes none: the late one, after it, owns them)
+        const bool own = blockIdx.x < SW_GRID && !early;
+        s_hend = s_hcur + (own ? SW_HCH : 0u);
+        s_ccur = cp.cand_ext_cap + (uint64_t)blockIdx.x * SW_CCH;
+        s_cend = s_ccur + (own ? SW_CCH : 0u);
+    }
+    auto take = [](unsigned long long* bump, unsigned long long& cur, unsigned long long& end, uint32_t need,
+                   uint32_t chunk, uint64_t cap) -> unsigned long long {
+        if (cur + need > end) {
+            const uint32_t g = max(need, chunk);
+            const unsigned long long at = atomicAdd(bump, (unsigned long long)g);
+            if (at + g > cap) return ~0ull;
+            cur = at;
+            end = at + g;
+        }
+        const unsigned long long at = cur;
+        cur += need;
+        return at;
+    };
     for (uint32_t e = lane; e < NK * 16 + 4; e += 64) s_rt[e] = p.rolltab[e];
     wave_sync();
     const uint64_t* seed = s_rt + NK * 16;
@@ -3035,7 +3113,8 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
             wave_sync();
             const uint8_t* sb = s_seq;
             st = bad ? SKQ_READ_INVALID : (len < p.maxk ? SKQ_READ_SHORT : SKQ_READ_OK);
-            for (uint32_t i = lane; i < p.nk; i += 64) p.hash_cnt[(uint64_t)i * n + r] = 0;
+            if (!p.hpack)  // (packed layout: the old count words still give the read's region shares)
+                for (uint32_t i = lane; i < p.nk; i += 64) p.hash_cnt[(uint64_t)i * n + r] = 0;
             bool fits = true;
             if (st == SKQ_READ_OK) {
 #pragma unroll
@@ -3097,24 +3176,28 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                     }
                     if (lane == 0) s_m[i] = 0;
                     // out: <= hcap in the padded slots, else a bump-allocated run in hash_ext
-                    // (packed layout: always a run, [count, hashes...], marked in hash_cnt)
+                    // (packed layout: always a run, [count, region share, hashes...], marked in hash_cnt)
                     uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * n + r;
                     uint32_t* dst = slot;
                     uint64_t dstride = n;
                     if (u_all > p.hcap || p.hpack) {
-                        const uint32_t need = u_all + (p.hpack ? 1u : 0u);
+                        const uint32_t need = u_all + (p.hpack ? 2u : 0u);
                         if (lane == 0) {
-                            const unsigned long long at = atomicAdd(bump_h, (unsigned long long)need);
-                            s_at = at + need <= p.hash_ext_cap && at < HASH_EXT ? at : ~0ull;
+                            const unsigned long long at = take(bump_h, s_hcur, s_hend, need, 1024u, p.hash_ext_cap);
+                            s_at = at != ~0ull && at < HASH_EXT ? at : ~0ull;
                             if (s_at == ~0ull) atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         }
                         wave_sync();
                         if (s_at == ~0ull) continue;  // (error recorded; hash_cnt stays 0)
-                        dst = p.hash_ext + s_at + (p.hpack ? 1u : 0u);
+                        dst = p.hash_ext + s_at + (p.hpack ? 2u : 0u);
                         dstride = 1;
                         if (lane == 0) {
-                            if (p.hpack) p.hash_ext[s_at] = u_all;
-                            else slot[0] = (uint32_t)s_at;
+                            if (p.hpack) {
+                                p.hash_ext[s_at + 1] = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * n + r);
+                                p.hash_ext[s_at] = u_all;
+                            } else {
+                                slot[0] = (uint32_t)s_at;
+                            }
                         }
                     }
                     for (uint32_t x = lane; x < u_all; x += 64) dst[(uint64_t)x * dstride] = s_h[i][x];
@@ -3263,8 +3346,8 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
         if (nc > (uint32_t)CCAP || cp.cpack) {  // (packed layout: always a run, behind a [count, 0] pair)
             const uint32_t hd = cp.cpack ? 1u : 0u;
             if (lane == 0) {
-                const unsigned long long at = atomicAdd(bump_c, (unsigned long long)(nc + hd));
-                if (at + nc + hd <= cp.cand_ext_cap && at < CAND_EXT) {
+                const unsigned long long at = take(bump_c, s_ccur, s_cend, nc + hd, 128u, cp.cand_ext_cap);
+                if (at != ~0ull && at < CAND_EXT) {
                     s_at = at;
                     if (cp.cpack) {
                         cp.cand_ext[2 * at] = nc;
@@ -3597,7 +3680,7 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // a 64-lane workgroup per listed read, grid-stride (the list length is on the device); 16
     // per CU fit (LDS ~9 KB, < 100 VGPRs)
-    const dim3 grid(4096), blk(64);
+    const dim3 grid(SW_GRID), blk(64);
     const bool cmp = cp.wide == 3;
     switch (cp.nk) {
     case 1:
