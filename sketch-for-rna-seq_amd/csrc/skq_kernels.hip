@@ -686,8 +686,15 @@ __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint6
         const uint64_t r0 = r & ~63ull;
         uint32_t off = 0;
         if constexpr (COOP) {
+            // (k_slow_wave: other workgroups may be turning these reads' count words into run
+            // marks meanwhile — a mark is stored with release after its run's header, so it is
+            // loaded with acquire before the header is; either word gives the same share)
             const uint64_t q = r0 + (threadIdx.x & 63u);
-            off = q < r ? packed_share(p.hash_cnt, p.hash_ext, ci + q) : 0u;
+            uint32_t cq = 0;
+            if (q < r)
+                cq = __hip_atomic_load(const_cast<uint32_t*>(p.hash_cnt) + ci + q, __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            off = (cq & HASH_EXT) ? p.hash_ext[(cq & ~HASH_EXT) + 1] : cq;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) off += (uint32_t)__shfl_xor(off, d, 64);
         } else {
@@ -3202,7 +3209,11 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                     }
                     for (uint32_t x = lane; x < u_all; x += 64) dst[(uint64_t)x * dstride] = s_h[i][x];
                     if (lane == 0) {
-                        p.hash_cnt[(uint64_t)i * n + r] = p.hpack ? (HASH_EXT | (uint32_t)s_at) : u_all;
+                        if (p.hpack)  // (after the run's header: hash_list's acquire pairs with it)
+                            __hip_atomic_store(p.hash_cnt + (uint64_t)i * n + r, HASH_EXT | (uint32_t)s_at,
+                                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            p.hash_cnt[(uint64_t)i * n + r] = u_all;
                         s_m[i] = u_all;
                     }
                 }

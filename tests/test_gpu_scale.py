@@ -124,12 +124,13 @@ def test_cfg5_multi_k_200k_transcripts(tx200k, slow, monkeypatch):
     assert sl[0] > 100  # the k = 21 pass's capacity sends reads to the slow path
 
 
-@pytest.mark.parametrize("n,seed,ks", [(10_000_000, 1000, [31]), (12_500_000, 1003, [31]), (2_000_000, 1000, [21, 25, 31])],
-                         ids=["cfg3_10M", "cfg4_rank3_12.5M", "cfg5_2M"])
+@pytest.mark.parametrize("n,seed,ks", [(10_000_000, 1000, [31]), (12_500_000, 1003, [31]), (10_000_000, 1000, [21, 25, 31])],
+                         ids=["cfg3_10M", "cfg4_rank3_12.5M", "cfg5_10M"])
 def test_full_batch_totals(tx200k, n, seed, ks):
     """The bench's own batches, one skq_map each: cfg3 (10M x 150 bp, rank 0), cfg4's per-GPU
-    shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it) and 2M reads of cfg5's
-    (multi-k passes): per-transcript totals equal the oracle's over the same reads as FASTQ text."""
+    shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it) and cfg5's batch (10M,
+    multi-k passes, ~37k slow reads whose runs the slow wave writes while it reads other reads'
+    packed offsets): per-transcript totals equal the oracle's over the same reads as FASTQ text."""
     L = 150
     tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
     index = skq.Index(ks, tx200k.ntx, tables)
