@@ -133,10 +133,10 @@ uint32_t skq_threshold(double fraction);
  *   hash_ext[hashes[i*hcap*n + r] + j].
  * hashes, hash_layout 1 (per-wave packed; skq_map's fused kernels, which then write whole 64-B
  *   lines): c = hash_cnt[i*n + r]; if c & 0x80000000 the set is a run in hash_ext at
- *   x = c & 0x7FFFFFFF: hash_ext[x] hashes at hash_ext[x + 2 ..] (hash_ext[x + 1]: the read's
- *   share of the wave's region, kept from the pass that sketched it before a slow path did);
+ *   x = (c & 0xFFFFFF) * 8: hash_ext[x] hashes at hash_ext[x + 2 ..], and (c >> 24) & 0x7F is the
+ *   read's share of its wave's region (the count the pass that sketched it first packed there);
  *   otherwise its c hashes are at hashes[i*hcap*n + (r & ~63)*hcap + o .. + c), o = the summed
- *   shares (counts, or the runs' shares) of reads (r & ~63) .. r - 1 at k slot i.
+ *   shares (counts, or the marks' shares) of reads (r & ~63) .. r - 1 at k slot i.
  *   skq_session_export gives either layout as flat arrays.
  * candidates (sorted by score desc, tid asc), cand_layout 0 (padded rows): c = cand_cnt[r]; if
  *   c <= ccap candidate j is (cand_tid[j*n + r], cand_score[j*n + r]); otherwise the (tid, score)

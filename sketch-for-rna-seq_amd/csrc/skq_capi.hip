@@ -913,7 +913,9 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     s->max_len = std::max<uint32_t>(max_len, 1);
     s->ovf_cap = (uint32_t)max_reads;  // any read may take a slow path (e.g. > 4 k slots)
     const uint32_t Lc = std::min<uint32_t>(s->max_len, skq::LFAST);
-    s->hash_ext_cap = std::max<uint64_t>(1ull << 24, (uint64_t)s->ovf_cap * 4) + (uint64_t)skq::SW_GRID * skq::SW_HCH;
+    // (8-word multiples: packed-layout runs start 8-word aligned; run marks address < RUN_MAX words)
+    s->hash_ext_cap = std::min<uint64_t>(skq::RUN_MAX, ((std::max<uint64_t>(1ull << 24, (uint64_t)s->ovf_cap * 4) + 7) & ~7ull) +
+                                                         (uint64_t)skq::SW_GRID * skq::SW_HCH);
     s->cand_ext_cap = (1ull << 22) + (uint64_t)skq::SW_GRID * skq::SW_CCH;
     s->scratch_cap = 1ull << 24;
     const uint32_t hcap0 = pick_hcap(Lc, ix->mink, skq_threshold((double)0.05f));
@@ -1461,11 +1463,9 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
         sh = hc;
         for (uint64_t e = 0; e < hc.size(); ++e)
             if (hc[e] & skq::HASH_EXT) {
-                xo[e] = hc[e] & ~skq::HASH_EXT;
-                uint32_t h2[2];
-                HIP_TRY(hipMemcpy(h2, s->hash_ext + xo[e], 8, hipMemcpyDeviceToHost));
-                hc[e] = h2[0];
-                sh[e] = h2[1];
+                xo[e] = (uint32_t)skq::run_at(hc[e]);
+                sh[e] = skq::run_share(hc[e]);
+                HIP_TRY(hipMemcpy(&hc[e], s->hash_ext + xo[e], 4, hipMemcpyDeviceToHost));
             }
     }
     uint64_t th = 0, tc = 0;

@@ -22,6 +22,16 @@ constexpr uint64_t MAX_BATCH = (1ull << 24) - 1;  // packed per-batch totals hol
 // status flags above SKQ_STATUS_MASK (internal)
 constexpr uint8_t ST_SLOW1 = 0x10;  // sketch handled by the slow path
 constexpr uint32_t HASH_EXT = 0x80000000u;  // packed hash layout: hash_cnt marks a hash_ext run
+// A run's mark carries the read's share of its wave's region itself, so a reader summing the
+// shares never needs a run header another workgroup may still be writing: HASH_EXT | share << 24
+// | run offset / 8 (runs start 8-word aligned; hash_ext below RUN_MAX words).
+constexpr uint64_t RUN_MAX = (1ull << 24) * 8;
+constexpr uint32_t run_mark(uint64_t at, uint32_t share) {
+    return HASH_EXT | (share << 24) | (uint32_t)(at >> 3);
+}
+constexpr uint64_t run_at(uint32_t c) { return (uint64_t)(c & 0xFFFFFFu) << 3; }
+constexpr uint32_t run_share(uint32_t c) { return (c >> 24) & 0x7Fu; }
+constexpr uint32_t run_words(uint32_t need) { return (need + 7u) & ~7u; }
 // k_slow_wave's workgroups (a fixed grid) and the stretch of hash_ext / cand_ext each owns past the
 // capacity the bump allocators see (SketchParams::hash_ext_cap, ChainParams::cand_ext_cap), so
 // its runs take no shared atomic until a workgroup's stretch is used up

@@ -512,7 +512,7 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
 // slow path re-sketched later, keeps its place in the region)
 __device__ __forceinline__ uint32_t packed_share(const uint32_t* hash_cnt, const uint32_t* hash_ext, uint64_t at) {
     const uint32_t c = hash_cnt[at];
-    return (c & HASH_EXT) ? hash_ext[(c & ~HASH_EXT) + 1] : c;
+    return (c & HASH_EXT) ? run_share(c) : c;
 }
 
 // Slow sketch path: one workgroup per listed read. Windows are split into one contiguous
@@ -560,8 +560,8 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     s_cnt = 0;
                     s_at = ~0ull;
                     if (nw > SLOW_CAP) {
-                        const unsigned long long at = atomicAdd(bump, (unsigned long long)nw);
-                        if (at + nw <= p.hash_ext_cap) s_at = at;
+                        const unsigned long long at = atomicAdd(bump, (unsigned long long)run_words((uint32_t)nw));
+                        if (at + run_words((uint32_t)nw) <= p.hash_ext_cap && at + nw <= RUN_MAX) s_at = at;
                         else atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                     }
                 }
@@ -604,12 +604,13 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     const uint32_t incl = block_incl_scan(mine, s_scan, u);
                     uint32_t* dst = slot;
                     uint64_t dstride = p.n;
+                    uint32_t s_share = 0;  // (thread 0: the read's region share, kept in its run mark)
                     if (u > p.hcap || p.hpack) {  // (packed layout: always a run, [count, share, hashes...])
-                        const uint32_t need = u + (p.hpack ? 2u : 0u);
+                        const uint32_t need = run_words(u + (p.hpack ? 2u : 0u));
                         if (t == 0) {
                             s_at = ~0ull;
                             const unsigned long long at = atomicAdd(bump, (unsigned long long)need);
-                            if (at + need <= p.hash_ext_cap && at < HASH_EXT) s_at = at;
+                            if (at + need <= p.hash_ext_cap && at + need <= RUN_MAX) s_at = at;
                             else atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         }
                         __syncthreads();
@@ -618,7 +619,8 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                         dstride = 1;
                         if (t == 0) {
                             if (p.hpack) {
-                                p.hash_ext[s_at + 1] = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
+                                s_share = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
+                                p.hash_ext[s_at + 1] = s_share;
                                 p.hash_ext[s_at] = u;
                             } else {
                                 slot[0] = (uint32_t)s_at;
@@ -628,20 +630,21 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     uint32_t o = incl - mine;
                     for (uint32_t x = a; x < b; ++x)
                         if (x == 0 || s_buf[x] != s_buf[x - 1]) dst[(uint64_t)(o++) * dstride] = s_buf[x];
-                    if (t == 0) p.hash_cnt[(uint64_t)i * p.n + r] = p.hpack ? (HASH_EXT | (uint32_t)s_at) : u;
+                    if (t == 0) p.hash_cnt[(uint64_t)i * p.n + r] = p.hpack ? run_mark(s_at, s_share) : u;
                 } else if (t == 0) {  // more windows than LDS holds: serial, in place
                     serial_sort(ext, m);
                     uint32_t u = 0;
                     for (uint32_t x = 0; x < m; ++x)
                         if (x == 0 || ext[x] != ext[u - 1]) ext[u++] = ext[x];
                     if (p.hpack) {  // the run behind its header (nw > u + 1: not every window is retained)
-                        if (u + 2 > nw || s_at >= HASH_EXT) {
+                        if (u + 2 > nw) {
                             atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         } else {
+                            const uint32_t sh = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
                             for (uint32_t x = u; x > 0; --x) ext[x + 1] = ext[x - 1];
-                            ext[1] = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
+                            ext[1] = sh;
                             ext[0] = u;
-                            p.hash_cnt[(uint64_t)i * p.n + r] = HASH_EXT | (uint32_t)s_at;
+                            p.hash_cnt[(uint64_t)i * p.n + r] = run_mark(s_at, sh);
                         }
                     } else {
                         if (u <= p.hcap) {
@@ -668,7 +671,7 @@ __device__ __forceinline__ uint32_t hash_count(const ChainParams& p, uint64_t r,
     // the join, before the loads that follow could issue)
     const uint64_t at = p.hash_offs ? r * p.nk + i : (uint64_t)i * p.n + r;
     const uint32_t c = p.hash_cnt[at];
-    if (p.hpack && (c & HASH_EXT)) return p.hash_ext[c & ~HASH_EXT];  // (packed: a run in hash_ext)
+    if (p.hpack && (c & HASH_EXT)) return p.hash_ext[run_at(c)];  // (packed: a run in hash_ext)
     return c;
 }
 
@@ -682,19 +685,14 @@ __device__ __forceinline__ const uint32_t* hash_list(const ChainParams& p, uint6
     if (p.hpack) {  // after the sets of the wave's earlier reads in k slot i's region, or a hash_ext run
         const uint64_t ci = (uint64_t)i * p.n;
         const uint32_t c = p.hash_cnt[ci + r];
-        if (c & HASH_EXT) return p.hash_ext + (c & ~HASH_EXT) + 2;
+        if (c & HASH_EXT) return p.hash_ext + run_at(c) + 2;
         const uint64_t r0 = r & ~63ull;
         uint32_t off = 0;
         if constexpr (COOP) {
             // (k_slow_wave: other workgroups may be turning these reads' count words into run
-            // marks meanwhile — a mark is stored with release after its run's header, so it is
-            // loaded with acquire before the header is; either word gives the same share)
+            // marks meanwhile; either word gives the same share, the mark carrying it itself)
             const uint64_t q = r0 + (threadIdx.x & 63u);
-            uint32_t cq = 0;
-            if (q < r)
-                cq = __hip_atomic_load(const_cast<uint32_t*>(p.hash_cnt) + ci + q, __ATOMIC_ACQUIRE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            off = (cq & HASH_EXT) ? p.hash_ext[(cq & ~HASH_EXT) + 1] : cq;
+            off = q < r ? packed_share(p.hash_cnt, p.hash_ext, ci + q) : 0u;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) off += (uint32_t)__shfl_xor(off, d, 64);
         } else {
@@ -3187,11 +3185,12 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                     uint32_t* slot = p.hashes + (uint64_t)i * p.hcap * n + r;
                     uint32_t* dst = slot;
                     uint64_t dstride = n;
+                    uint32_t s_share = 0;  // (lane 0: the read's region share, kept in its run mark)
                     if (u_all > p.hcap || p.hpack) {
-                        const uint32_t need = u_all + (p.hpack ? 2u : 0u);
+                        const uint32_t need = run_words(u_all + (p.hpack ? 2u : 0u));
                         if (lane == 0) {
                             const unsigned long long at = take(bump_h, s_hcur, s_hend, need, 1024u, p.hash_ext_cap);
-                            s_at = at != ~0ull && at < HASH_EXT ? at : ~0ull;
+                            s_at = at != ~0ull && at + need <= RUN_MAX ? at : ~0ull;
                             if (s_at == ~0ull) atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                         }
                         wave_sync();
@@ -3200,7 +3199,8 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                         dstride = 1;
                         if (lane == 0) {
                             if (p.hpack) {
-                                p.hash_ext[s_at + 1] = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * n + r);
+                                s_share = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * n + r);
+                                p.hash_ext[s_at + 1] = s_share;
                                 p.hash_ext[s_at] = u_all;
                             } else {
                                 slot[0] = (uint32_t)s_at;
@@ -3209,11 +3209,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                     }
                     for (uint32_t x = lane; x < u_all; x += 64) dst[(uint64_t)x * dstride] = s_h[i][x];
                     if (lane == 0) {
-                        if (p.hpack)  // (after the run's header: hash_list's acquire pairs with it)
-                            __hip_atomic_store(p.hash_cnt + (uint64_t)i * n + r, HASH_EXT | (uint32_t)s_at,
-                                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                        else
-                            p.hash_cnt[(uint64_t)i * n + r] = u_all;
+                        p.hash_cnt[(uint64_t)i * n + r] = p.hpack ? run_mark(s_at, s_share) : u_all;
                         s_m[i] = u_all;
                     }
                 }
