@@ -147,8 +147,6 @@ struct skq_session {
     // side stream for the totals (k_bin_sum runs beside the slow paths), created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork{}, ev_join[2]{};  // ev_join[b]: k_bin_sum of the last batch of parity b
-    hipEvent_t ev_early{};               // the early k_slow_wave (multi-k passes) is done
-    bool early_pending = false;
     bool join_rec[2] = {false, false};
 };
 
@@ -969,7 +967,6 @@ int skq_session_free(skq_session* s) {
         (void)hipEventDestroy(s->ev_fork);
         (void)hipEventDestroy(s->ev_join[0]);
         (void)hipEventDestroy(s->ev_join[1]);
-        (void)hipEventDestroy(s->ev_early);
     }
     dev_free(s->status);
     dev_free(s->hash_cnt);
@@ -1095,14 +1092,13 @@ static int wait_totals(skq_session* s, hipStream_t st) {
 // with atomics (commuting with the slow paths' direct adds). For batches of 512k+ reads it runs on
 // the session's side stream and nothing on the launch stream waits for it: it overlaps the slow
 // paths and the next batch's map kernel, which bins into the other buffer (wait_bins).
-// the side stream (totals binning, the early k_slow_wave) and its events
+// the side stream (totals binning) and its events
 static int ensure_side(skq_session* s) {
     if (s->side) return 0;
     HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_join[0], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_join[1], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_early, hipEventDisableTiming));
     return 0;
 }
 
@@ -1126,10 +1122,6 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
     }
     if (sp && (p.wide == 1 || p.wide == 3) && p.nk <= (uint32_t)skq::NK_FAST) {
         // the fused map's slow reads: the wave path first, the general paths for what it leaves
-        if (s->early_pending) {  // (its marks on the list are read by the late launch)
-            HIP_TRY(hipStreamWaitEvent(st, s->ev_early, 0));
-            s->early_pending = false;
-        }
         if (int rc = skq::launch_slow_wave(*sp, p, s->ovf3, s->ovf4, st))
             return fail(-3, rc == -4 ? "slow path: unsupported tables" : "slow-path launch failed");
         skq::SketchParams sp2 = *sp;
@@ -1262,18 +1254,6 @@ static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t f
     return (ix->mode == 3 || ix->mode == 5) && ix->nk <= (uint32_t)skq::NK_FAST && (hcap == 16 || hcap == 32);
 }
 
-// the early k_slow_wave (multi-k passes, large batches): opt-in, SKQ_EARLY_SLOW=1 (from 512k
-// reads) or 2 (any batch; tests). Off by default: the passes run at the fabric's request ceiling,
-// so the overlapped slow wave's requests slow them by as much as it saves (profiles/r3_early_slow.log)
-static bool early_slow(const skq::ChainParams& cp) {
-    const char* e = std::getenv("SKQ_EARLY_SLOW");
-    const int mode = e ? std::atoi(e) : 0;
-    // (not with the packed layout: a later pass writes the slow reads' zero shares of its region
-    // while the early wave would be rewriting their count words)
-    return mode != 0 && !cp.hpack && cp.nk > 1 && (cp.wide == 1 || cp.wide == 3) &&
-           cp.nk <= (uint32_t)skq::NK_FAST && (mode == 2 || cp.n >= (1u << 19));
-}
-
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
                      uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction, int accumulate,
                      void* stream) {
@@ -1322,18 +1302,6 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
             const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(ml, s->max_len), skq::LFAST));
             rc = skq::launch_map1_pass(pi, cp, std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, pass_sigmas())),
                                        i + 1 == nk, stream);
-            if (!rc && i == 0 && early_slow(cp)) {
-                // the first pass's slow reads (ST_SLOW1) on the side stream while the others run:
-                // the list's length now, then the early k_slow_wave over that much of it
-                HIP_TRY(hipMemcpyAsync(s->ctrl + skq::C_SNAP, s->ctrl + skq::C_OVF2, 4, hipMemcpyDeviceToDevice, st));
-                if (int e = ensure_side(s)) return e;
-                HIP_TRY(hipEventRecord(s->ev_fork, st));
-                HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
-                if (skq::launch_slow_wave(sp, cp, s->ovf3, s->ovf4, s->side, true))
-                    return fail(-3, "slow-path launch failed");
-                HIP_TRY(hipEventRecord(s->ev_early, s->side));
-                s->early_pending = true;
-            }
         }
     }
     if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");

@@ -39,7 +39,6 @@ constexpr uint32_t SW_GRID = 4096;
 constexpr uint32_t SW_HCH = 2048;  // hash_ext words per workgroup
 constexpr uint32_t SW_CCH = 128;   // cand_ext pairs per workgroup
 constexpr uint32_t CAND_EXT = 0x80000000u;  // packed candidate layout: cand_cnt marks a cand_ext run
-constexpr uint8_t ST_EARLY = 0x20;  // done by the early k_slow_wave (ST_SLOW1 kept until the late one)
 
 // control block (u32 words): the sketch half (words 0-7) is zeroed before every sketch, the
 // chain half (words 8-15) before every chain.
@@ -53,7 +52,6 @@ enum Ctrl : int {
     C_BUMP_S = 10,  // u64 (words 10-11): chain scratch u64 words used
     C_BUMP_C = 12,  // u64 (words 12-13): cand_ext pairs used
     C_OVF4 = 14,    // second-level chain list (k_slow_wave -> k_chain_slow)
-    C_SNAP = 15,    // the chain list's length after the first multi-k pass (the early k_slow_wave's)
     C_WORDS = 16
 };
 enum Err : uint32_t {
@@ -241,8 +239,7 @@ int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
 // the wave slow path behind k_map1 and its passes (wide or compact tables, <= 4 k slots; -4 otherwise):
 // the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
-int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream,
-                     bool early = false);
+int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);
 int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx, void* stream);
 // per-transcript totals of the batch's final candidates into p.tx_acc (k_bin + k_bin_sum), then
 // launch_fold_totals adds them into p.tx_reads / p.tx_score with atomics (commuting with the slow

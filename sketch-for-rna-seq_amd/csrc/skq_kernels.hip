@@ -2741,7 +2741,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     }
                     cp.cand_cnt[r] = nc;
                 }
-            } else if (live && !sk_prev) {  // (sk_prev: k_slow_wave writes them, maybe already has)
+            } else if (live && !sk_prev) {  // (sk_prev: k_slow_wave writes them)
                 cp.cand_cnt[r] = 0;
             }
             if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
@@ -3013,17 +3013,9 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-//
-// Early mode (multi-k passes): launched on a side stream right after the first pass, over the list
-// as that pass left it (C_SNAP), it takes the reads that pass sent to the slow path (ST_SLOW1)
-// while the other passes run — they skip such reads. It keeps ST_SLOW1 in their status (the
-// passes still read it), adding ST_EARLY, and marks their list entries (bit 31); the late launch
-// after the last pass skips marked entries, clearing the flags of the ones done here.
-constexpr uint32_t SW_DONE = 0x80000000u;
 
 template <int NK, bool CMP>
-__global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp, uint32_t* ovf3, uint32_t* ovf4,
-                                                  uint32_t early) {
+__global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp, uint32_t* ovf3, uint32_t* ovf4) {
     __shared__ uint32_t s_h[NK][SW_H + 1];
     __shared__ uint32_t s_tid[SW_T], s_c[SW_T];
     __shared__ uint64_t s_key[SW_T];
@@ -3034,7 +3026,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                                             // below are chains of dependent lookups: LDS, not global)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
     const uint32_t lane = threadIdx.x;
-    const uint32_t cnt = min(cp.ctrl[early ? C_SNAP : C_OVF2], cp.ovf_cap);
+    const uint32_t cnt = min(cp.ctrl[C_OVF2], cp.ovf_cap);
     if (blockIdx.x >= cnt) return;  // (uniform) nothing listed for this workgroup
     unsigned long long* bump_h = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(cp.ctrl + C_BUMP_C);
@@ -3044,8 +3036,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
     __shared__ unsigned long long s_hcur, s_hend, s_ccur, s_cend;
     if (lane == 0) {  // first this workgroup's own stretches (past the bump allocators' capacity)
         s_hcur = p.hash_ext_cap + (uint64_t)blockIdx.x * SW_HCH;
-        // (the early launch takes none: the late one, after it, owns them)
-        const bool own = blockIdx.x < SW_GRID && !early;
+        const bool own = blockIdx.x < SW_GRID;
         s_hend = s_hcur + (own ? SW_HCH : 0u);
         s_ccur = cp.cand_ext_cap + (uint64_t)blockIdx.x * SW_CCH;
         s_cend = s_ccur + (own ? SW_CCH : 0u);
@@ -3068,18 +3059,8 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
     const uint64_t* seed = s_rt + NK * 16;
     const uint64_t n = cp.n;
     for (uint32_t jr = blockIdx.x; jr < cnt; jr += gridDim.x) {
-        const uint32_t e = cp.ovf2[jr];
-        if (e & SW_DONE) {  // (late launch) done by the early one
-            const uint32_t r = e & ~SW_DONE;
-            if (lane == 0 && (p.status[r] & ST_EARLY)) p.status[r] &= SKQ_STATUS_MASK;
-            continue;
-        }
-        const uint32_t r = e;
+        const uint32_t r = cp.ovf2[jr];
         const uint8_t st0 = p.status[r];
-        if (early) {
-            if (!(st0 & ST_SLOW1)) continue;  // (a chain-overflow read: it needs every pass)
-            if (lane == 0) cp.ovf2[jr] = r | SW_DONE;
-        }
         bool hashed = false;  // (uniform) the read's retained sets are in s_h / s_m
         uint8_t st = st0 & SKQ_STATUS_MASK;
         if (st0 & ST_SLOW1) {
@@ -3221,7 +3202,7 @@ __global__ __launch_bounds__(64) void k_slow_wave(SketchParams p, ChainParams cp
                 }
                 continue;
             }
-            if (lane == 0) p.status[r] = early ? (uint8_t)(st | ST_SLOW1 | ST_EARLY) : st;
+            if (lane == 0) p.status[r] = st;
             hashed = true;
         }
         if (st != SKQ_READ_OK) {
@@ -3680,8 +3661,7 @@ int launch_count(const ChainParams& p, void* stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream,
-                     bool early) {
+int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream) {
     if (cp.n == 0) return 0;
     if (cp.wide != 1 && cp.wide != 3) return -4;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -3691,20 +3671,20 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
     const bool cmp = cp.wide == 3;
     switch (cp.nk) {
     case 1:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<1, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
-        else hipLaunchKernelGGL((k_slow_wave<1, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<1, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<1, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
         break;
     case 2:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<2, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
-        else hipLaunchKernelGGL((k_slow_wave<2, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<2, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<2, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
         break;
     case 3:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<3, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
-        else hipLaunchKernelGGL((k_slow_wave<3, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<3, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<3, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
         break;
     case 4:
-        if (cmp) hipLaunchKernelGGL((k_slow_wave<4, true>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
-        else hipLaunchKernelGGL((k_slow_wave<4, false>), grid, blk, 0, st, p, cp, ovf3, ovf4, early ? 1u : 0u);
+        if (cmp) hipLaunchKernelGGL((k_slow_wave<4, true>), grid, blk, 0, st, p, cp, ovf3, ovf4);
+        else hipLaunchKernelGGL((k_slow_wave<4, false>), grid, blk, 0, st, p, cp, ovf3, ovf4);
         break;
     default: return -4;
     }

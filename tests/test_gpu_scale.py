@@ -113,12 +113,7 @@ def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-@pytest.mark.parametrize("slow", ["late", "early"])
-def test_cfg5_multi_k_200k_transcripts(tx200k, slow, monkeypatch):
-    """early: the first pass's slow reads on the side stream while the other passes run
-    (SKQ_EARLY_SLOW, opt-in; forced here at any batch size), late: all of them after the last
-    pass (the default)."""
-    monkeypatch.setenv("SKQ_EARLY_SLOW", "2" if slow == "early" else "0")
+def test_cfg5_multi_k_200k_transcripts(tx200k):
     cpu, _, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501)
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert sl[0] > 100  # the k = 21 pass's capacity sends reads to the slow path
