@@ -126,13 +126,15 @@ def test_sharded_rounds_equal_one_device():
     np.testing.assert_allclose(pi.cpu().numpy(), pi_ref, rtol=RTOL, atol=0)
 
 
-def test_from_session_results():
-    """Candidates appended straight from the session (device to device), two batches, then the
+@pytest.mark.parametrize("kset", [[31], [21, 25, 31]], ids=["k31", "k21_25_31"])
+def test_from_session_results(kset):
+    """Candidates appended straight from the session (device to device, the packed candidate
+    layout of the fused map at one k slot and with the multi-k passes), two batches, then the
     reference's read filter applied with select."""
     tx = synth.transcriptome(400, seed=9)
     seqs = [tx.seq(i) for i in range(tx.ntx)]
     buf, offs = skq.pack_reads(seqs)
-    index = skq.Index([31], tx.ntx, skq.build_tables(buf, offs, [31]))
+    index = skq.Index(kset, tx.ntx, skq.build_tables(buf, offs, kset))
     bases, _, _ = synth.reads(tx, 6000, 150, seed=10, err=0.002)
     reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(6000)]
     reads[17] = reads[17][:20]                      # short: dropped by the reference
