@@ -1308,6 +1308,9 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     record_stop(s, 0, t0, st);
     if (int rc = chain_tail(s, &sp, cp, accumulate, st)) return rc;
     s->have_chain = true;
+    // the fused kernels filled no probe offsets (lofs): a later skq_chain on these sketches
+    // probes them itself (k_probe, then the count kernel over the packed sets)
+    s->probed = false;
     return 0;
 }
 

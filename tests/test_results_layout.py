@@ -141,3 +141,29 @@ def test_results_layout_matches_export(ks, split):
     d_buf.free()
     d_offs.free()
     index.free()
+
+
+@pytest.mark.parametrize("ks", [[31], [21, 31]], ids=["k31", "k21_31"])
+def test_chain_after_map(ks):
+    """skq_chain on a fused map's (packed) sketches, at another fraction, equals a map at that
+    fraction (which the parity suite pins to the oracle)."""
+    seqs, reads = batch()
+    buf, offs = skq.pack_reads(seqs)
+    index = skq.Index(ks, len(seqs), skq.build_tables(buf, offs, ks))
+    rb, ro = skq.pack_reads(reads)
+    n = len(reads)
+    d_buf = skq.DeviceBuffer.from_numpy(rb)
+    d_offs = skq.DeviceBuffer.from_numpy(ro)
+    s = skq.Session(index, n, 512)
+    s.map(d_buf.ptr, d_offs.ptr, n, 512, fraction=0.9, accumulate=False)
+    s.chain(fraction=0.5, accumulate=False)
+    s.check()
+    a = s.export()
+    t = skq.Session(index, n, 512)
+    t.map(d_buf.ptr, d_offs.ptr, n, 512, fraction=0.5, accumulate=False)
+    t.check()
+    b = t.export()
+    for key in ("status", "hash_offs", "hashes", "cand_offs", "cand_tid", "cand_score"):
+        np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+    for x in (s, t, d_buf, d_offs, index):
+        x.free()
