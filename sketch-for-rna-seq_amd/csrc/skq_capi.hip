@@ -135,6 +135,8 @@ struct skq_session {
     uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
     uint32_t* ktab = nullptr;    // multi-k map by passes: per-k count tables (allocated on first use)
     uint8_t* kcnt = nullptr;
+    uint32_t* stash = nullptr;   // multi-k map by passes: the first pass's staged bases (SketchParams::stash)
+    uint64_t stash_words = 0;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     uint32_t* ctrl = nullptr;
@@ -189,6 +191,16 @@ uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold, double s
 
 // the multi-k passes' raw capacity: the mean retained windows of the pass's k plus this many
 // standard deviations (reads beyond it take k_slow_wave); SKQ_PASS_SIGMAS overrides (A/B)
+// the multi-k passes stage from the first pass's image of the bases; SKQ_STASH=0 re-reads the
+// bases in every pass (A/B)
+static bool use_stash() {
+    static const bool v = [] {
+        const char* e = std::getenv("SKQ_STASH");
+        return !e || std::atoi(e) != 0;
+    }();
+    return v;
+}
+
 double pass_sigmas() {
     static const double v = [] {
         const char* e = std::getenv("SKQ_PASS_SIGMAS");
@@ -990,6 +1002,7 @@ int skq_session_free(skq_session* s) {
     dev_free(s->tx_acc);
     dev_free(s->ktab);
     dev_free(s->kcnt);
+    dev_free(s->stash);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
     dev_free(s->ctrl);
@@ -1272,6 +1285,18 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         }
     }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
+    if (s->idx->nk > 1 && use_stash()) {  // the first pass's image of the bases, for the later passes
+        const uint64_t words = ((n_reads + 63) / 64) * (uint64_t)skq::stash_stride(sp.tile_chunks);
+        if (words > s->stash_words) {
+            DeviceGuard g(s->idx->device);
+            dev_free(s->stash);
+            s->stash_words = 0;
+            if (int rc = dev_alloc(&s->stash, words)) return rc;
+            s->stash_words = words;
+        }
+        sp.stash = s->stash;
+        sp.stash_stride = skq::stash_stride(sp.tile_chunks);
+    }
     // the hashes (and the multi-k passes' per-k tables) in the per-wave packed layout (whole
     // lines written; skq.h)
     s->hash_packed = true;

@@ -111,6 +111,12 @@ struct SketchParams {
     // (r & ~63) * hcap, except runs in hash_ext, marked hash_cnt = HASH_EXT | offset ([count,
     // region share, hashes...]); the multi-k passes' per-k tables (ktab) likewise, TS per read
     uint32_t hpack;
+    // multi-k passes: the first pass stores each wave's staged bases (2-bit codes, then the
+    // per-chunk bad bits as u64 from word (tile_chunks + 1) & ~1) at stash + wave * stash_stride,
+    // and the later passes stage from there instead of re-reading the bases (null: every pass
+    // reads the bases)
+    uint32_t* stash;
+    uint32_t stash_stride;  // words per wave, a multiple of 16 (whole 64-B lines)
     // fused index probe (direct tables, DESIGN.md "Index"): when fuse is set, each retained hash
     // h of k slot i is looked up as dir[i][h] (h < dir_len[i], else a miss) and the list offset
     // lands in lofs[(i*hcap + j)*n + r]; pflag[r] = 1 marks reads the count kernel must hand to
@@ -279,6 +285,10 @@ SKQ_HD inline uint32_t cmp_slot(uint32_t kh, uint32_t pilot, uint64_t nslots) {
 }
 constexpr uint32_t CMP_LONG = 8;  // F of an entry whose list continues at lists[offset]
 size_t sketch_lds_bytes(uint32_t nk, uint32_t tile_chunks, uint32_t hcap, bool nthash);
+// SketchParams::stash: words per wave (codes, then 2 words of bad bits per 64 chunks), whole lines
+SKQ_HD inline uint32_t stash_stride(uint32_t tile_chunks) {
+    return (((tile_chunks + 1) & ~1u) + 2 * ((tile_chunks + 63) / 64) + 15) & ~15u;
+}
 
 // 33-bit ntHash lane (bits 0..32 of ntHash's split rotate evolve on their own)
 constexpr uint64_t M33 = (1ull << 33) - 1;

@@ -2055,7 +2055,23 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         nch = (uint32_t)min((uint64_t)wc, c1 - c0);
         const uint4* src = reinterpret_cast<const uint4*>(p.reads - delta) + c0;
         constexpr uint32_t SU = 10;
-        for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
+        // multi-k passes (SketchParams::stash): the first stores the wave's staged image, the
+        // later ones stage from it (38 B per 150-bp read instead of the 150 B of bases)
+        uint32_t* sw = PASS && p.stash ? p.stash + (r0 >> 6) * p.stash_stride : nullptr;
+        const uint32_t sbad = (wc + 1) & ~1u;  // (the bad bits' first word)
+        if (PASS && sw && ks > 0) {
+            for (uint32_t cb = lane; cb < nch; cb += SU * 64) {
+                uint32_t x[SU];
+#pragma unroll
+                for (uint32_t u = 0; u < SU; ++u) x[u] = __builtin_nontemporal_load(sw + min(cb + u * 64, nch - 1));
+#pragma unroll
+                for (uint32_t u = 0; u < SU; ++u)
+                    if (cb + u * 64 < nch) s_codes[cb + u * 64] = x[u];
+            }
+            if (lane < (nch + 63) / 64)
+                s_badw[lane] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sw + sbad) + lane);
+        }
+        for (uint32_t cb = lane; cb < nch && !(PASS && sw && ks > 0); cb += SU * 64) {
             uint4 vv[SU];
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u) {
@@ -2082,6 +2098,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 s_codes[cs] = code;
                 const uint64_t wbits = __ballot(x != 0);
                 if (lane == 0 && c < nch) s_badw[c >> 6] = wbits;
+                if (PASS && sw && c < nch) {  // (first pass: the image for the later ones)
+                    __builtin_nontemporal_store(code, sw + c);
+                    if (lane == 0) __builtin_nontemporal_store(wbits, reinterpret_cast<uint64_t*>(sw + sbad) + (c >> 6));
+                }
             }
         }
         if (lane == 0) s_codes[nch] = 0;
