@@ -2,7 +2,7 @@
 // (src/main.cpp:113-148) with the text itself parsed in HBM.
 //
 // Host side: a reader thread fills pinned staging buffers straight from the file (parallel
-// pread) and copies each chunk to the device on its own stream, two chunks ahead, so file I/O and
+// pread by a pool of workers; the buffers are cached across ingests) and copies each chunk to the device on its own stream, two chunks ahead, so file I/O and
 // PCIe overlap the GPU work and the caller's result handling. The host never touches the bytes.
 //
 // Device side, per chunk (a run of whole lines, plus the line that follows as a halo so the
@@ -32,6 +32,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <hipcub/hipcub.hpp>
@@ -315,6 +318,109 @@ struct Slot {
     uint64_t file_off = 0, own = 0, len = 0;
 };
 
+// The reader's pread workers, started once per ingest (a chunk's preads used to start and join
+// io_threads threads of their own: ~1,200 thread starts per 3.2-GB file). run() splits [off,
+// off + n) into one part per worker and returns when every part is in.
+struct PreadPool {
+    std::vector<std::thread> ws;
+    std::mutex mu;
+    std::condition_variable go, done;
+    int fd = -1;
+    uint8_t* dst = nullptr;
+    uint64_t off = 0, n = 0;
+    uint64_t gen = 0;
+    int left = 0;
+    bool fail = false, stop = false;
+
+    void start(int nthreads, int file) {
+        fd = file;
+        for (int t = 0; t < nthreads; ++t) ws.emplace_back([this, t, nthreads] { work(t, nthreads); });
+    }
+    void work(int t, int T) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint8_t* d;
+            uint64_t a, b, o;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                go.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+                const uint64_t step = (n + T - 1) / T;
+                d = dst;
+                o = off;
+                a = off + std::min<uint64_t>(n, step * t);
+                b = off + std::min<uint64_t>(n, step * (t + 1));
+            }
+            bool ok = true;
+            while (a < b) {
+                const ssize_t got = ::pread(fd, d + (a - o), (size_t)std::min<uint64_t>(b - a, 1ull << 30), (off_t)a);
+                if (got <= 0) {
+                    ok = false;
+                    break;
+                }
+                a += (uint64_t)got;
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            fail |= !ok;
+            if (--left == 0) done.notify_all();
+        }
+    }
+    int run(uint8_t* d, uint64_t o, uint64_t len) {
+        std::unique_lock<std::mutex> lk(mu);
+        dst = d;
+        off = o;
+        n = len;
+        fail = false;
+        left = (int)ws.size();
+        ++gen;
+        go.notify_all();
+        done.wait(lk, [&] { return left == 0; });
+        return fail ? -1 : 0;
+    }
+    void shut() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto& w : ws) w.join();
+        ws.clear();
+    }
+};
+
+// Pinned staging buffers outlive their ingest (hipHostFree of three 32-MiB slots cost ~13 ms of
+// every file's close): a closed ingest returns them here and the next one on the process takes
+// them back, as a caching host allocator does.
+std::mutex g_pin_mu;
+struct Pin {
+    uint8_t* p;
+    uint64_t cap;
+    int device;  // (the device current when it was allocated)
+};
+std::vector<Pin> g_pins;
+
+uint8_t* pin_take(uint64_t need, uint64_t& cap, int device) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (size_t i = 0; i < g_pins.size(); ++i)
+        if (g_pins[i].cap >= need && g_pins[i].device == device) {
+            uint8_t* p = g_pins[i].p;
+            cap = g_pins[i].cap;
+            g_pins.erase(g_pins.begin() + (long)i);
+            return p;
+        }
+    return nullptr;
+}
+
+void pin_give(uint8_t* p, uint64_t cap, int device) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (g_pins.size() < 16) {
+        g_pins.push_back({p, cap, device});
+        return;
+    }
+    (void)hipHostFree(p);
+}
+
 }  // namespace
 
 struct skq_ingest {
@@ -327,6 +433,7 @@ struct skq_ingest {
     const char* map = nullptr;   // the file, mapped for duplicate-id comparisons
     uint64_t chunk = 0;
     int io_threads = 1;
+    PreadPool pool;
     hipStream_t copy = nullptr;
     // reader thread
     std::thread th;
@@ -353,41 +460,18 @@ struct skq_ingest {
     DevArray<uint32_t> id_len;
     DevArray<uint8_t> status;
     bool finished = false;
+    // SKQ_INGEST_TRACE=1: where the time goes, printed to stderr on close (seconds): the reader's
+    // preads and its waits for a free slot, the consumer's waits for a ready chunk, its parse
+    // (with the two host syncs) and its map launches
+    bool trace = false;
+    double t_read = 0, t_slot = 0, t_ready = 0, t_parse = 0, t_map = 0;
+    uint64_t n_chunks = 0;
 };
 
 namespace {
 
-int pread_all(int fd, uint8_t* dst, uint64_t off, uint64_t n, int nthreads, std::string& err) {
-    auto part = [&](uint64_t a, uint64_t b, int* rc) {
-        while (a < b) {
-            const ssize_t got = ::pread(fd, dst + (a - off), (size_t)std::min<uint64_t>(b - a, 1ull << 30), (off_t)a);
-            if (got <= 0) {
-                *rc = -1;
-                return;
-            }
-            a += (uint64_t)got;
-        }
-        *rc = 0;
-    };
-    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)nthreads, n >> 22));
-    std::vector<int> rcs(T, 0);
-    if (T == 1) {
-        part(off, off + n, &rcs[0]);
-    } else {
-        std::vector<std::thread> ts;
-        const uint64_t step = (n + T - 1) / T;
-        for (int t = 0; t < T; ++t) {
-            const uint64_t a = off + std::min<uint64_t>(n, step * t), b = off + std::min<uint64_t>(n, step * (t + 1));
-            ts.emplace_back(part, a, b, &rcs[t]);
-        }
-        for (auto& t : ts) t.join();
-    }
-    for (int rc : rcs)
-        if (rc) {
-            err = "FASTQ read failed";
-            return -2;
-        }
-    return 0;
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // first '\n' in h[from, to) or `to`
@@ -404,6 +488,7 @@ void reader_main(skq_ingest* g) {
     std::string err;
     for (uint64_t c = 0; off < g->hi; ++c) {
         Slot& sl = g->slot[c % NSLOT];
+        const double tw = g->trace ? now_s() : 0.0;
         {
             std::unique_lock<std::mutex> lk(g->mu);
             g->cv.wait(lk, [&] { return g->stop || sl.state == 0; });
@@ -417,25 +502,30 @@ void reader_main(skq_ingest* g) {
             (void)hipEventSynchronize(sl.h2d);
             sl.h2d_pending = false;
         }
+        const double tr = g->trace ? now_s() : 0.0;
+        if (g->trace) g->t_slot += tr - tw;
         // read until the own region ends at a newline (or EOF) and the halo line is complete
         const uint64_t lim = g->hi - off;  // bytes of the range left (hi is a line start or EOF)
         uint64_t have = 0, want = std::min<uint64_t>(g->fsize - off, std::min(lim, g->chunk) + (1u << 16));
         uint64_t own = 0, len = 0;
         for (;;) {
             if (want > sl.host_cap) {
-                uint8_t* h = nullptr;
-                const uint64_t cap = std::max<uint64_t>(want, sl.host_cap * 2);
-                if (hipHostMalloc(reinterpret_cast<void**>(&h), cap, hipHostMallocDefault) != hipSuccess) {
+                uint64_t cap = std::max<uint64_t>(want, sl.host_cap * 2);
+                uint8_t* h = pin_take(cap, cap, g->device);
+                if (!h && hipHostMalloc(reinterpret_cast<void**>(&h), cap, hipHostMallocDefault) != hipSuccess) {
                     err = "pinned staging allocation failed";
                     break;
                 }
                 if (have) std::memcpy(h, sl.host, have);
-                if (sl.host) (void)hipHostFree(sl.host);
+                if (sl.host) pin_give(sl.host, sl.host_cap, g->device);
                 sl.host = h;
                 sl.host_cap = cap;
             }
             if (want > have) {
-                if (pread_all(g->fd, sl.host + have, off + have, want - have, g->io_threads, err)) break;
+                if (g->pool.run(sl.host + have, off + have, want - have)) {
+                    err = "FASTQ read failed";
+                    break;
+                }
                 have = want;
             }
             const bool at_eof = off + have == g->fsize;
@@ -470,6 +560,10 @@ void reader_main(skq_ingest* g) {
             want = std::min<uint64_t>(g->fsize - off, have * 2);
         }
         if (!err.empty()) break;
+        if (g->trace) {
+            g->t_read += now_s() - tr;
+            ++g->n_chunks;
+        }
         if (len + PAD > sl.dev_cap) {
             if (sl.dev) (void)hipFree(sl.dev);
             sl.dev = nullptr;
@@ -601,6 +695,7 @@ int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_
     g->max_reads = skq::session_max_reads(s);
     g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (32ull << 20), 1u << 12);  // (32 MiB, 12 preads: profiles/r3_ingest_sweep.log)
     g->io_threads = io_threads > 0 ? io_threads : 12;  // 4 preads: 37 M reads/s end to end, 8: 53 M (profiles/r2_ingest_threads.log); 12 with 32-MiB chunks: 75 M (profiles/r3_ingest_sweep.log)
+    if (const char* e = std::getenv("SKQ_INGEST_TRACE")) g->trace = std::atoi(e) != 0;
     g->fd = ::open(path, O_RDONLY);
     if (g->fd < 0) {
         delete g;
@@ -645,6 +740,7 @@ int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_
         skq_ingest_close(g);
         return rc;
     }
+    g->pool.start(g->io_threads, g->fd);
     g->th = std::thread(reader_main, g);
     *out = g;
     return 0;
@@ -673,6 +769,7 @@ int skq_ingest_map(skq_ingest* g, uint32_t threshold, double fraction, int accum
             g->cur = -1;
         }
         const int c = (int)(g->consumed_chunks % NSLOT);
+        const double tw = g->trace ? now_s() : 0.0;
         {
             std::unique_lock<std::mutex> lk(g->mu);
             g->cv.wait(lk, [&] { return g->slot[c].state == 1 || (g->eof && g->produced == g->consumed_chunks); });
@@ -684,11 +781,15 @@ int skq_ingest_map(skq_ingest* g, uint32_t threshold, double fraction, int accum
             g->slot[c].state = 2;
         }
         g->cur = c;
+        const double tp = g->trace ? now_s() : 0.0;
+        if (g->trace) g->t_ready += tp - tw;
         if ((rc = parse_chunk(g, c, st))) {
             (void)hipSetDevice(prev);
             return rc;
         }
+        if (g->trace) g->t_parse += now_s() - tp;
     }
+    const double tm = g->trace ? now_s() : 0.0;
     const uint64_t m = std::min<uint64_t>(g->cur_n - g->cur_done, g->max_reads);
     const uint64_t* offs = g->offs.p + g->cur_done;
     rc = skq_map(g->s, g->batch.p, offs, 0, m, std::max<uint32_t>(g->cur_maxlen, 1), threshold, fraction, accumulate,
@@ -706,6 +807,7 @@ int skq_ingest_map(skq_ingest* g, uint32_t threshold, double fraction, int accum
         g->records += m;
         g->cur_done += m;
     }
+    if (g->trace) g->t_map += now_s() - tm;
     (void)hipSetDevice(prev);
     return rc;
 }
@@ -841,6 +943,7 @@ int skq_ingest_supersede(skq_ingest* const* gs, uint32_t nparts, uint8_t* const*
 
 int skq_ingest_close(skq_ingest* g) {
     if (!g) return 0;
+    const double tc = g->trace ? now_s() : 0.0;
     if (g->th.joinable()) {
         {
             std::lock_guard<std::mutex> lk(g->mu);
@@ -849,12 +952,13 @@ int skq_ingest_close(skq_ingest* g) {
         g->cv.notify_all();
         g->th.join();
     }
+    g->pool.shut();
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
     (void)hipDeviceSynchronize();
     for (auto& sl : g->slot) {
-        if (sl.host) (void)hipHostFree(sl.host);
+        if (sl.host) pin_give(sl.host, sl.host_cap, g->device);
         if (sl.dev) (void)hipFree(sl.dev);
         if (sl.h2d) (void)hipEventDestroy(sl.h2d);
         if (sl.consumed) (void)hipEventDestroy(sl.consumed);
@@ -863,6 +967,12 @@ int skq_ingest_close(skq_ingest* g) {
     if (g->copy) (void)hipStreamDestroy(g->copy);
     if (g->map) munmap(const_cast<char*>(g->map), g->fsize);
     if (g->fd >= 0) ::close(g->fd);
+    if (g->trace)
+        std::fprintf(stderr,
+                     "[skq ingest] %llu chunks: reader pread %.4f s, waits for a slot %.4f s; consumer waits %.4f s, "
+                     "parse %.4f s, map %.4f s; close %.4f s\n",
+                     (unsigned long long)g->n_chunks, g->t_read, g->t_slot, g->t_ready, g->t_parse, g->t_map,
+                     now_s() - tc);
     delete g;  // DevArrays free themselves on this device
     (void)hipSetDevice(prev);
     return 0;

@@ -67,8 +67,10 @@ def main():
     print("[ingest] setup %.1fs, %.2f GB FASTQ" % (time.time() - t0, size / 1e9), file=sys.stderr, flush=True)
 
     def run():
+        t_a = time.perf_counter()
         g = skq.Ingest(sess, args.path, chunk_bytes=args.chunk << 20, io_threads=args.io_threads)
         em = skq.EMSet(tx.ntx) if args.em else None
+        timing["open_s"] = time.perf_counter() - t_a
         tot = 0
         ncand = 0
         while True:
@@ -81,8 +83,11 @@ def main():
             if em is not None:
                 em.add_session(sess)
         sess.check()
+        t_b = time.perf_counter()
+        timing["loop_s"] = t_b - t_a - timing["open_s"]
         kept = g.finish()
         g.close()
+        timing["finish_close_s"] = time.perf_counter() - t_b
         if em is not None:
             t1 = time.perf_counter()
             em.select(kept)
