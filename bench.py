@@ -42,8 +42,8 @@ def _args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: min(16, affinity CPUs): the box's CPU share per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the 1-thread CPU timing")
-    ap.add_argument("--io-threads", type=int, default=12, help="end to end: FASTQ pread threads per GPU")
-    ap.add_argument("--chunk-mb", type=int, default=32, help="end to end: FASTQ chunk (MiB)")
+    ap.add_argument("--io-threads", type=int, default=16, help="end to end: FASTQ pread threads per GPU")
+    ap.add_argument("--chunk-mb", type=int, default=64, help="end to end: FASTQ chunk (MiB)")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the FASTQ-file -> EM leg reported beside the kernel path")
     ap.add_argument("--dist-backend", default="nccl",

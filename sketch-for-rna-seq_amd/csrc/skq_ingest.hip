@@ -303,8 +303,9 @@ struct DevArray {
 };
 
 // chunk slots: the reader fills one while the device copies another and the consumer parses and
-// maps a third (pread, H2D and the map overlap; two slots serialised the pread with the copy)
-constexpr int NSLOT = 3;
+// maps a third (pread, H2D and the map overlap; two slots serialised the pread with the copy; a
+// fourth absorbs the consumer's uneven chunks)
+constexpr int NSLOT = 4;
 
 struct Slot {
     uint8_t* host = nullptr;   // pinned
@@ -693,8 +694,10 @@ int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_
     g->s = s;
     g->device = skq::session_device(s);
     g->max_reads = skq::session_max_reads(s);
-    g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (32ull << 20), 1u << 12);  // (32 MiB, 12 preads: profiles/r3_ingest_sweep.log)
-    g->io_threads = io_threads > 0 ? io_threads : 12;  // 4 preads: 37 M reads/s end to end, 8: 53 M (profiles/r2_ingest_threads.log); 12 with 32-MiB chunks: 75 M (profiles/r3_ingest_sweep.log)
+    // (64 MiB, 16 pread workers, four slots: profiles/r3_ingest_pool.log; before the worker pool
+    // 12 x 32 MiB was best, profiles/r3_ingest_sweep.log)
+    g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (64ull << 20), 1u << 12);
+    g->io_threads = io_threads > 0 ? io_threads : 16;
     if (const char* e = std::getenv("SKQ_INGEST_TRACE")) g->trace = std::atoi(e) != 0;
     g->fd = ::open(path, O_RDONLY);
     if (g->fd < 0) {
