@@ -191,7 +191,7 @@ int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, i
 
 /* ---- FASTQ ingest on the GPU (process_fastq_single_pass's reader, src/main.cpp:113-148) ------
  * The FASTQ text itself goes to the device: a reader thread pulls the file into pinned staging
- * buffers (io_threads parallel preads, <= 0 = 16) and copies chunks of about chunk_bytes (0 = 64 MiB) to HBM
+ * buffers (io_threads parallel preads, <= 0 = 16, at most 64) and copies chunks of about chunk_bytes (0 = 64 MiB) to HBM
  * on its own stream, up to three chunks ahead; the GPU splits them into records with the reader's rules
  * (a line starting with '@' opens a record whose id is the rest of that line; the next three
  * lines are sequence, '+' and quality, whatever they hold; other lines between records are

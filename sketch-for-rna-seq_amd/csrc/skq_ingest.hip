@@ -697,7 +697,7 @@ int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_
     // (64 MiB, 16 pread workers, four slots: profiles/r3_ingest_pool.log; before the worker pool
     // 12 x 32 MiB was best, profiles/r3_ingest_sweep.log)
     g->chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (64ull << 20), 1u << 12);
-    g->io_threads = io_threads > 0 ? io_threads : 16;
+    g->io_threads = io_threads > 0 ? std::min(io_threads, 64) : 16;  // (workers started per ingest)
     if (const char* e = std::getenv("SKQ_INGEST_TRACE")) g->trace = std::atoi(e) != 0;
     g->fd = ::open(path, O_RDONLY);
     if (g->fd < 0) {
