@@ -83,7 +83,8 @@ int skq_index_direct(const skq_index* ix);
  * follow it along the transcripts (nearest first, whole lists). skq_map then settles a read's
  * retained hashes with one entry request plus one per hash the entry does not hold (2.6 instead
  * of 6 at cfg3); results are identical (a record is used only for its exact key).
- * Built only with SKQ_CHAIN=1 in the environment (measured 2 % faster at cfg3, for 27.5 GB);
+ * Built only with SKQ_CHAIN=1 in the environment (27.5 GB at cfg3; 11 % slower than the wide
+ * tables after round 3's write-request changes);
  * otherwise, and for other indexes: as skq_index_create. */
 int skq_index_create_chained(int device, uint32_t ntx, uint32_t nk, const uint32_t* ks, uint32_t ntables,
                              const skq_kmer_table* tables, const uint8_t* seqs, const uint64_t* seq_offs,
@@ -92,7 +93,9 @@ int skq_index_create_chained(int device, uint32_t ntx, uint32_t nk, const uint32
 double skq_index_chained(const skq_index* ix);
 
 /* A session owns the device workspace for batches of up to max_reads reads of at most
- * max_len bases each (longer reads are still handled exactly, by the slow path). */
+ * max_len bases each (longer reads are still handled exactly, by the slow path). Indexes of
+ * 2-4 k add, on the first skq_map, the passes' per-k tables (nk * 64 + 2 * nk B per read) and
+ * the first pass's image of the bases (about a quarter of the bases' bytes). */
 int skq_session_create(skq_index* idx, uint64_t max_reads, uint32_t max_len, skq_session** out);
 /* (max_reads < 2^24: per-batch transcript totals are packed into 24-bit read counts) */
 int skq_session_free(skq_session* s);

@@ -192,13 +192,10 @@ uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold, double s
 // the multi-k passes' raw capacity: the mean retained windows of the pass's k plus this many
 // standard deviations (reads beyond it take k_slow_wave); SKQ_PASS_SIGMAS overrides (A/B)
 // the multi-k passes stage from the first pass's image of the bases; SKQ_STASH=0 re-reads the
-// bases in every pass (A/B)
+// bases in every pass (A/B; read per batch, so the parity tests run both)
 static bool use_stash() {
-    static const bool v = [] {
-        const char* e = std::getenv("SKQ_STASH");
-        return !e || std::atoi(e) != 0;
-    }();
-    return v;
+    const char* e = std::getenv("SKQ_STASH");
+    return !e || std::atoi(e) != 0;
 }
 
 double pass_sigmas() {

@@ -3,6 +3,7 @@
 Every comparison is exact: retained-hash sets per (read, k), per-read status, and candidate
 lists (tid, score) in the normalised order (score desc, tid asc).
 """
+import ctypes as C
 import random
 import sys
 
@@ -524,3 +525,42 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     tr, ts = totals_from(ref, len(reads), tx300.ntx)
     np.testing.assert_array_equal(out["totals"][0], tr)
     np.testing.assert_array_equal(out["totals"][1], ts)
+
+
+@pytest.mark.parametrize("stash", ["1", "0"])
+def test_multi_k_passes_base_image(tx300, probe_mode, monkeypatch, stash):
+    """The k_map1 passes: the first stores each wave's staged bases (2-bit codes + bad bits) and
+    the later passes stage from that image (SKQ_STASH=1, the default) or re-read the bases
+    (SKQ_STASH=0). Variable lengths, an unaligned buffer, bad bytes, short and > 256-bp reads and
+    several batches through one session (the image grows with the batch): bit-exact both ways."""
+    monkeypatch.setenv("SKQ_STASH", stash)
+    ks = [21, 25, 31]
+    gi, oi = build(ks, tx=tx300)
+    rng = random.Random(11)
+    reads = []
+    for i in range(2500):
+        s = tx300.seq(rng.randrange(tx300.ntx))
+        L = rng.choice([0, 20, 31, 90, 150, 150, 150, 199, 256, 300]) if i % 3 else rng.randint(0, 260)
+        L = min(L, len(s))
+        p = rng.randint(0, len(s) - L)
+        r = bytearray(s[p:p + L])
+        if L and i % 97 == 0:
+            r[rng.randrange(L)] = ord("N")
+        reads.append(bytes(r))
+    ref = oi.map_batch(reads)
+    s = skq.Session(gi, 1500, 300)
+    for lo, hi in ((1500, 2500), (0, 1500), (0, 1000)):  # (the image grows, then a smaller batch)
+        buf, offs = skq.pack_reads(reads[lo:hi])
+        pad = np.concatenate([np.zeros(5, np.uint8), buf])  # reads start 5 bytes into the buffer
+        d_buf = skq.DeviceBuffer.from_numpy(pad)
+        d_offs = skq.DeviceBuffer.from_numpy(offs)
+        at = C.c_void_p(d_buf.value + 5)
+        if SPLIT:
+            s.sketch(at, d_offs.ptr, hi - lo, 300)
+            s.chain()
+        else:
+            s.map(at, d_offs.ptr, hi - lo, 300)
+        s.check()
+        out = s.export()
+        sub = {key: v[lo:hi] for key, v in ref.items()}
+        compare(out, sub, hi - lo, len(ks))
