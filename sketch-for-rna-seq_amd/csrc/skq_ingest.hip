@@ -436,6 +436,7 @@ struct skq_ingest {
     int io_threads = 1;
     PreadPool pool;
     hipStream_t copy = nullptr;
+    hipStream_t pst = nullptr;  // the parse's first phase (record count), beside the caller's map
     // reader thread
     std::thread th;
     std::mutex mu;
@@ -612,6 +613,11 @@ int cub_call(skq_ingest* g, F&& f) {
 // parse the chunk in slot c into the flat batch; sets cur_n / cur_maxlen
 int parse_chunk(skq_ingest* g, int c, hipStream_t st) {
     Slot& sl = g->slot[c];
+    // first phase (line starts, record machine, record count) on the parse stream: it touches only
+    // the parse's own arrays, so it runs beside the previous chunk's map on the caller's stream and
+    // its host sync does not wait for that map
+    hipStream_t ps = g->pst;
+    IHIP(hipStreamWaitEvent(ps, sl.h2d, 0));
     IHIP(hipStreamWaitEvent(st, sl.h2d, 0));
     const uint64_t nseg = (sl.own + SEG - 1) / SEG;
     if (sl.len >= (1ull << 32) - PAD) return ifail(-1, "FASTQ line too long for one chunk");
@@ -622,21 +628,21 @@ int parse_chunk(skq_ingest* g, int c, hipStream_t st) {
     const uint8_t* text = sl.dev;
     const uint32_t* s_in = g->state.p + (g->consumed_chunks & 1);
     uint32_t* s_out = g->state.p + ((g->consumed_chunks + 1) & 1);
-    k_fq_func<<<blocks(nseg, 256), 256, 0, st>>>(text, sl.own, nseg, g->func.p);
+    k_fq_func<<<blocks(nseg, 256), 256, 0, ps>>>(text, sl.own, nseg, g->func.p);
     IHIP(hipGetLastError());
     if (int rc = cub_call(g, [&](void* t, size_t& b) {
-            return hipcub::DeviceScan::ExclusiveScan(t, b, g->func.p, g->prefix.p, Then(), (uint8_t)F_ID, (int)nseg, st);
+            return hipcub::DeviceScan::ExclusiveScan(t, b, g->func.p, g->prefix.p, Then(), (uint8_t)F_ID, (int)nseg, ps);
         }))
         return rc;
-    IHIP(hipMemsetAsync(g->cnt.p + nseg, 0, 4, st));
-    k_fq_count<<<blocks(nseg, 256), 256, 0, st>>>(text, sl.own, nseg, g->prefix.p, s_in, s_out, g->cnt.p);
+    IHIP(hipMemsetAsync(g->cnt.p + nseg, 0, 4, ps));
+    k_fq_count<<<blocks(nseg, 256), 256, 0, ps>>>(text, sl.own, nseg, g->prefix.p, s_in, s_out, g->cnt.p);
     IHIP(hipGetLastError());
     if (int rc = cub_call(g, [&](void* t, size_t& b) {
-            return hipcub::DeviceScan::ExclusiveSum(t, b, g->cnt.p, g->slotoff.p, (int)(nseg + 1), st);
+            return hipcub::DeviceScan::ExclusiveSum(t, b, g->cnt.p, g->slotoff.p, (int)(nseg + 1), ps);
         }))
         return rc;
-    IHIP(hipMemcpyAsync(g->h_scal, g->slotoff.p + nseg, 4, hipMemcpyDeviceToHost, st));
-    IHIP(hipStreamSynchronize(st));
+    IHIP(hipMemcpyAsync(g->h_scal, g->slotoff.p + nseg, 4, hipMemcpyDeviceToHost, ps));
+    IHIP(hipStreamSynchronize(ps));  // (the second phase, on the caller's stream, follows it)
     const uint32_t n = g->h_scal[0];
     g->cur_n = n;
     g->cur_done = 0;
@@ -729,6 +735,7 @@ int skq_ingest_open_range(skq_session* s, const char* path, uint64_t lo, uint64_
     (void)hipSetDevice(g->device);
     int rc = 0;
     if (hipStreamCreateWithFlags(&g->copy, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&g->pst, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->h_scal), 16, hipHostMallocDefault) != hipSuccess ||
         g->state.reserve(2) != hipSuccess || g->scal.reserve(2) != hipSuccess ||
         hipMemset(g->state.p, 0, 8) != hipSuccess ||
@@ -968,6 +975,7 @@ int skq_ingest_close(skq_ingest* g) {
     }
     if (g->h_scal) (void)hipHostFree(g->h_scal);
     if (g->copy) (void)hipStreamDestroy(g->copy);
+    if (g->pst) (void)hipStreamDestroy(g->pst);
     if (g->map) munmap(const_cast<char*>(g->map), g->fsize);
     if (g->fd >= 0) ::close(g->fd);
     if (g->trace)
