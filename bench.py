@@ -18,7 +18,8 @@ sharded (each rank its own seeded batch), the index is replicated; rank 0 prints
 After the timed steps (rank 0): the parity sample — the first --cpu-reads reads of the batch as
 FASTQ text through the CPU oracle (oracle/oracle.c, the checker), compared bit-exact with the GPU's
 statuses, retained-hash sets, candidate lists and per-transcript totals for the same reads; a
-mismatch exits non-zero. At N = 1 the same oracle runs are the CPU baseline (P threads and 1),
+mismatch exits non-zero. At every N the same oracle runs are the CPU baseline (rank 0, its
+per-GPU share of the host cores and 1 thread),
 and `end_to_end` reports quant as the CLI runs it (FASTQ file -> device parse -> sketch + chain ->
 EM + assignment) over the same batch, checked against the in-HBM map's totals; never `value`.
 """
@@ -38,9 +39,10 @@ def _args(argv=None):
                     help="default: cfg3 at N = 1, cfg4 at N > 1")
     ap.add_argument("--reads", type=int, default=0, help="reads per GPU (default: the config's)")
     ap.add_argument("--cpu-reads", type=int, default=2_000_000,
-                    help="parity sample / CPU-baseline sample (reads; N > 1: capped at 200k)")
+                    help="parity sample / CPU-baseline sample (reads, rank 0)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (default: min(16, affinity CPUs): the box's CPU share per GPU)")
+                    help="CPU baseline threads (default: the per-GPU share of the affinity set, affinity CPUs "
+                         "/ GPUs on the node, capped at OMP_NUM_THREADS when the box sets it)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the 1-thread CPU timing")
     ap.add_argument("--io-threads", type=int, default=16, help="end to end: FASTQ pread threads per GPU")
     ap.add_argument("--chunk-mb", type=int, default=64, help="end to end: FASTQ chunk (MiB)")
@@ -285,6 +287,44 @@ def end_to_end(index, ntx, bases, d_ptr, n, L, sess, sp, rank=0, world=1, dev=No
             os.unlink(path)
 
 
+def node_gpus(world):
+    """GPUs on this node: the KFD topology's GPU nodes (every GPU of the machine, visible or not),
+    at least the ranks of this job."""
+    n = 0
+    try:
+        top = "/sys/class/kfd/kfd/topology/nodes"
+        for d in os.listdir(top):
+            try:
+                props = open(os.path.join(top, d, "properties")).read().split("\n")
+            except OSError:
+                continue
+            for ln in props:
+                f = ln.split()
+                if len(f) == 2 and f[0] == "simd_count" and int(f[1]) > 0:
+                    n += 1
+    except OSError:
+        pass
+    return max(n, world, 1)
+
+
+def cpu_share(args, world):
+    """(threads, how they were derived): the per-GPU share of the affinity set, capped at the
+    box's CPU share (OMP_NUM_THREADS, which the GPU pool sets per one-GPU box)."""
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    g = node_gpus(world)
+    share = max(1, ncpu // g)
+    how = "affinity set %d CPUs / %d GPUs on the node = %d" % (ncpu, g, share)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if args.cpu_threads:
+        return args.cpu_threads, ncpu, "--cpu-threads %d (%s)" % (args.cpu_threads, how)
+    if omp and omp < share:
+        return omp, ncpu, how + ", capped at OMP_NUM_THREADS = %d (this box's CPU share)" % omp
+    return share, ncpu, how
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -358,7 +398,7 @@ def main(args):
     slow = sess.slow_counts()
 
     # the sample: the first m reads of this rank's batch, mapped alone (fresh totals), exported
-    m = min(n, args.cpu_reads if world == 1 else min(args.cpu_reads, 200_000))
+    m = min(n, args.cpu_reads)
     sess.reset_totals(sp)
     sess.map(d_reads.data_ptr(), None, m, L, fixed_len=L, stream=sp, accumulate=True)
     sess.check(sp)
@@ -432,13 +472,7 @@ def main(args):
             pairs.append((np.repeat(keys, np.diff(offs.astype(np.int64))), tids))
         oi = orc.Index(ks, pairs=pairs, ntx=tx.ntx)
         fq = synth.fastq_bytes(bases[:m * L], L)
-        try:
-            ncpu = len(os.sched_getaffinity(0))
-        except AttributeError:
-            ncpu = os.cpu_count() or 1
-        # the box's CPU share: 16 threads per GPU (the pool's rule for worker pools); the affinity
-        # set can list the whole machine's CPUs, reported beside it
-        P_thr = args.cpu_threads or max(1, min(16, ncpu))
+        P_thr, ncpu, share_how = cpu_share(args, world)
         tc = time.perf_counter()
         cout = orc.fastq_map(oi, fq, nthreads=P_thr, outputs=True, hcap=64, ccap=64)
         dt_p = time.perf_counter() - tc
@@ -446,26 +480,27 @@ def main(args):
         parity = ("bit-exact, %d reads (status, retained-hash sets, candidate lists, per-transcript totals)" % m
                   if not bad else "MISMATCH: " + "; ".join(bad))
         log("parity sample: %s" % parity)
-        if world == 1:
-            cpu = {"value": m / dt_p, "unit": "reads/s", "cores": P_thr, "kind": "port",
-                   "cpu_model": cpu_model(), "affinity_cpus": ncpu,
-                   "cores_note": "threads = the box's CPU share per GPU (16) unless --cpu-threads; the "
-                                 "reference itself is single-threaded (see single_core)",
-                   "sample": "first %d reads of the same batch as FASTQ text (%d MB in RAM), same index: "
-                             "oracle/oracle.c orc_fastq_map (record machine, is_valid_sequence, sketch, "
-                             "sparse_chain, id map, totals), %d threads over read shards, %.1fs"
-                             % (m, fq.size >> 20, P_thr, dt_p)}
-            if not args.no_cpu_baseline:
-                m1 = min(m, 1_000_000)
-                fq1 = fq[:m1 * (fq.size // m)]
-                tc = time.perf_counter()
-                orc.fastq_map(oi, fq1, nthreads=1, outputs=False, totals=True)
-                dt_1 = time.perf_counter() - tc
-                cpu["single_core"] = {"value": m1 / dt_1, "cores": 1,
-                                      "sample": "first %d reads, 1 thread, %.1fs" % (m1, dt_1)}
-            cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
-            if os.path.exists(cal):  # reference sparse_chain vs the oracle's, timed in the build container
-                cpu["calibration"] = json.load(open(cal)).get("summary")
+        # (every N: rank 0 times the same oracle path on its host-core share while the other ranks
+        # wait at the barrier below)
+        cpu = {"value": m / dt_p, "unit": "reads/s", "cores": P_thr, "kind": "port",
+               "cpu_model": cpu_model(), "affinity_cpus": ncpu, "cores_derivation": share_how,
+               "cores_note": "threads over read shards; the reference itself is single-threaded (see "
+                             "single_core)",
+               "sample": "first %d reads of rank 0's batch as FASTQ text (%d MB in RAM), same index: "
+                         "oracle/oracle.c orc_fastq_map (record machine, is_valid_sequence, sketch, "
+                         "sparse_chain, id map, totals), %d threads over read shards, %.1fs"
+                         % (m, fq.size >> 20, P_thr, dt_p)}
+        if not args.no_cpu_baseline:
+            m1 = min(m, 1_000_000)
+            fq1 = fq[:m1 * (fq.size // m)]
+            tc = time.perf_counter()
+            orc.fastq_map(oi, fq1, nthreads=1, outputs=False, totals=True)
+            dt_1 = time.perf_counter() - tc
+            cpu["single_core"] = {"value": m1 / dt_1, "cores": 1,
+                                  "sample": "first %d reads, 1 thread, %.1fs" % (m1, dt_1)}
+        cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+        if os.path.exists(cal):  # reference sparse_chain vs the oracle's, timed in the build container
+            cpu["calibration"] = json.load(open(cal)).get("summary")
     e2e = None
     if not args.no_end_to_end:
         try:

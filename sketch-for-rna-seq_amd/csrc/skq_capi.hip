@@ -150,6 +150,7 @@ struct skq_session {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork{}, ev_join[2]{};  // ev_join[b]: k_bin_sum of the last batch of parity b
     bool join_rec[2] = {false, false};
+
 };
 
 int skq::session_device(const skq_session* s) { return s->idx->device; }
@@ -434,18 +435,19 @@ int build_compact(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
 }
 
 
-// Chained tables for one k slot (ChainParams::chain). The transcripts are sketched in position
-// order (the index's own hashing: skq::sketch_positions); every retained k-mer's successors within
-// CHAIN_HOPS retained positions in any transcript are candidates for its entry, nearest first
-// (ties: smaller key). An entry is 8 slots of 16 B: records [key, n << 22 | t0, t1, t2] (a list
-// of 4-7 continues in the next slot as [t3, t4, t5, t6]; longer: [key, 8 << 22, list offset, 0]),
-// the key's own record first, then successors while slots remain. Each record carries its key's
-// WHOLE postings list from the index's own tables (lists[] through the key's list offset), so
-// whatever a record settles is exactly what a lookup of that key returns. The entries (one per
-// present key) are built on the host and scattered on the device into a table of 128-B entries
-// for every possible key up to the largest (27.5 GB at (double)0.05f and 4.24M keys: HBM3E holds
-// it; one 128-B request per lookup, no key hashing).
-constexpr uint32_t CHAIN_HOPS = 8;
+// Chained tables for one k slot (ChainParams::chain; entry layout skq_internal.h CHN_*). The
+// transcripts are sketched in position order (the index's own hashing: skq::sketch_positions);
+// every retained k-mer's successors within CHAIN_HOPS retained positions in any transcript are
+// candidates for its entry, nearest first (ties: smaller key). An entry takes the key's own record,
+// then successors while they fit: at most CHN_KEYS records, CHN_TIDS distinct transcripts over the
+// whole entry (their ids stored once) and CHN_CLASSES distinct postings lists (each an 8-bit mask
+// over those ids); a successor that does not fit is skipped, a later one may. A record names its
+// key's WHOLE postings list (the index's own lists[]), so whatever it settles is exactly what a
+// lookup of that key returns. The entries (one per present key) are built on the host and
+// scattered on the device into a table of 128-B entries for every possible key up to the largest
+// (27.5 GB at (double)0.05f and 4.24M keys: HBM3E holds it); entries of absent keys stay zero.
+// One entry settles all of a read's retained hashes for 92 % of cfg3's reads (tools/chain_sim.py).
+constexpr uint32_t CHAIN_HOPS = 12;
 
 __global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* ent, uint64_t n) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -453,11 +455,55 @@ __global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* e
     tab[(uint64_t)keys[j >> 3] * 8 + (j & 7)] = ent[j];
 }
 
+// one key's entry: its own record (a list of <= CHN_TIDS transcripts), then successors in order
+// while they fit (records, distinct transcripts, distinct lists); returns the successors taken
+static uint32_t chain_entry(uint32_t* e, uint32_t key, uint32_t off, const std::vector<uint32_t>& lists,
+                            const uint32_t* sk, const uint32_t* so, size_t ns) {
+    if (lists[off] > skq::CHN_TIDS) {
+        e[0] = skq::CHN_LONG;
+        return 0;
+    }
+    uint32_t tids[skq::CHN_TIDS], nt = 0, cls[skq::CHN_CLASSES], nc = 0, nr = 0;
+    auto add = [&](uint32_t k2, uint32_t o2) -> bool {
+        const uint32_t n = lists[o2];
+        if (n == 0 || n > skq::CHN_TIDS) return false;
+        uint32_t tt[skq::CHN_TIDS], ntt = nt, mk = 0;
+        std::copy(tids, tids + nt, tt);
+        for (uint32_t q = 0; q < n; ++q) {
+            const uint32_t t = lists[o2 + 1 + q];
+            uint32_t s = 0;
+            while (s < ntt && tt[s] != t) ++s;
+            if (s == ntt) {
+                if (ntt == skq::CHN_TIDS) return false;
+                tt[ntt++] = t;
+            }
+            mk |= 1u << s;
+        }
+        uint32_t c = 0;
+        while (c < nc && cls[c] != mk) ++c;
+        if (c == nc) {
+            if (nc == skq::CHN_CLASSES) return false;
+            cls[nc++] = mk;
+        }
+        std::copy(tt, tt + ntt, tids);
+        nt = ntt;
+        e[skq::CHN_W_KEY + nr++] = ~(k2 << 4 | c);
+        return true;
+    };
+    add(key, off);  // (always fits)
+    uint32_t taken = 0;
+    for (size_t q = 0; q < ns && nr < skq::CHN_KEYS; ++q) taken += add(sk[q], so[q]) ? 1u : 0u;
+    e[0] = nr;
+    for (uint32_t c = 0; c < nc; ++c) e[skq::CHN_W_MASK + c / 4] |= cls[c] << (8 * (c & 3));
+    for (uint32_t t = 0; t < nt; ++t) e[skq::CHN_W_TID + t] = tids[t];
+    return taken;
+}
+
 int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
                 const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
                 uint32_t nseq, uint32_t threshold) {
     const uint64_t m = keys.size();
-    if (m == 0) return 0;
+    if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key << 4)
     const uint64_t len = (uint64_t)keys.back() + 1;
     // 128 B per possible key, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
     uint64_t budget = 65536ull << 20;
@@ -496,34 +542,18 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
     std::vector<uint32_t> ent(m * skq::CHAIN_WORDS, 0);
     std::vector<uint8_t> built(m, 0);
     std::atomic<uint64_t> nsucc{0};
+    auto index_of = [&](uint32_t key) -> int64_t {
+        const auto it = std::lower_bound(keys.begin(), keys.end(), key);
+        return it != keys.end() && *it == key ? (int64_t)(it - keys.begin()) : -1;
+    };
     {
         std::atomic<uint32_t> next{0};
         std::vector<std::thread> pool;
         for (uint32_t w = 0; w < P; ++w)
             pool.emplace_back([&] {
                 std::vector<Cand> c;
+                std::vector<uint32_t> sk, so;
                 uint64_t ns = 0;
-                auto index_of = [&](uint32_t key) -> int64_t {
-                    const auto it = std::lower_bound(keys.begin(), keys.end(), key);
-                    return it != keys.end() && *it == key ? (int64_t)(it - keys.begin()) : -1;
-                };
-                // one record in slots (4 words each); false: no room
-                auto put = [&](uint32_t* e, uint32_t& used, uint32_t key, uint32_t off) -> bool {
-                    const uint32_t n = lists[off];
-                    const uint32_t slots = (n >= 4 && n <= 7) ? 2u : 1u;
-                    if (used + slots > skq::CHAIN_WORDS / 4) return false;
-                    uint32_t* w = e + 4 * used;
-                    w[0] = key;
-                    if (n <= 7) {
-                        w[1] = (n << 22) | lists[off + 1];
-                        for (uint32_t q = 1; q < n; ++q) w[1 + q] = lists[off + 1 + q];  // (t3.. run into the next slot)
-                    } else {
-                        w[1] = skq::CMP_LONG << 22;
-                        w[2] = off;
-                    }
-                    used += slots;
-                    return true;
-                };
                 for (uint32_t b; (b = next.fetch_add(1)) < NB;) {
                     c.clear();
                     for (uint32_t q = 0; q < P; ++q) c.insert(c.end(), part[q][b].begin(), part[q][b].end());
@@ -533,19 +563,19 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
                         while (j < c.size() && c[j].h == c[i].h) ++j;
                         const int64_t x = index_of(c[i].h);
                         if (x >= 0 && !built[x]) {
-                            uint32_t* e = ent.data() + (uint64_t)x * skq::CHAIN_WORDS;
-                            uint32_t used = 0;
-                            put(e, used, c[i].h, vals[x]);  // the key's own record first (always fits)
-                            built[x] = 1;
-                            std::vector<uint32_t> seen;
+                            // the key's successors, each once, nearest first
+                            sk.clear();
+                            so.clear();
                             for (size_t q = i; q < j; ++q) {
-                                if (std::find(seen.begin(), seen.end(), c[q].g) != seen.end()) continue;
-                                seen.push_back(c[q].g);
+                                if (std::find(sk.begin(), sk.end(), c[q].g) != sk.end()) continue;
                                 const int64_t y = index_of(c[q].g);
                                 if (y < 0) continue;
-                                if (!put(e, used, c[q].g, vals[y])) break;
-                                ++ns;
+                                sk.push_back(c[q].g);
+                                so.push_back(vals[y]);
                             }
+                            ns += chain_entry(ent.data() + (uint64_t)x * skq::CHAIN_WORDS, c[i].h, vals[x], lists,
+                                              sk.data(), so.data(), sk.size());
+                            built[x] = 1;
                         }
                         i = j;
                     }
@@ -556,19 +586,8 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
         for (auto& t : pool) t.join();
     }
     // keys no transcript of `seqs` retained still get their own record
-    for (uint64_t x = 0; x < m; ++x) {
-        if (built[x]) continue;
-        uint32_t* e = ent.data() + x * skq::CHAIN_WORDS;
-        const uint32_t off = vals[x], n = lists[off];
-        e[0] = keys[x];
-        if (n <= 7) {
-            e[1] = (n << 22) | lists[off + 1];
-            for (uint32_t q = 1; q < n; ++q) e[1 + q] = lists[off + 1 + q];
-        } else {
-            e[1] = skq::CMP_LONG << 22;
-            e[2] = off;
-        }
-    }
+    for (uint64_t x = 0; x < m; ++x)
+        if (!built[x]) chain_entry(ent.data() + x * skq::CHAIN_WORDS, keys[x], vals[x], lists, nullptr, nullptr, 0);
     uint32_t* dk = nullptr;
     uint4* de = nullptr;
     if (dev_alloc(&ix->d_chain, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
@@ -946,9 +965,10 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
     s->bin_nb = s->bin_bits <= 14 ? (uint32_t)(((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits) : 0u;
     const uint64_t nW = (max_reads + skq::WG - 1) / skq::WG;
+    const uint64_t rwords = nW * skq::WG * skq::CCAP;
     for (int b = 0; b < 2 && s->bin_nb; ++b)
         if ((rc = dev_alloc(&s->bin_hdr[b], (uint64_t)(s->bin_nb + 1) * nW)) ||
-            (rc = dev_alloc(&s->bin_region[b], nW * skq::WG * skq::CCAP))) {
+            (rc = dev_alloc(&s->bin_region[b], rwords))) {
             skq_session_free(s);
             return rc;
         }
@@ -976,6 +996,7 @@ int skq_session_free(skq_session* s) {
         (void)hipEventDestroy(s->ev_fork);
         (void)hipEventDestroy(s->ev_join[0]);
         (void)hipEventDestroy(s->ev_join[1]);
+
     }
     dev_free(s->status);
     dev_free(s->hash_cnt);
@@ -1216,6 +1237,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.chain = reinterpret_cast<const uint32_t*>(ix->d_chain);
     p.chain_len = ix->chain_len;
     p.stamps = s->stamps;
+    if (const char* e = std::getenv("SKQ_ABLATE")) p.ablate = (uint32_t)std::strtoul(e, nullptr, 0);
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
     p.bin_nb = s->bin_nb;
@@ -1301,6 +1323,12 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
         return rc;
+    // (chained records hold key << 4 and decode unused slots as 0x0FFFFFFF: reads sketched at a
+    // threshold that reaches that far use the wide entries alone)
+    if (sp.threshold >= skq::CHN_KEY_LIMIT) {
+        cp.chain = nullptr;
+        cp.chain_len = 0;
+    }
     // candidates packed too, unless the totals would be binned from the padded rows (k_bin)
     s->cand_packed = s->hash_packed && (!accumulate || cp.slow_totals);
     cp.cpack = s->cand_packed ? 1u : 0u;

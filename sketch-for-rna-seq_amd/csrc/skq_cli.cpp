@@ -51,7 +51,7 @@ void print_help(const std::string& prog) {
               << "  " << prog << " -o quant <index_file> <reads.fastq> <output>\n\n"
               << "Environment: SKQ_DEVICE (GPU ordinal, default 0), SKQ_DEVICES (GPU list for quant,\n"
               << "             e.g. 0,1,2,3 or all), SKQ_BATCH (reads per batch), SKQ_CHUNK_MB (FASTQ MiB\n"
-              << "             per device chunk, default 32), SKQ_REDUCE (rccl | host: how the EM sums\n"
+              << "             per device chunk, default 64), SKQ_REDUCE (rccl | host: how the EM sums\n"
               << "             reduce over devices; rccl on one device runs the sharded EM over a\n"
               << "             one-rank RCCL communicator).\n";
 }

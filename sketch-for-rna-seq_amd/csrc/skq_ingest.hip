@@ -413,9 +413,17 @@ uint8_t* pin_take(uint64_t need, uint64_t& cap, int device) {
     return nullptr;
 }
 
+// (bounded by bytes: one ingest's slots per device, at most 512 MiB in all; what does not fit is
+// freed at once)
+constexpr uint64_t PIN_CACHE_BYTES = 512ull << 20;
 void pin_give(uint8_t* p, uint64_t cap, int device) {
     std::lock_guard<std::mutex> lk(g_pin_mu);
-    if (g_pins.size() < 16) {
+    uint64_t held = 0, mine = 0;
+    for (const Pin& x : g_pins) {
+        held += x.cap;
+        mine += x.device == device ? 1u : 0u;
+    }
+    if (mine < (uint64_t)NSLOT && held + cap <= PIN_CACHE_BYTES) {
         g_pins.push_back({p, cap, device});
         return;
     }

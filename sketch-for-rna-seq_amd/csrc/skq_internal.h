@@ -182,6 +182,10 @@ struct ChainParams {
     uint32_t* bin_region;
     int slow_totals;
     uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
+    uint32_t ablate;           // development (SKQ_ABLATE, results WRONG when set): k_map1 phases
+                               // skipped to price them: 2 entry-list gathers, 4 filter/order/candidate
+                               // writes, 8 hash writes, 16 base loads (codes left as they are),
+                               // 32 windows after the first
     // multi-k map by passes (k_map1 pass mode; the final pass merges): per k slot i and read r, the
     // entries of the read's count table at that k that meet that k's need (tid << 8 | count):
     // kcnt[i * n + r] of them at ktab[(i * TS + j) * n + r], and the need itself (min(ceil(fraction
@@ -204,10 +208,10 @@ struct ChainParams {
     const uint32_t* wdir[SKQ_MAX_K];
     uint64_t wdir_len[SKQ_MAX_K];
     // chained tables (k_map1 TAB = 3, one k slot): a 128-B entry per possible key
-    // (chain_len of them, 8 uint4 each): word 0 = payload words used (0: no key), then records
-    // [key, n << 22 | t0, t1 .. t(n-1)] (n <= 7) or [key, 8 << 22, list offset], the entry's own
-    // key first, then keys that follow it along the transcripts (nearest first), each with its
-    // whole postings list: one 128-B request settles a run of a read's retained hashes
+    // (chain_len of them, 8 uint4 each; layout CHN_* below): the key's own record, then records of
+    // keys that follow it along the transcripts (nearest first), each naming the key's WHOLE
+    // postings list as a set of the entry's transcripts, so one 128-B request settles a run of a
+    // read's retained hashes
     const uint32_t* chain;
     uint64_t chain_len;
 };
@@ -221,7 +225,19 @@ uint64_t session_max_reads(const skq_session* s);
 // host: one sequence's retained hashes at k in position order (repeats kept; ntHash's window
 // rules: windows holding a byte outside ACGTUacgtu skipped) (skq_tables.cpp)
 void sketch_positions(const uint8_t* s, uint64_t len, uint32_t k, uint32_t thr, std::vector<uint32_t>& out);
+// Chained entries (ChainParams::chain), CHAIN_WORDS words per possible key:
+//   word 0            header: records (0..CHN_KEYS); CHN_LONG: the key's own list holds more than
+//                     CHN_TIDS transcripts (the entry holds nothing: lookups go to the wide entries);
+//                     an all-zero entry: no such key
+//   words 1-2         class masks: class c (0..7) = byte c of the pair, a set over the entry's ids
+//   words 3-10        the entry's transcript ids (up to CHN_TIDS, each once)
+//   words 11-26       records: ~(key << 4 | class), the entry's own key first (unused: 0, which
+//                     decodes to the key 0x0FFFFFFF no retained hash reaches: keys < CHN_KEY_LIMIT)
 constexpr uint32_t CHAIN_WORDS = 32;  // chained entry: 128 B
+constexpr uint32_t CHN_KEYS = 16, CHN_TIDS = 8, CHN_CLASSES = 8;
+constexpr uint32_t CHN_W_MASK = 1, CHN_W_TID = 3, CHN_W_KEY = 11;
+constexpr uint32_t CHN_LONG = 0x80000000u;
+constexpr uint32_t CHN_KEY_LIMIT = 0x0FFFFFFFu;
 // host: ascending sort with threads (skq_tables.cpp)
 void parallel_sort_u64(std::vector<uint64_t>& v, int threads);
 // host: tables from (key << 32 | tid) words per distinct k (consumed; duplicates removed)

@@ -604,6 +604,8 @@ int skq_index_open(const char* path, skq_legacy_index** out, int* from_sidecar) 
                         ix->tx.offs.resize(ntx + 1);
                         r.raw(ix->tx.offs.data(), (ntx + 1) * 8);
                         r.ok = r.ok && ix->tx.offs[0] == 0 && ix->tx.offs[ntx] == sb;
+                        // (never decreasing: the chained tables' builder sketches offs[u] .. offs[u+1])
+                        for (uint32_t u = 0; r.ok && u < ntx; ++u) r.ok = ix->tx.offs[u] <= ix->tx.offs[u + 1];
                     } else {
                         r.ok = false;
                     }

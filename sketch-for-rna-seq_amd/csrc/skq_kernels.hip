@@ -560,8 +560,11 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     s_cnt = 0;
                     s_at = ~0ull;
                     if (nw > SLOW_CAP) {
-                        const unsigned long long at = atomicAdd(bump, (unsigned long long)run_words((uint32_t)nw));
-                        if (at + run_words((uint32_t)nw) <= p.hash_ext_cap && at + nw <= RUN_MAX) s_at = at;
+                        // (packed layout: room for the run's [count, share] header too, whatever
+                        // share of the windows is retained)
+                        const uint32_t need = run_words((uint32_t)nw + (p.hpack ? 2u : 0u));
+                        const unsigned long long at = atomicAdd(bump, (unsigned long long)need);
+                        if (at + need <= p.hash_ext_cap && at + need <= RUN_MAX) s_at = at;
                         else atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
                     }
                 }
@@ -636,16 +639,12 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
                     uint32_t u = 0;
                     for (uint32_t x = 0; x < m; ++x)
                         if (x == 0 || ext[x] != ext[u - 1]) ext[u++] = ext[x];
-                    if (p.hpack) {  // the run behind its header (nw > u + 1: not every window is retained)
-                        if (u + 2 > nw) {
-                            atomicOr(&p.ctrl[C_ERR1], (uint32_t)E_HASH_EXT);
-                        } else {
-                            const uint32_t sh = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
-                            for (uint32_t x = u; x > 0; --x) ext[x + 1] = ext[x - 1];
-                            ext[1] = sh;
-                            ext[0] = u;
-                            p.hash_cnt[(uint64_t)i * p.n + r] = run_mark(s_at, sh);
-                        }
+                    if (p.hpack) {  // the run behind its header (allocated nw + 2 words)
+                        const uint32_t sh = packed_share(p.hash_cnt, p.hash_ext, (uint64_t)i * p.n + r);
+                        for (uint32_t x = u; x > 0; --x) ext[x + 1] = ext[x - 1];
+                        ext[1] = sh;
+                        ext[0] = u;
+                        p.hash_cnt[(uint64_t)i * p.n + r] = run_mark(s_at, sh);
                     } else {
                         if (u <= p.hcap) {
                             for (uint32_t x = 0; x < u; ++x) slot[(uint64_t)x * p.n] = ext[x];
@@ -1949,24 +1948,17 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // k_map1 LDS: per wave max(staged codes + bad bits, one pass of the entry list: MAP_P hashes and
 // their owning lanes)
 // (the per-chunk bad bits sit in row 0 of the wave's raw columns, dead until hashing starts; the
-// binning counts in wave 0's region, dead once every wave has counted; HCAP + 1 raw rows, the
+// binning counts in wave 0's region, dead once every wave has counted; HCAP + 2 raw rows, the
 // last one the sink of windows past the capacity)
 // (MAP_P: 8 per read; at 384 — the mean of cfg3's ~6.0 distinct hashes per read x 64 — half of
 // the waves listed their hashes in two passes, the second one a dependent reload and gather
 // round; profiles/r3_map1_writes.log)
 constexpr uint32_t MAP_P = 512;
-// chained tables: the wave's entries' record keys ([64][8]) and hit masks ([64]), dead once the
-// entry list is written, then (after the list) the per-read overflow flags
-__host__ __device__ inline size_t chn_flag_at(uint32_t) {
-    const size_t keys = (size_t)64 * 8 * 4 + 256, list = ((size_t)MAP_P * 5 + 15) & ~(size_t)15;
-    return keys > list ? keys : list;
-}
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
-// lanes (u8; compact tables: u32 slot | lane << 26) — or the chained step's keys (tab: 0 wide,
-// 2 compact, 3 chained). (Round 3 measured 6 workgroups per CU against 5 with the list packed
+// lanes (u8; compact tables: u32 slot | lane << 26) (tab: 0 wide, 2 compact, 3 chained over
+// wide). (Round 3 measured 6 workgroups per CU against 5 with the list packed
 // tighter: no change, profiles/r3_ingest_sweep.log.)
 inline size_t map1_flag_at(int tab, uint32_t hcap) {
-    if (tab == 3) return chn_flag_at(hcap);
     if (tab == 2) return (size_t)MAP_P * 8;
     return ((size_t)MAP_P * 5 + 15) & ~(size_t)15;
 }
@@ -1983,7 +1975,7 @@ size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
     p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
     p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
     // (+ the binning epilogue's bucket counters, their own so they are zeroed up front)
-    return sketch_tab_bytes(1) + (WG / 64) * (size_t)p.map_wave_bytes + ((size_t)hcap + 1) * WG * 4 +
+    return sketch_tab_bytes(1) + (WG / 64) * (size_t)p.map_wave_bytes + ((size_t)hcap + 2) * WG * 4 +
            (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 }
 
@@ -2015,6 +2007,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     constexpr bool CMP = TAB == 2, CHN = TAB == 3;
     static_assert(PASS || !FINAL, "the final pass is a pass");
     static_assert(!(CHN && PASS), "chained tables serve one k slot");
+    static_assert(!CHN || HCAP <= 32, "hit bits");
     const uint32_t ks = PASS ? p.kslot : 0u;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2023,13 +2016,15 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
     const size_t wave_bytes = p.map_wave_bytes;
-    uint2* s_tab = reinterpret_cast<uint2*>(smem);
+    // (the roll terms in static LDS: their addresses fold into the reads' offsets)
+    __shared__ uint2 s_tab_st[16 + 4];
+    uint2* s_tab = s_tab_st;
     const uint2* s_seed = s_tab + 16;
     unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
     uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * wave_bytes);
     uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + wv * 64);  // (row 0 of the wave's columns)
-    uint32_t* s_bc = s_raw + (HCAP + 1) * WG;  // the binning's bucket counters (map1_layout)
+    uint32_t* s_bc = s_raw + (HCAP + 2) * WG;  // the binning's bucket counters (map1_layout)
     const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
     for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot ks's roll terms, then the seeds
         const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
@@ -2071,7 +2066,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             if (lane < (nch + 63) / 64)
                 s_badw[lane] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sw + sbad) + lane);
         }
-        for (uint32_t cb = lane; cb < nch && !(PASS && sw && ks > 0); cb += SU * 64) {
+        for (uint32_t cb = lane; cb < nch && !(PASS && sw && ks > 0) && !(cp.ablate & 16u); cb += SU * 64) {
             uint4 vv[SU];
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u) {
@@ -2151,6 +2146,15 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     uint64_t keepm = 0;  // bit j: v[j] is a distinct retained hash
     uint32_t nraw_out = 0;  // retained windows in the raw rows (position order), fast reads
     const bool hashing = live && !slow && !sk_prev && st == SKQ_READ_OK;
+    // chained tables: the read's first retained window (position order) is its query; its entry is
+    // requested as soon as the hashing loop is done, so the sort and the hash writes below run
+    // while it is in flight
+    // (the request is issued by every lane outside any divergent branch — lanes without a query
+    // read entry 0 and drop it — so no copy at a branch join waits for it)
+    uint32_t cq = 0;
+    bool has_q = false;
+    uint4 ce[CHN ? 7 : 1];
+    uint32_t nraw = 0;  // retained windows (position order) in the raw rows
     if (hashing) {
         const uint32_t T = p.threshold;
         const uint32_t L = (uint32_t)len;
@@ -2177,15 +2181,27 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         }
         uint32_t* raw = s_raw + tid;
         raw[0] = hlo;
-        uint32_t nraw = hlo <= T ? 1u : 0u;  // src/sketch.cpp:33-35
         const uint32_t nw = L - k + 1;
         const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
         // windows 1..nw-1, 16 per block (in-base at w + k - 1, out-base at w - 1). A window's roll
         // term sits at byte (in << 5 | out << 3) of s_tab: with A the in-bases' 2-bit codes
         // shifted up by 2 and B the out-bases', the nibbles of ce = A:B (even windows) and
         // co = B:A (odd windows) hold (in, out) pairs, so a term's offset is one shift and one
-        // mask. Every window's value goes to raw slot min(nraw, HCAP) (HCAP: a spare slot); full
-        // blocks skip the window-count test.
+        // mask. Every window's value is stored at the lane's write row: rows 0..HCAP-1 hold the
+        // retained windows in order, row HCAP takes the rest once HCAP are retained and row
+        // HCAP + 1 once more are (the read then goes slow); the row only advances on a retained
+        // window. The test hlo <= T (src/sketch.cpp:33-35) is the borrow of T - hlo computed
+        // bitwise — (~T & h) | (~(T ^ h) & (T - h)), bit 31 — so no compare result passes through
+        // VCC: a VALU write of VCC read by the next VALU stalls the SIMD (tools/micro/valu_rate).
+        const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)raw;
+        const uint32_t rlim = rbase + (uint32_t)(HCAP + 1) * WG * 4;
+        auto radv = [&](uint32_t h) -> uint32_t {  // (h <= T) << 10 (the row stride, WG * 4 bytes)
+            const uint32_t d = T - h;
+            const uint32_t g = ~((~T & h) | (~(T ^ h) & d));
+            return (g >> 21) & ((uint32_t)WG * 4u);
+        };
+        static_assert(WG * 4 == 1024, "row stride");
+        uint32_t wa = min(rbase + radv(hlo), rlim);  // the next write's row
         const unsigned char* tabb = reinterpret_cast<const unsigned char*>(s_tab);
         auto block = [&](uint32_t w0, uint32_t jn, auto full) {
             const uint32_t A = codes16(qin + w0 - 1), B = codes16(qout + w0 - 1);
@@ -2204,14 +2220,27 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 roll33b(hlo, hhi, e[j]);
-                const bool rec = hlo <= T && (decltype(full)::value || (uint32_t)j < jn);
-                raw[min(nraw, (uint32_t)HCAP) * WG] = hlo;
-                nraw += rec ? 1u : 0u;
+                *(__attribute__((address_space(3))) uint32_t*)(size_t)wa = hlo;
+                uint32_t adv = radv(hlo);
+                if (!decltype(full)::value) adv &= (uint32_t)((int)(j - (int)jn) >> 31);  // (windows past the read)
+                wa = min(wa + adv, rlim);
             }
         };
         uint32_t w0 = 1;
-        for (; w0 + 16 <= nw; w0 += 16) block(w0, 16u, std::true_type{});
-        if (w0 < nw) block(w0, nw - w0, std::false_type{});
+        for (; w0 + 16 <= nw && !(cp.ablate & 32u); w0 += 16) block(w0, 16u, std::true_type{});
+        if (w0 < nw && !(cp.ablate & 32u)) block(w0, nw - w0, std::false_type{});
+        nraw = (wa - rbase) / (WG * 4u);  // (HCAP + 1: more than HCAP retained)
+    }
+    if constexpr (CHN) {
+        cq = s_raw[tid];  // (raw row 0: the first retained window)
+        has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len;
+        // words 0-26 of the entry (27-31 unused)
+        const uint4* ent = reinterpret_cast<const uint4*>(cp.chain) + (has_q ? (uint64_t)cq * 8 : 0ull);
+#pragma unroll
+        for (int u = 0; u < 7; ++u) ce[u] = ent[u];
+        has_q = hashing && nraw && nraw <= HCAP;  // (a query past the table: no such key)
+    }
+    if (hashing) {
         if (nraw > HCAP) {
             slow = true;
         } else {
@@ -2237,7 +2266,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // region — whole 64-B lines, where the padded rows leave most lines partly written (the
     // kernel's write requests share the fabric's request budget with its gathers)
     uint32_t hoff = 0;  // (packed) this read's first hash in the wave's region of k slot ks
-    if (p.hpack) {
+    if (p.hpack && !(cp.ablate & 8u)) {
         const uint32_t mw = (uint32_t)__builtin_popcountll(keepm);
         hoff = wave_incl_scan(mw, lane) - mw;
         uint32_t* out = p.hashes + (uint64_t)ks * p.hcap * p.n + (r - lane) * p.hcap + hoff;
@@ -2280,9 +2309,6 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const bool act = hashing && !slow && (!PASS || cp.tabs[ks].present);
     const uint64_t keepm_all = keepm;  // the read's distinct retained hashes (as written out)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
-    // chained tables: the read's first retained window (position order) is its chain query, read
-    // from its own raw column before the count table overlays it
-    const uint32_t cq = CHN && act && nraw_out ? s_raw[tid] : 0u;
 #pragma unroll
     for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
     uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + p.map_flag_at);  // per read: > TS transcripts
@@ -2299,16 +2325,16 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // slot sl of read (lane) o sits in column (o + sl) & 63 of row sl: the slots of one read
     // fall in distinct LDS banks (the lane pairs of one round mostly insert into the same read)
     // an insert whose home slot holds another tid probes on from the next slot (rare: not unrolled)
-    auto ains_probe = [&](uint32_t x, uint32_t o) {
+    auto ains_probe = [&](uint32_t x, uint32_t o, uint32_t c = 1u) {
         uint32_t sl = Counter<1, WG>::slot_of(x);
 #pragma unroll 1
         for (int z = 1; z < TS; ++z) {
             sl = (sl + 1) & (TS - 1);
             uint32_t* a = colbase + sl * WG + ((o + sl) & 63u);
-            const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | 1u);
+            const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | c);
             if (old == EMPTY) return;
             if ((old >> 8) == x) {
-                atomicAdd(a, 1u);
+                atomicAdd(a, c);
                 return;
             }
         }
@@ -2323,119 +2349,71 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         else ains_probe(x, o);
     };
     if constexpr (CHN) {
-        // chained tables, one request per read (ChainParams::chain): the entry of the read's first
-        // retained window holds 8 slots of 16 B — records [key, n << 22 | t0, t1, t2] (a list of
-        // 4-7 continues in the next slot as [t3, t4, t5, t6]; n = 8: [key, 8 << 22, list offset]),
-        // the window's own record first, then those of the keys that follow it in the transcripts.
-        // Lane group g of 8 loads the entry of read 8u + g, one slot per lane, u = 0..7; a lane
-        // matches its record's key against the owner's distinct retained hashes (LDS) and, on a
-        // match, inserts the record's tids into the owner's count table (the CAS inserts below)
-        // and marks the hash counted. What is left goes through the entry list as before.
-        const uint4* ctab = reinterpret_cast<const uint4*>(cp.chain);
-        const uint64_t clen = cp.chain_len;
-        uint32_t* s_keys = reinterpret_cast<uint32_t*>(s_wave);  // [64 owners][8 slots]: record keys
-        uint32_t* s_hit = s_keys + 64 * 8;                         // [64 owners]: slots whose key it holds
-        s_flag[lane] = 0;
-        const int has_q = act && nraw_out ? 1 : 0;
-        const uint32_t slot = lane & 7u;
-        // the owner's side: which of its retained hashes a key is (keepm bits)
-        auto match = [&](uint32_t key) -> uint32_t {
-            uint32_t mm = 0;
+        // chained tables, one request per read (ChainParams::chain, layout skq_internal.h CHN_*):
+        // the lane matches its own retained hashes (v, registers) against the records of its
+        // query's entry (ce, requested after the hashing loop), counts each matched record's
+        // transcript set into per-transcript byte counters over the entry's ids, and inserts those
+        // into its own count table (no other lane writes it before the entry list below). What no
+        // record holds goes through the entry list as before. An all-zero entry (no such key, or a
+        // query past the table) settles the query itself: no postings.
+        uint32_t w[28];
+        const bool inb = has_q && cq < cp.chain_len;  // (else the lane read entry 0 and drops it)
 #pragma unroll
-            for (int j = 0; j < HCAP; ++j) mm |= (v[j] == key ? 1u : 0u) << j;
-            return mm & (uint32_t)keepm;
-        };
-        uint32_t cov = 0;
-        // two batches of 4 owner rounds: half of the wave's reads each
-#pragma unroll 1
-        for (uint32_t u0 = 0; u0 < 8; u0 += 4) {
-            uint4 xb[4];
-            uint64_t heads[4];
-#pragma unroll
-            for (uint32_t w = 0; w < 4; ++w) {
-                const uint32_t o = 8 * (u0 + w) + (lane >> 3);
-                const uint32_t qo = __shfl(cq, o, 64);
-                const int ho = __shfl(has_q, o, 64);
-                xb[w] = make_uint4(0, 0, 0, 0);
-                if (ho && qo < clen) xb[w] = ctab[(uint64_t)qo * 8 + slot];
-            }
-#pragma unroll
-            for (uint32_t w = 0; w < 4; ++w) {
-                const uint32_t o = 8 * (u0 + w) + (lane >> 3);
-                const bool head = (xb[w].y >> 22) != 0;  // (empty slots and continuations: 0)
-                heads[w] = __ballot(head);
-                s_keys[o * 8 + slot] = xb[w].x;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // owners of this batch (lanes 8 u0 .. 8 u0 + 31): match the entry's record keys
-            if ((lane >> 5) == (u0 >> 2)) {
-                const uint32_t w = (lane >> 3) & 3u;  // this owner's round in the batch
-                const uint64_t hw = w == 0 ? heads[0] : w == 1 ? heads[1] : w == 2 ? heads[2] : heads[3];
-                const uint32_t hm = (uint32_t)(hw >> (8 * (lane & 7u))) & 0xFFu;
-                const uint4 k0 = *reinterpret_cast<const uint4*>(s_keys + lane * 8);
-                const uint4 k1 = *reinterpret_cast<const uint4*>(s_keys + lane * 8 + 4);
-                const uint32_t kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-                uint32_t hit = 0;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {  // (an entry's keys are distinct: each counted once)
-                    const uint32_t mm = (hm >> q) & 1u ? match(kk[q]) : 0u;
-                    hit |= mm ? (1u << q) : 0u;
-                    cov |= mm;
-                }
-                // the query is settled by its own record, or is a miss (no entry)
-                if (has_q) cov |= match(cq);
-                s_hit[lane] = has_q ? hit : 0u;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // the slot lanes insert the matched records' tids into the owners' count tables
-#pragma unroll
-            for (uint32_t w = 0; w < 4; ++w) {
-                const uint32_t o = 8 * (u0 + w) + (lane >> 3);
-                const uint4 x = xb[w];
-                const uint32_t n = x.y >> 22;
-                const uint32_t nprev = __shfl_up(n, 1, 64);
-                const uint32_t hm = s_hit[o];
-                const bool hit = (hm >> slot) & 1u;
-                const bool cont = slot > 0 && n == 0 && nprev >= 4 && nprev <= 7;
-                const bool chit = cont && ((hm >> (slot - 1)) & 1u);
-                uint32_t xs[4];
-                bool vs[4];
-                xs[0] = cont ? x.x : x.y & TID_MASK;
-                xs[1] = cont ? x.y : x.z;
-                xs[2] = cont ? x.z : x.w;
-                xs[3] = x.w;
-                vs[0] = (hit && n <= 7) || chit;
-                vs[1] = (hit && n >= 2 && n <= 7) || (chit && nprev >= 5);
-                vs[2] = (hit && n >= 3 && n <= 7) || (chit && nprev >= 6);
-                vs[3] = chit && nprev >= 7;
-                uint32_t olds[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
-                    olds[q] = vs[q] ? atomicCAS(colbase + sl * WG + ((o + sl) & 63u), EMPTY, (xs[q] << 8) | 1u) : EMPTY;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t xq = xs[q], sl = Counter<1, WG>::slot_of(xq), ol = olds[q];
-                    if (ol == EMPTY) continue;
-                    if ((ol >> 8) == xq) atomicAdd(colbase + sl * WG + ((o + sl) & 63u), 1u);
-                    else ains_probe(xq, o);
-                }
-                const bool lng = hit && n == CMP_LONG;  // a list longer than 7 (rare): all of it from lists[]
-                if (__any(lng) && lng) {
-                    const uint32_t lo = x.z, len = cp.lists[lo];
-                    for (uint32_t q = 0; q < len; ++q) ains(cp.lists[lo + 1 + q], o);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int u = 0; u < 7; ++u) {
+            w[4 * u] = inb ? ce[u].x : 0u;
+            w[4 * u + 1] = inb ? ce[u].y : 0u;
+            w[4 * u + 2] = inb ? ce[u].z : 0u;
+            w[4 * u + 3] = inb ? ce[u].w : 0u;
         }
-        keepm &= ~(uint64_t)cov;
+        const bool absent = has_q && w[0] == 0u;
+        uint32_t kh[CHN_KEYS];
+#pragma unroll
+        for (int i = 0; i < (int)CHN_KEYS; ++i) kh[i] = (~w[CHN_W_KEY + i]) >> 4;  // (unused: 0x0FFFFFFF)
+        kh[0] = absent ? cq : kh[0];
+        bool hk[CHN_KEYS];
+#pragma unroll
+        for (int i = 0; i < (int)CHN_KEYS; ++i) hk[i] = false;
+        uint32_t hitv = 0;  // bit j: v[j] is a record's key
+#pragma unroll
+        for (int j = 0; j < HCAP; ++j) {
+            if (!__any((uint32_t)j < nraw_out)) break;  // (uniform: the wave's longest set)
+            bool hj = false;
+#pragma unroll
+            for (int i = 0; i < (int)CHN_KEYS; ++i) {
+                const bool e = v[j] == kh[i];
+                hk[i] = hk[i] || e;
+                hj = hj || e;
+            }
+            hitv |= hj ? (1u << j) : 0u;
+        }
+        // per matched record: its class's transcript set, one byte counter per entry id
+        uint32_t acc0 = 0, acc1 = 0;
+#pragma unroll
+        for (int i = 0; i < (int)CHN_KEYS; ++i) {
+            const uint32_t c = (~w[CHN_W_KEY + i]) & 7u;
+            const uint32_t mw = (c & 4u) ? w[CHN_W_MASK + 1] : w[CHN_W_MASK];
+            const uint32_t mk = __builtin_amdgcn_ubfe(mw, (c & 3u) * 8u, 8u);
+            acc0 += hk[i] ? ((mk & 15u) * 0x00204081u) & 0x01010101u : 0u;
+            acc1 += hk[i] ? ((mk >> 4) * 0x00204081u) & 0x01010101u : 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the entry's ids with their counts into this read's table: every first attempt (a CAS at
+        // the id's home slot) in flight together; the ids are distinct, so an occupied home slot
+        // holds another id and the insert probes on
+        uint32_t olds[CHN_TIDS], xs[CHN_TIDS], cs[CHN_TIDS];
+#pragma unroll
+        for (int q = 0; q < (int)CHN_TIDS; ++q) {
+            cs[q] = ((q < 4 ? acc0 : acc1) >> (8 * (q & 3))) & 0xFFu;
+            xs[q] = w[CHN_W_TID + q];
+            const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
+            olds[q] = cs[q] ? atomicCAS(colbase + sl * WG + ((lane + sl) & 63u), EMPTY, (xs[q] << 8) | cs[q]) : EMPTY;
+        }
+#pragma unroll
+        for (int q = 0; q < (int)CHN_TIDS; ++q)
+            if (olds[q] != EMPTY) ains_probe(xs[q], lane, cs[q]);
+        keepm &= ~(uint64_t)hitv;
     }
     // the wave's entry list: every retained hash not counted above
     const uint64_t keep0 = keepm_all;
@@ -2459,7 +2437,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             rank += kj ? 1u : 0u;
         }
     }
-    for (uint32_t pb = 0; pb < M; pb += MAP_P) {  // wave-uniform
+    for (uint32_t pb = 0; pb < ((cp.ablate & 2u) ? 0u : M); pb += MAP_P) {  // wave-uniform
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2773,7 +2751,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
         }
     } else {
-        if (act) {
+        if (act && !(cp.ablate & 4u)) {
             if (s_flag[lane] == 0) {
                 // filter and order (src/sparse_chaining.cpp:76-110), as Counter::finish
                 uint32_t ev[TS];
@@ -3492,7 +3470,8 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
 }
 
 __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nb, uint32_t nW,
-                                               uint32_t chunk, const uint32_t* hdr, const uint32_t* region) {
+                                               uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
+                                               uint32_t rstride) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
     const uint32_t bs = 1u << bits;
@@ -3510,7 +3489,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
         s1 = hdr[(uint64_t)(b + 1) * nW + w];
     }
     while (w < w1) {
-        const uint32_t* reg = region + (uint64_t)w * (WG * CCAP);
+        const uint32_t* reg = region + (uint64_t)w * rstride;
         const uint32_t wn = w + WG;
         uint32_t n0 = 0, n1 = 0;
         if (wn < w1) {
@@ -3545,7 +3524,8 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
 // dependent round trips: 57 us for 1M reads against 10k transcripts)
 template <int GS>
 __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nW,
-                                                  uint32_t chunk, const uint32_t* hdr, const uint32_t* region) {
+                                                  uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
+                                                  uint32_t rstride) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
     const uint32_t bs = 1u << bits;
@@ -3555,7 +3535,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx
     const uint32_t g = t / GS, gl = t % GS;
     constexpr int U = 8;
     for (uint32_t w = w0 + g; w < w1; w += WG / GS) {
-        const uint32_t* reg = region + (uint64_t)w * (WG * CCAP);
+        const uint32_t* reg = region + (uint64_t)w * rstride;
         const uint32_t s0 = hdr[(uint64_t)b * nW + w], s1 = hdr[(uint64_t)(b + 1) * nW + w];
         for (uint32_t q = s0 + gl; q < s1; q += GS * U) {
             uint32_t x[U];
@@ -3853,10 +3833,10 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum_g<16>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_bin_sum_g<16>, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx,
-                           bits, nW, chunk, hdr, region);
+                           bits, nW, chunk, hdr, region, (uint32_t)(WG * CCAP));
     } else {
         hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits,
-                           nb, nW, chunk, hdr, region);
+                           nb, nW, chunk, hdr, region, (uint32_t)(WG * CCAP));
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
