@@ -22,7 +22,7 @@ ref: $(OUT)/libskq.so
 HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
 LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o \
             $(OUT)/obj/skq_io.o $(OUT)/obj/skq_ingest.o $(OUT)/obj/skq_em.o \
-            $(OUT)/obj/skq_build.o $(OUT)/obj/skq_dropin_io.o
+            $(OUT)/obj/skq_build.o $(OUT)/obj/skq_dropin_io.o $(OUT)/obj/skq_sketcher.o
 HOST_CXX ?= g++
 HOSTFLAGS := $(CXXFLAGS_COMMON) -pthread
 

@@ -113,6 +113,20 @@ int skq_sketch(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, u
  * empty set for that k. Same layout and session results as skq_sketch. */
 int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_offs, uint32_t fixed_len,
                     uint64_t n_seqs, uint32_t max_len, uint32_t threshold, void* stream);
+/* One sequence per call, for per-sequence callers: the reference calls
+ * createSketch_FracMinhash_direct once per transcript per k (src/main.cpp:79) and once per read
+ * per k (src/main.cpp:143-144), and the C++ drop-in (include/dropin/sketch.h, kmer.h) serves those
+ * calls here. skq_sketch_seqs semantics for one sequence; the bytes go through pinned host memory
+ * the device maps, one kernel, one stream synchronisation per call. hashes receives up to cap of
+ * the retained windows' hashes (unordered; a hash retained at two windows appears twice: the
+ * caller's set removes repeats), *count how many there are. Handles are not thread-safe; one per
+ * host thread. max_len only sizes the first buffers (longer sequences grow them). */
+typedef struct skq_sketcher skq_sketcher;
+int skq_sketcher_create(int device, uint64_t max_len, skq_sketcher** out);
+int skq_sketcher_run(skq_sketcher* h, const char* seq, uint64_t len, uint32_t k, uint32_t threshold,
+                     uint32_t* hashes, uint64_t cap, uint64_t* count);
+int skq_sketcher_free(skq_sketcher* h);
+
 /* Chain the session's current sketches; `fraction` as sparse_chain's (0.9 in quant).
  * accumulate != 0 adds each read's candidates into the per-transcript totals. */
 int skq_chain(skq_session* s, double fraction, int accumulate, void* stream);

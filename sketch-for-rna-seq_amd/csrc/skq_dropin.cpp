@@ -53,45 +53,20 @@ struct DevBuf {
     }
 };
 
-// one sketcher per k: an index without tables (sketching only) and a one-sequence session
-struct Sketcher {
-    skq_index* ix = nullptr;
-    skq_session* s = nullptr;
-    DevBuf seq;
-    ~Sketcher() {
-        skq_session_free(s);
-        skq_index_free(ix);
-    }
-};
-
+// one per-call sketcher for every k (skq_sketcher_run: pinned mapped buffers, one kernel, one
+// synchronisation per call), behind the drop-in's single-threaded contract
 std::mutex g_mu;
-std::map<int, std::unique_ptr<Sketcher>> g_sketchers;
-
-Sketcher& sketcher(int k) {
-    auto& slot = g_sketchers[k];
-    if (!slot) {
-        auto sk = std::make_unique<Sketcher>();
-        const uint32_t kk = (uint32_t)k;
-        sk->seq.dev = device();
-        check(skq_index_create(sk->seq.dev, 0, 1, &kk, 0, nullptr, &sk->ix));
-        check(skq_session_create(sk->ix, 1, 256, &sk->s));
-        slot = std::move(sk);
-    }
-    return *slot;
-}
+skq_sketcher* g_sk = nullptr;
+std::vector<uint32_t> g_buf;
 
 std::unordered_set<uint32_t> gpu_sketch(const std::string& seq, int k, uint32_t threshold) {
     std::lock_guard<std::mutex> lock(g_mu);
-    Sketcher& S = sketcher(k);
-    S.seq.put(seq.data(), seq.size());
-    check(skq_sketch_seqs(S.s, static_cast<const uint8_t*>(S.seq.p), nullptr, (uint32_t)seq.size(), 1,
-                          (uint32_t)seq.size(), threshold, nullptr));
-    uint64_t nh = 0, nc = 0;
-    check(skq_session_export(S.s, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &nh, &nc));
-    std::vector<uint32_t> h(nh + 1);
-    uint64_t offs[2];
-    check(skq_session_export(S.s, nullptr, offs, h.data(), nullptr, nullptr, nullptr, &nh, &nc));
-    return std::unordered_set<uint32_t>(h.begin(), h.begin() + (ptrdiff_t)nh);
+    if (!g_sk) check(skq_sketcher_create(device(), 4096, &g_sk));
+    const uint64_t nw = seq.size() >= (size_t)k ? seq.size() - (size_t)k + 1 : 0;
+    if (g_buf.size() < nw + 1) g_buf.resize(nw + 1);
+    uint64_t n = 0;
+    check(skq_sketcher_run(g_sk, seq.data(), seq.size(), (uint32_t)k, threshold, g_buf.data(), nw, &n));
+    return std::unordered_set<uint32_t>(g_buf.begin(), g_buf.begin() + (ptrdiff_t)std::min<uint64_t>(n, nw));
 }
 
 }  // namespace

@@ -2187,23 +2187,19 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // term sits at byte (in << 5 | out << 3) of s_tab: with A the in-bases' 2-bit codes
         // shifted up by 2 and B the out-bases', the nibbles of ce = A:B (even windows) and
         // co = B:A (odd windows) hold (in, out) pairs, so a term's offset is one shift and one
-        // mask. Every window's value is stored at the lane's write row: rows 0..HCAP-1 hold the
-        // retained windows in order, row HCAP takes the rest once HCAP are retained and row
-        // HCAP + 1 once more are (the read then goes slow); the row only advances on a retained
-        // window. The test hlo <= T (src/sketch.cpp:33-35) is the borrow of T - hlo computed
-        // bitwise — (~T & h) | (~(T ^ h) & (T - h)), bit 31 — so no compare result passes through
-        // VCC: a VALU write of VCC read by the next VALU stalls the SIMD (tools/micro/valu_rate).
+        // mask. Every window's value is stored at the lane's write row, which a retained window
+        // (src/sketch.cpp:33-35) advances: rows 0..HCAP-1 hold the retained windows in order, row
+        // HCAP the next and row HCAP + 1 any past it (the read then goes slow). The row is kept as
+        // its distance d below row HCAP + 1, advanced by a saturating subtract, so no compare or
+        // clamp sits in the loop: for T < 2^31 the test h <= T is bit 31 of ~((T - h) | h). Every
+        // operation in the loop but the rotate is a full-rate VALU form (tools/micro/valu_mix:
+        // compares, min/max and the three-operand integer forms issue at half rate).
         const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)raw;
-        const uint32_t rlim = rbase + (uint32_t)(HCAP + 1) * WG * 4;
-        auto radv = [&](uint32_t h) -> uint32_t {  // (h <= T) << 10 (the row stride, WG * 4 bytes)
-            const uint32_t d = T - h;
-            const uint32_t g = ~((~T & h) | (~(T ^ h) & d));
-            return (g >> 21) & ((uint32_t)WG * 4u);
-        };
-        static_assert(WG * 4 == 1024, "row stride");
-        uint32_t wa = min(rbase + radv(hlo), rlim);  // the next write's row
+        constexpr uint32_t ROW = (uint32_t)WG * 4u;
+        const uint32_t rtop = rbase + (uint32_t)(HCAP + 1) * ROW;
+        uint32_t d = (uint32_t)(HCAP + 1) * ROW - (hlo <= T ? ROW : 0u);
         const unsigned char* tabb = reinterpret_cast<const unsigned char*>(s_tab);
-        auto block = [&](uint32_t w0, uint32_t jn, auto full) {
+        auto block = [&](uint32_t w0, uint32_t jn, auto full, auto small) {
             const uint32_t A = codes16(qin + w0 - 1), B = codes16(qout + w0 - 1);
             const uint32_t A2 = A << 2;
             const uint32_t ce = (A2 & 0xCCCCCCCCu) | (B & 0x33333333u);
@@ -2220,24 +2216,39 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 roll33b(hlo, hhi, e[j]);
-                *(__attribute__((address_space(3))) uint32_t*)(size_t)wa = hlo;
-                uint32_t adv = radv(hlo);
+                *(__attribute__((address_space(3))) uint32_t*)(size_t)(rtop - d) = hlo;
+                uint32_t adv = decltype(small)::value ? ((~((T - hlo) | hlo)) >> 21) & ROW : (hlo <= T ? ROW : 0u);
                 if (!decltype(full)::value) adv &= (uint32_t)((int)(j - (int)jn) >> 31);  // (windows past the read)
-                wa = min(wa + adv, rlim);
+                d = __builtin_elementwise_sub_sat(d, adv);
             }
         };
         uint32_t w0 = 1;
-        for (; w0 + 16 <= nw && !(cp.ablate & 32u); w0 += 16) block(w0, 16u, std::true_type{});
-        if (w0 < nw && !(cp.ablate & 32u)) block(w0, nw - w0, std::false_type{});
-        nraw = (wa - rbase) / (WG * 4u);  // (HCAP + 1: more than HCAP retained)
+        if (T < 0x80000000u) {  // (uniform)
+            for (; w0 + 16 <= nw && !(cp.ablate & 32u); w0 += 16) block(w0, 16u, std::true_type{}, std::true_type{});
+            if (w0 < nw && !(cp.ablate & 32u)) block(w0, nw - w0, std::false_type{}, std::true_type{});
+        } else {
+            for (; w0 + 16 <= nw; w0 += 16) block(w0, 16u, std::true_type{}, std::false_type{});
+            if (w0 < nw) block(w0, nw - w0, std::false_type{}, std::false_type{});
+        }
+        nraw = (rtop - d - rbase) / ROW;  // (HCAP + 1: more than HCAP retained)
     }
     if constexpr (CHN) {
         cq = s_raw[tid];  // (raw row 0: the first retained window)
         has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len;
         // words 0-26 of the entry (27-31 unused)
         const uint4* ent = reinterpret_cast<const uint4*>(cp.chain) + (has_q ? (uint64_t)cq * 8 : 0ull);
+        if (cp.ablate & 64u) {  // (development A/B: the entry's loads with sc0, past the L1)
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int u = 0; u < 7; ++u) ce[u] = ent[u];
+            for (int u = 0; u < 7; ++u) {
+                u32x4 x;
+                asm volatile("global_load_dwordx4 %0, %1, off sc0" : "=v"(x) : "v"(ent + u) : "memory");
+                ce[u] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 7; ++u) ce[u] = ent[u];
+        }
         has_q = hashing && nraw && nraw <= HCAP;  // (a query past the table: no such key)
     }
     if (hashing) {
@@ -2356,6 +2367,18 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // into its own count table (no other lane writes it before the entry list below). What no
         // record holds goes through the entry list as before. An all-zero entry (no such key, or a
         // query past the table) settles the query itself: no postings.
+        if (cp.ablate & 64u) {  // (the asm loads above: wait for them before their registers are read)
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 x[7];
+#pragma unroll
+            for (int u = 0; u < 7; ++u) x[u] = u32x4{ce[u].x, ce[u].y, ce[u].z, ce[u].w};
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6])
+                         :
+                         : "memory");
+#pragma unroll
+            for (int u = 0; u < 7; ++u) ce[u] = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
+        }
         uint32_t w[28];
         const bool inb = has_q && cq < cp.chain_len;  // (else the lane read entry 0 and drops it)
 #pragma unroll
@@ -3763,8 +3786,12 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     case 130: kern = k_map1<32, 4, 2>; break;
     default: return -4;
     }
-    map1_report_occupancy(reinterpret_cast<const void*>(kern), lds);
-    hipLaunchKernelGGL(kern, grid, dim3(WG), lds, st, p, cp);
+    // (development: SKQ_LDS_PAD bytes of unused LDS per workgroup lower the occupancy, to price it)
+    static const size_t pad = std::getenv("SKQ_LDS_PAD") ? std::strtoull(std::getenv("SKQ_LDS_PAD"), nullptr, 10) : 0;
+    if (lds + pad > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds + pad));
+    map1_report_occupancy(reinterpret_cast<const void*>(kern), lds + pad);
+    hipLaunchKernelGGL(kern, grid, dim3(WG), lds + pad, st, p, cp);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

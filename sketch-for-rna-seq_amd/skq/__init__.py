@@ -61,6 +61,9 @@ def lib():
             "skq_session_free": (i32, [vp]),
             "skq_sketch": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
             "skq_sketch_seqs": (i32, [vp, vp, vp, u32, u64, u32, u32, vp]),
+            "skq_sketcher_create": (i32, [i32, u64, C.POINTER(vp)]),
+            "skq_sketcher_run": (i32, [vp, C.c_char_p, u64, u32, u32, vp, u64, C.POINTER(u64)]),
+            "skq_sketcher_free": (i32, [vp]),
             "skq_chain": (i32, [vp, dbl, i32, vp]),
             "skq_map": (i32, [vp, vp, vp, u32, u64, u32, u32, dbl, i32, vp]),
             "skq_chain_sketches": (i32, [vp, u64, vp, vp, vp, vp, dbl, i32, vp]),
@@ -662,6 +665,34 @@ def assign(cand_offs, cand_tid, cand_score, ntx, pi):
     assigned = np.zeros(max(ntx, 1), np.uint8)
     _check(lib().skq_assign(len(o) - 1, _p(o), _p(t), _p(s), ntx, _p(pi), _p(counts), _p(assigned)))
     return counts[:ntx], assigned[:ntx].astype(bool)
+
+
+class Sketcher:
+    """One sequence per call (skq_sketcher_run): the per-sequence path the C++ drop-in serves."""
+
+    def __init__(self, device=0, max_len=4096):
+        self.h = C.c_void_p()
+        _check(lib().skq_sketcher_create(device, max_len, C.byref(self.h)))
+
+    def run(self, seq: bytes, k: int, thr=None):
+        """The retained windows' hashes (unordered, repeats kept) as uint32."""
+        t = threshold() if thr is None else thr
+        nw = max(0, len(seq) - k + 1) if k > 0 else 0
+        out = np.empty(max(nw, 1), np.uint32)
+        n = C.c_uint64()
+        _check(lib().skq_sketcher_run(self.h, seq, len(seq), k, t, _p(out), nw, C.byref(n)))
+        return out[:min(n.value, nw)]
+
+    def free(self):
+        if self.h:
+            lib().skq_sketcher_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def host_sketch(seq: bytes, k: int, thr=None):

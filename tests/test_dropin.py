@@ -63,3 +63,44 @@ def test_dropin_signatures_match_oracle():
         exp = sorted(((names[t], int(sc)) for t, sc in zip(ref["cand_tid"][i, :c], ref["cand_score"][i, :c])),
                      key=lambda x: (-x[1], x[0]))
         assert got_c[rid] == exp, rid
+
+
+@pytest.mark.gpu
+def test_sketcher_per_call_matches_oracle_and_is_cheap():
+    """skq_sketcher_run, the per-sequence path the drop-in's createSketch_FracMinhash_direct and
+    extract_and_hash_kmers_nthash take (src/main.cpp:79,143-144 call them once per sequence per
+    k): sets equal the oracle's for reads, transcripts, ntHash-skipped bytes, lowercase, U, a k
+    longer than the sequence and sequences past the LDS staging size; then the per-call cost on
+    150-bp reads (DESIGN.md §2 records it)."""
+    import time
+
+    import numpy as np
+
+    import skq
+
+    rng = random.Random(7)
+    sk = skq.Sketcher()
+    seqs = [bytes(rng.choice(b"ACGT") for _ in range(n)) for n in (31, 32, 100, 150, 151, 999, 5000)]
+    seqs.append(b"ACGTNACGTACGTACGTACGTACGTACGTACGTACGTACGTAC" * 5)
+    seqs.append(bytes(rng.choice(b"acgtuACGTUN") for _ in range(400)))
+    seqs.append(bytes(rng.choice(b"ACGT") for _ in range(60000)))  # (read in place, past the LDS stage)
+    seqs.append(b"")
+    for s in seqs:
+        for k in (21, 25, 31):
+            for thr in (None, 0xFFFFFFFF):
+                got = set(int(x) for x in sk.run(s, k, thr))
+                if len(s) < k:
+                    assert got == set()
+                    continue
+                exp = set(orc.sketch(s, k, thr)) if thr is None else set(orc.all_hashes(s, k))
+                assert got == exp, (len(s), k, thr)
+    reads = [bytes(rng.choice(b"ACGT") for _ in range(150)) for _ in range(2000)]
+    for r in reads[:50]:
+        sk.run(r, 31)
+    t0 = time.perf_counter()
+    for r in reads:
+        sk.run(r, 31)
+    us = (time.perf_counter() - t0) / len(reads) * 1e6
+    print("skq_sketcher_run: %.1f us per 150-bp read (k = 31, %d calls)" % (us, len(reads)))
+    assert us < 200.0
+    sk.free()

@@ -166,3 +166,39 @@ def test_reference_cli_agrees_with_skq_cli(tmp_path):
         for t, (c, p) in base.items():  # 6 printed digits; EM sums in another order
             assert g[t][0] == pytest.approx(c, rel=5e-6, abs=1e-9), (name, t)
             assert g[t][1] == pytest.approx(p, rel=5e-6), (name, t)
+
+
+def _timed(exe, *args):
+    """(stdout lines with the seconds since start at which each appeared, total seconds)"""
+    import time
+    t0 = time.perf_counter()
+    p = subprocess.Popen([exe, *map(str, args)], stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = []
+    for ln in p.stdout:
+        lines.append((time.perf_counter() - t0, ln.rstrip()))
+    assert p.wait(timeout=600) == 0
+    return lines, time.perf_counter() - t0
+
+
+@pytest.mark.gpu
+@need_bins
+def test_reference_cli_timing_200tx_100k_reads(tmp_path):
+    """The reference's own main.cpp over the drop-in (one GPU call per sequence per k at
+    src/main.cpp:79 and :143-144, batched sparse_chain) against the skq CLI, 200 transcripts x
+    100k 150-bp reads, k = 31: phase times from the reference's progress lines."""
+    tx = synth.transcriptome(200, seed=81)
+    fa, fq = tmp_path / "t.fa", tmp_path / "r.fq"
+    tx.write_fasta(fa)
+    n = 100_000
+    bases, _, _ = synth.reads(tx, n, 150, seed=82)
+    with open(fq, "wb") as f:
+        f.write(synth.fastq_bytes(bases, 150).tobytes())
+    rows = {}
+    for name, exe in (("ref_cli_skq", CLIS[0]), ("skq", SKQ)):
+        idx, csv = tmp_path / (name + ".idx"), tmp_path / (name + ".csv")
+        li, ti = _timed(exe, "-k", "31", "-o", "index", fa, idx)
+        lq, tq = _timed(exe, "-o", "quant", idx, fq, csv)
+        rows[name] = {r[0]: (float(r[1]), float(r[2])) for r in _rows(csv)}
+        print("%s: index %.2fs, quant %.2fs; quant progress: %s" % (
+            name, ti, tq, "; ".join("%.2fs %s" % (t, l[:40]) for t, l in lq)))
+    assert set(rows["ref_cli_skq"]) == set(rows["skq"])
