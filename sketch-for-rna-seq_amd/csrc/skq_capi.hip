@@ -439,9 +439,9 @@ int build_compact(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
 // transcripts are sketched in position order (the index's own hashing: skq::sketch_positions);
 // every retained k-mer's successors within CHAIN_HOPS retained positions in any transcript are
 // candidates for its entry, nearest first (ties: smaller key). An entry takes the key's own record,
-// then successors while they fit: at most CHN_KEYS records, CHN_TIDS distinct transcripts over the
-// whole entry (their ids stored once) and CHN_CLASSES distinct postings lists (each an 8-bit mask
-// over those ids); a successor that does not fit is skipped, a later one may. A record names its
+// then successors while they fit: at most CHN_KEYS records and CHN_TIDS distinct transcripts over
+// the whole entry (their ids stored once, each with the set of records whose list holds it); a
+// successor that does not fit is skipped, a later one may. A record names its
 // key's WHOLE postings list (the index's own lists[]), so whatever it settles is exactly what a
 // lookup of that key returns. The entries (one per present key) are built on the host and
 // scattered on the device into a table of 128-B entries for every possible key up to the largest
@@ -456,14 +456,14 @@ __global__ void k_chain_scatter(uint4* tab, const uint32_t* keys, const uint4* e
 }
 
 // one key's entry: its own record (a list of <= CHN_TIDS transcripts), then successors in order
-// while they fit (records, distinct transcripts, distinct lists); returns the successors taken
+// while they fit (records, distinct transcripts); returns the successors taken
 static uint32_t chain_entry(uint32_t* e, uint32_t key, uint32_t off, const std::vector<uint32_t>& lists,
                             const uint32_t* sk, const uint32_t* so, size_t ns) {
     if (lists[off] > skq::CHN_TIDS) {
-        e[0] = skq::CHN_LONG;
+        e[skq::CHN_W_KEY] = skq::CHN_LONG;
         return 0;
     }
-    uint32_t tids[skq::CHN_TIDS], nt = 0, cls[skq::CHN_CLASSES], nc = 0, nr = 0;
+    uint32_t tids[skq::CHN_TIDS], sets[skq::CHN_TIDS] = {}, nt = 0, nr = 0;
     auto add = [&](uint32_t k2, uint32_t o2) -> bool {
         const uint32_t n = lists[o2];
         if (n == 0 || n > skq::CHN_TIDS) return false;
@@ -479,23 +479,20 @@ static uint32_t chain_entry(uint32_t* e, uint32_t key, uint32_t off, const std::
             }
             mk |= 1u << s;
         }
-        uint32_t c = 0;
-        while (c < nc && cls[c] != mk) ++c;
-        if (c == nc) {
-            if (nc == skq::CHN_CLASSES) return false;
-            cls[nc++] = mk;
-        }
         std::copy(tt, tt + ntt, tids);
         nt = ntt;
-        e[skq::CHN_W_KEY + nr++] = ~(k2 << 4 | c);
+        for (uint32_t s = 0; s < nt; ++s)
+            if ((mk >> s) & 1u) sets[s] |= 1u << nr;
+        e[skq::CHN_W_KEY + nr++] = k2 ^ skq::CHN_KEY_LIMIT;
         return true;
     };
     add(key, off);  // (always fits)
     uint32_t taken = 0;
     for (size_t q = 0; q < ns && nr < skq::CHN_KEYS; ++q) taken += add(sk[q], so[q]) ? 1u : 0u;
-    e[0] = nr;
-    for (uint32_t c = 0; c < nc; ++c) e[skq::CHN_W_MASK + c / 4] |= cls[c] << (8 * (c & 3));
-    for (uint32_t t = 0; t < nt; ++t) e[skq::CHN_W_TID + t] = tids[t];
+    for (uint32_t t = 0; t < nt; ++t) {
+        e[skq::CHN_W_SET + t / 2] |= sets[t] << (16 * (t & 1));
+        e[skq::CHN_W_TID + t] = tids[t];
+    }
     return taken;
 }
 
@@ -503,7 +500,7 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
                 const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
                 uint32_t nseq, uint32_t threshold) {
     const uint64_t m = keys.size();
-    if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key << 4)
+    if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key ^ CHN_KEY_LIMIT)
     const uint64_t len = (uint64_t)keys.back() + 1;
     // 128 B per possible key, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
     uint64_t budget = 65536ull << 20;
@@ -1323,7 +1320,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
         return rc;
-    // (chained records hold key << 4 and decode unused slots as 0x0FFFFFFF: reads sketched at a
+    // (chained records decode unused slots as the key 0x0FFFFFFF: reads sketched at a
     // threshold that reaches that far use the wide entries alone)
     if (sp.threshold >= skq::CHN_KEY_LIMIT) {
         cp.chain = nullptr;

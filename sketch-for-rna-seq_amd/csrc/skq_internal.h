@@ -226,17 +226,17 @@ uint64_t session_max_reads(const skq_session* s);
 // rules: windows holding a byte outside ACGTUacgtu skipped) (skq_tables.cpp)
 void sketch_positions(const uint8_t* s, uint64_t len, uint32_t k, uint32_t thr, std::vector<uint32_t>& out);
 // Chained entries (ChainParams::chain), CHAIN_WORDS words per possible key:
-//   word 0            header: records (0..CHN_KEYS); CHN_LONG: the key's own list holds more than
-//                     CHN_TIDS transcripts (the entry holds nothing: lookups go to the wide entries);
-//                     an all-zero entry: no such key
-//   words 1-2         class masks: class c (0..7) = byte c of the pair, a set over the entry's ids
-//   words 3-10        the entry's transcript ids (up to CHN_TIDS, each once)
-//   words 11-26       records: ~(key << 4 | class), the entry's own key first (unused: 0, which
-//                     decodes to the key 0x0FFFFFFF no retained hash reaches: keys < CHN_KEY_LIMIT)
-constexpr uint32_t CHAIN_WORDS = 32;  // chained entry: 128 B
-constexpr uint32_t CHN_KEYS = 16, CHN_TIDS = 8, CHN_CLASSES = 8;
-constexpr uint32_t CHN_W_MASK = 1, CHN_W_TID = 3, CHN_W_KEY = 11;
-constexpr uint32_t CHN_LONG = 0x80000000u;
+//   words 0-3         per entry id q (0..7): the records whose list holds it, a 16-bit set in half
+//                     q & 1 of word q >> 1 (a record's count is its key's; an id's is the records')
+//   words 4-11        the entry's transcript ids (up to CHN_TIDS, each once)
+//   words 12-27       records: key ^ CHN_KEY_LIMIT, the entry's own key first (unused: 0, which
+//                     decodes to the key 0x0FFFFFFF no retained hash reaches: keys < CHN_KEY_LIMIT).
+//                     Word 12 CHN_LONG: the key's own list holds more than CHN_TIDS transcripts (the
+//                     entry holds nothing: lookups go to the wide entries); word 12 zero: no such key
+constexpr uint32_t CHAIN_WORDS = 32;  // chained entry: 128 B (words 28-31 unused: 7 of its 8 pieces read)
+constexpr uint32_t CHN_KEYS = 16, CHN_TIDS = 8;
+constexpr uint32_t CHN_W_SET = 0, CHN_W_TID = 4, CHN_W_KEY = 12;
+constexpr uint32_t CHN_LONG = 0x80000000u;  // (decodes to 0x8FFFFFFF: neither a hash nor the sort's padding)
 constexpr uint32_t CHN_KEY_LIMIT = 0x0FFFFFFFu;
 // host: ascending sort with threads (skq_tables.cpp)
 void parallel_sort_u64(std::vector<uint64_t>& v, int threads);

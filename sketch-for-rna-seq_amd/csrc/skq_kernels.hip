@@ -55,23 +55,63 @@ __device__ __forceinline__ void cswap(T& a, T& b) {
     b = hi;
 }
 
-// ascending bitonic sort of a register array (fully unrolled: every index is a constant)
+// Sorting networks of the fewest known comparators (each a min and a max, both half-rate VALU:
+// the bitonic network of 16 has 80, this one 60), entries lo | hi << 8; every one checked on all
+// 0-1 inputs (tests/test_sort_networks.py)
+constexpr uint16_t kNet8[19] = {0 | 2 << 8, 1 | 3 << 8, 4 | 6 << 8, 5 | 7 << 8, 0 | 4 << 8, 1 | 5 << 8, 2 | 6 << 8, 3 | 7 << 8, 0 | 1 << 8, 2 | 3 << 8, 4 | 5 << 8, 6 | 7 << 8, 2 | 4 << 8, 3 | 5 << 8, 1 | 4 << 8, 3 | 6 << 8, 1 | 2 << 8, 3 | 4 << 8, 5 | 6 << 8};
+constexpr uint16_t kNet12[39] = {0 | 8 << 8, 1 | 7 << 8, 2 | 6 << 8, 3 | 11 << 8, 4 | 10 << 8, 5 | 9 << 8, 0 | 1 << 8, 2 | 5 << 8, 3 | 4 << 8, 6 | 9 << 8, 7 | 8 << 8, 10 | 11 << 8, 0 | 2 << 8, 1 | 6 << 8, 5 | 10 << 8, 9 | 11 << 8, 0 | 3 << 8, 1 | 2 << 8, 4 | 6 << 8, 5 | 7 << 8, 8 | 11 << 8, 9 | 10 << 8, 1 | 4 << 8, 3 | 5 << 8, 6 | 8 << 8, 7 | 10 << 8, 1 | 3 << 8, 2 | 5 << 8, 6 | 9 << 8, 8 | 10 << 8, 2 | 3 << 8, 4 | 5 << 8, 6 | 7 << 8, 8 | 9 << 8, 4 | 6 << 8, 5 | 7 << 8, 3 | 4 << 8, 5 | 6 << 8, 7 | 8 << 8};
+constexpr uint16_t kNet16[60] = {0 | 13 << 8, 1 | 12 << 8, 2 | 15 << 8, 3 | 14 << 8, 4 | 8 << 8, 5 | 6 << 8, 7 | 11 << 8, 9 | 10 << 8, 0 | 5 << 8, 1 | 7 << 8, 2 | 9 << 8, 3 | 4 << 8, 6 | 13 << 8, 8 | 14 << 8, 10 | 15 << 8, 11 | 12 << 8, 0 | 1 << 8, 2 | 3 << 8, 4 | 5 << 8, 6 | 8 << 8, 7 | 9 << 8, 10 | 11 << 8, 12 | 13 << 8, 14 | 15 << 8, 0 | 2 << 8, 1 | 3 << 8, 4 | 10 << 8, 5 | 11 << 8, 6 | 7 << 8, 8 | 9 << 8, 12 | 14 << 8, 13 | 15 << 8, 1 | 2 << 8, 3 | 12 << 8, 4 | 6 << 8, 5 | 7 << 8, 8 | 10 << 8, 9 | 11 << 8, 13 | 14 << 8, 1 | 4 << 8, 2 | 6 << 8, 5 | 8 << 8, 7 | 10 << 8, 9 | 13 << 8, 11 | 14 << 8, 2 | 4 << 8, 3 | 6 << 8, 9 | 12 << 8, 11 | 13 << 8, 3 | 5 << 8, 6 | 8 << 8, 7 | 9 << 8, 10 | 12 << 8, 3 | 4 << 8, 5 | 6 << 8, 7 | 8 << 8, 9 | 10 << 8, 11 | 12 << 8, 6 | 7 << 8, 8 | 9 << 8};
+
+// ascending sort of a[0..M) by the network above (fully unrolled: every index is a constant)
+template <int M, typename T>
+__device__ __forceinline__ void net_sort(T* a) {
+    static_assert(M == 8 || M == 12 || M == 16, "networks of 8, 12 and 16");
+    static_for<M == 8 ? 19 : (M == 12 ? 39 : 60)>([&](auto c) {
+        constexpr uint16_t e = M == 8 ? kNet8[c] : (M == 12 ? kNet12[c] : kNet16[c]);
+        cswap(a[e & 255], a[e >> 8]);
+    });
+}
+
+// ascending sort of a register array: the networks above at 8 and 16, else bitonic (fully
+// unrolled: every index is a constant)
 template <int N, typename T>
 __device__ __forceinline__ void bitonic_sort(T (&a)[N]) {
+    if constexpr (N == 8 || N == 16) {
+        net_sort<N>(a);
+    } else {
 #pragma unroll
-    for (int k = 2; k <= N; k <<= 1) {
+        for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
 #pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    if ((i & k) == 0) cswap(a[i], a[l]);
-                    else cswap(a[l], a[i]);
+                for (int i = 0; i < N; ++i) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        if ((i & k) == 0) cswap(a[i], a[l]);
+                        else cswap(a[l], a[i]);
+                    }
                 }
             }
         }
     }
+}
+
+// ascending sort of a[0..N) whose entries from n on are padding no smaller than any before
+// (n <= N per lane): the active lanes' longest prefix picks the network (a uniform branch;
+// cfg3: about 6 retained windows per read, the wave's longest mostly 9-13)
+template <int N, typename T>
+__device__ __forceinline__ void sort_prefix(T (&a)[N], uint32_t n) {
+    if constexpr (N == 16) {
+        if (!__any(n > 8)) {
+            net_sort<8>(a);
+            return;
+        }
+        if (!__any(n > 12)) {
+            net_sort<12>(a);
+            return;
+        }
+    }
+    bitonic_sort<N>(a);
 }
 
 // ascending bitonic sort of a[0..n) in LDS by the whole workgroup (n a power of two)
@@ -429,7 +469,7 @@ __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
             uint32_t v[HCAP];
 #pragma unroll
             for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
-            bitonic_sort<HCAP>(v);
+            sort_prefix<HCAP>(v, nraw);
             // SoA layout: value j of (read r, k slot i) at hashes[(i*hcap + j)*n + r], so the
             // wave's stores of one j are contiguous
             uint32_t* out = p.hashes + (uint64_t)i * p.hcap * p.n + r;
@@ -1945,15 +1985,22 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
     if (bin) bin_candidates(p, t, blockIdx.x, nc, key, s_bc, s_tabs);
 }
 
-// k_map1 LDS: per wave max(staged codes + bad bits, one pass of the entry list: MAP_P hashes and
-// their owning lanes)
-// (the per-chunk bad bits sit in row 0 of the wave's raw columns, dead until hashing starts; the
-// binning counts in wave 0's region, dead once every wave has counted; HCAP + 2 raw rows, the
-// last one the sink of windows past the capacity)
+// k_map1 LDS: static, at LDS address 0, the HCAP + 2 raw rows (Map1Static: row 0 the sink of
+// windows past the capacity, then the retained windows from the last row down, so a row's LDS
+// address is the hashing loop's own counter) and the roll terms; dynamic, the binning's bucket
+// counters, then per wave max(staged codes, one pass of the entry list: MAP_P hashes and their
+// owning lanes)
+// (the per-chunk bad bits sit in the wave's columns of the last raw row, dead until hashing starts)
 // (MAP_P: 8 per read; at 384 — the mean of cfg3's ~6.0 distinct hashes per read x 64 — half of
 // the waves listed their hashes in two passes, the second one a dependent reload and gather
 // round; profiles/r3_map1_writes.log)
 constexpr uint32_t MAP_P = 512;
+constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
+template <int HCAP>
+struct Map1Static {
+    uint32_t raw[(HCAP + 2) * WG];  // (first: at LDS address 0, the kernel's only static LDS)
+    uint2 tab[16 + 4];              // the roll terms, then the seeds
+};
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
 // lanes (u8; compact tables: u32 slot | lane << 26) (tab: 0 wide, 2 compact, 3 chained over
 // wide). (Round 3 measured 6 workgroups per CU against 5 with the list packed
@@ -1974,9 +2021,10 @@ inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
 size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
     p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
     p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
-    // (+ the binning epilogue's bucket counters, their own so they are zeroed up front)
-    return sketch_tab_bytes(1) + (WG / 64) * (size_t)p.map_wave_bytes + ((size_t)hcap + 2) * WG * 4 +
-           (((size_t)WG + 1) * 4 + 15) / 16 * 16;
+    // (the binning epilogue's bucket counters first, their own so they are zeroed up front; the
+    // raw rows are static)
+    (void)hcap;
+    return MAP1_BC_BYTES + (WG / 64) * (size_t)p.map_wave_bytes;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -2016,15 +2064,18 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
     const size_t wave_bytes = p.map_wave_bytes;
-    // (the roll terms in static LDS: their addresses fold into the reads' offsets)
-    __shared__ uint2 s_tab_st[16 + 4];
-    uint2* s_tab = s_tab_st;
+    // (static LDS: the raw rows' and the roll terms' addresses fold into the instructions' offsets)
+    __shared__ __attribute__((aligned(16))) Map1Static<HCAP> s_st;
+    uint2* s_tab = s_st.tab;
     const uint2* s_seed = s_tab + 16;
-    unsigned char* s_wave = smem + sketch_tab_bytes(1) + wv * wave_bytes;
+    uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem);  // the binning's bucket counters (map1_layout)
+    unsigned char* s_wave = smem + MAP1_BC_BYTES + wv * wave_bytes;
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
-    uint32_t* s_raw = reinterpret_cast<uint32_t*>(smem + sketch_tab_bytes(1) + (WG / 64) * wave_bytes);
-    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + wv * 64);  // (row 0 of the wave's columns)
-    uint32_t* s_bc = s_raw + (HCAP + 2) * WG;  // the binning's bucket counters (map1_layout)
+    // raw rows: row 0 the sink, retained window i of the read (position order) in row HCAP + 1 - i;
+    // after the hashing, rows 1..TS hold the count tables (s_rows)
+    uint32_t* s_raw = s_st.raw;
+    uint32_t* s_rows = s_raw + WG;
+    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + (HCAP + 1) * WG + wv * 64);  // (the wave's columns, last row)
     const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
     for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot ks's roll terms, then the seeds
         const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
@@ -2179,8 +2230,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     if (b + j < k) roll33b(hlo, hhi, e[j]);
             }
         }
-        uint32_t* raw = s_raw + tid;
-        raw[0] = hlo;
+        s_raw[(HCAP + 1) * WG + tid] = hlo;
         const uint32_t nw = L - k + 1;
         const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
         // windows 1..nw-1, 16 per block (in-base at w + k - 1, out-base at w - 1). A window's roll
@@ -2188,16 +2238,18 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // shifted up by 2 and B the out-bases', the nibbles of ce = A:B (even windows) and
         // co = B:A (odd windows) hold (in, out) pairs, so a term's offset is one shift and one
         // mask. Every window's value is stored at the lane's write row, which a retained window
-        // (src/sketch.cpp:33-35) advances: rows 0..HCAP-1 hold the retained windows in order, row
-        // HCAP the next and row HCAP + 1 any past it (the read then goes slow). The row is kept as
-        // its distance d below row HCAP + 1, advanced by a saturating subtract, so no compare or
-        // clamp sits in the loop: for T < 2^31 the test h <= T is bit 31 of ~((T - h) | h). Every
-        // operation in the loop but the rotate is a full-rate VALU form (tools/micro/valu_mix:
-        // compares, min/max and the three-operand integer forms issue at half rate).
-        const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)raw;
+        // (src/sketch.cpp:33-35) moves down a row: retained window i in row HCAP + 1 - i, row 1 the
+        // (HCAP + 1)-th (the read then goes slow), row 0 the sink of any past it. The lane's slot is
+        // kept as its LDS offset d from the raw rows (at LDS address 0: the offset is the store's
+        // address), moved by a saturating subtract, so no compare or clamp sits in the loop: a lane
+        // past row 0 lands at offset 0, lane 0's sink slot, which nothing reads. For T < 2^31 the
+        // test h <= T is bit 31 of ~((T - h) | h). Every operation in the loop but the rotate is a
+        // full-rate VALU form (tools/micro/valu_mix: compares, min/max and the three-operand
+        // integer forms issue at half rate).
+        const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)s_raw;
         constexpr uint32_t ROW = (uint32_t)WG * 4u;
-        const uint32_t rtop = rbase + (uint32_t)(HCAP + 1) * ROW;
-        uint32_t d = (uint32_t)(HCAP + 1) * ROW - (hlo <= T ? ROW : 0u);
+        const uint32_t d0 = (uint32_t)tid * 4u + (uint32_t)(HCAP + 1) * ROW;
+        uint32_t d = d0 - (hlo <= T ? ROW : 0u);
         const unsigned char* tabb = reinterpret_cast<const unsigned char*>(s_tab);
         auto block = [&](uint32_t w0, uint32_t jn, auto full, auto small) {
             const uint32_t A = codes16(qin + w0 - 1), B = codes16(qout + w0 - 1);
@@ -2216,8 +2268,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 roll33b(hlo, hhi, e[j]);
-                *(__attribute__((address_space(3))) uint32_t*)(size_t)(rtop - d) = hlo;
-                uint32_t adv = decltype(small)::value ? ((~((T - hlo) | hlo)) >> 21) & ROW : (hlo <= T ? ROW : 0u);
+                *(__attribute__((address_space(3))) uint32_t*)(size_t)(rbase + d) = hlo;
+                // (small: ~((T - h) | h) & 2^31 as one bitop3, then the shift down to ROW)
+                uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - hlo, hlo, 0x80000000u, 0x02) >> 21
+                                                      : (hlo <= T ? ROW : 0u);
                 if (!decltype(full)::value) adv &= (uint32_t)((int)(j - (int)jn) >> 31);  // (windows past the read)
                 d = __builtin_elementwise_sub_sat(d, adv);
             }
@@ -2230,10 +2284,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             for (; w0 + 16 <= nw; w0 += 16) block(w0, 16u, std::true_type{}, std::false_type{});
             if (w0 < nw) block(w0, nw - w0, std::false_type{}, std::false_type{});
         }
-        nraw = (rtop - d - rbase) / ROW;  // (HCAP + 1: more than HCAP retained)
+        nraw = (d0 - d) / ROW;  // (HCAP + 1: more than HCAP retained)
     }
     if constexpr (CHN) {
-        cq = s_raw[tid];  // (raw row 0: the first retained window)
+        cq = s_raw[(HCAP + 1) * WG + tid];  // (the first retained window)
         has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len;
         // words 0-26 of the entry (27-31 unused)
         const uint4* ent = reinterpret_cast<const uint4*>(cp.chain) + (has_q ? (uint64_t)cq * 8 : 0ull);
@@ -2257,8 +2311,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         } else {
             nraw_out = nraw;
 #pragma unroll
-            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[j * WG + tid] : 0xFFFFFFFFu;
-            bitonic_sort<HCAP>(v);
+            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[(HCAP + 1 - j) * WG + tid] : 0xFFFFFFFFu;
+            sort_prefix<HCAP>(v, nraw);
             uint32_t* out = p.hashes + (uint64_t)ks * p.hcap * p.n + r;
             uint32_t m = 0;
 #pragma unroll
@@ -2321,13 +2375,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint64_t keepm_all = keepm;  // the read's distinct retained hashes (as written out)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 #pragma unroll
-    for (int sl = 0; sl < TS; ++sl) s_raw[sl * WG + tid] = EMPTY;
+    for (int sl = 0; sl < TS; ++sl) s_rows[sl * WG + tid] = EMPTY;
     uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + p.map_flag_at);  // per read: > TS transcripts
     s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
     uint8_t* s_own = reinterpret_cast<uint8_t*>(s_wave) + MAP_P * 4;
     uint32_t* s_x = reinterpret_cast<uint32_t*>(s_wave + MAP_P * 4);  // compact: slot | lane << 26
-    uint32_t* colbase = s_raw + wv * 64;
+    uint32_t* colbase = s_rows + wv * 64;
     const uint32_t* wd = cp.wdir[ks];
     const uint64_t wlen = cp.wdir_len[ks];
     const uint16_t* cpil = cp.wpil[ks];
@@ -2362,11 +2416,11 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     if constexpr (CHN) {
         // chained tables, one request per read (ChainParams::chain, layout skq_internal.h CHN_*):
         // the lane matches its own retained hashes (v, registers) against the records of its
-        // query's entry (ce, requested after the hashing loop), counts each matched record's
-        // transcript set into per-transcript byte counters over the entry's ids, and inserts those
-        // into its own count table (no other lane writes it before the entry list below). What no
-        // record holds goes through the entry list as before. An all-zero entry (no such key, or a
-        // query past the table) settles the query itself: no postings.
+        // query's entry (ce, requested after the hashing loop), counts each of the entry's ids as
+        // the matched records whose list holds it (a popcount over the id's record set), and inserts
+        // those into its own count table (no other lane writes it before the entry list below).
+        // What no record holds goes through the entry list as before. An entry with no records (no
+        // such key, or a query past the table) settles the query itself: no postings.
         if (cp.ablate & 64u) {  // (the asm loads above: wait for them before their registers are read)
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
             u32x4 x[7];
@@ -2388,10 +2442,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             w[4 * u + 2] = inb ? ce[u].z : 0u;
             w[4 * u + 3] = inb ? ce[u].w : 0u;
         }
-        const bool absent = has_q && w[0] == 0u;
+        const bool absent = has_q && w[CHN_W_KEY] == 0u;
         uint32_t kh[CHN_KEYS];
 #pragma unroll
-        for (int i = 0; i < (int)CHN_KEYS; ++i) kh[i] = (~w[CHN_W_KEY + i]) >> 4;  // (unused: 0x0FFFFFFF)
+        for (int i = 0; i < (int)CHN_KEYS; ++i) kh[i] = w[CHN_W_KEY + i] ^ CHN_KEY_LIMIT;  // (unused: 0x0FFFFFFF)
         kh[0] = absent ? cq : kh[0];
         bool hk[CHN_KEYS];
 #pragma unroll
@@ -2409,16 +2463,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
             hitv |= hj ? (1u << j) : 0u;
         }
-        // per matched record: its class's transcript set, one byte counter per entry id
-        uint32_t acc0 = 0, acc1 = 0;
+        // the matched records as a set; an id's count is the number of them whose list holds it
+        uint32_t hm = 0;
 #pragma unroll
-        for (int i = 0; i < (int)CHN_KEYS; ++i) {
-            const uint32_t c = (~w[CHN_W_KEY + i]) & 7u;
-            const uint32_t mw = (c & 4u) ? w[CHN_W_MASK + 1] : w[CHN_W_MASK];
-            const uint32_t mk = __builtin_amdgcn_ubfe(mw, (c & 3u) * 8u, 8u);
-            acc0 += hk[i] ? ((mk & 15u) * 0x00204081u) & 0x01010101u : 0u;
-            acc1 += hk[i] ? ((mk >> 4) * 0x00204081u) & 0x01010101u : 0u;
-        }
+        for (int i = 0; i < (int)CHN_KEYS; ++i) hm |= hk[i] ? 1u << i : 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2428,7 +2476,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         uint32_t olds[CHN_TIDS], xs[CHN_TIDS], cs[CHN_TIDS];
 #pragma unroll
         for (int q = 0; q < (int)CHN_TIDS; ++q) {
-            cs[q] = ((q < 4 ? acc0 : acc1) >> (8 * (q & 3))) & 0xFFu;
+            cs[q] = (uint32_t)__builtin_popcount(hm & (w[CHN_W_SET + q / 2] >> (16 * (q & 1))));
             xs[q] = w[CHN_W_TID + q];
             const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
             olds[q] = cs[q] ? atomicCAS(colbase + sl * WG + ((lane + sl) & 63u), EMPTY, (xs[q] << 8) | cs[q]) : EMPTY;
