@@ -76,13 +76,14 @@ struct skq_index {
     const uint16_t* wpil[SKQ_MAX_K] = {};
     uint32_t wnb[SKQ_MAX_K] = {}, wseed[SKQ_MAX_K] = {};
     uint64_t dir_bytes = 0;
-    // chained tables (one k slot; ChainParams::chain): a 128-B entry per possible key up to the
+    // chained tables (per k slot; ChainParams::chain): a 128-B entry per possible key up to the
     // largest, carrying the key's postings list and those of the keys that follow it in the
     // transcripts; k_map1 then settles a read with ~1.5 entry requests instead of one per hash
-    uint4* d_chain = nullptr;
-    uint64_t chain_len = 0;
+    uint4* d_chain[SKQ_MAX_K] = {};
+    uint64_t chain_len[SKQ_MAX_K] = {};
     uint64_t chain_bytes = 0;
-    double chain_succ = 0;  // mean successor records per entry (stats)
+    double chain_succ = 0;  // mean successor records per entry over the slots' tables (stats)
+    uint32_t chain_slots = 0;
     // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 5 = compact tables
     // (4 was the block tables, retired in round 3: compact tables are smaller and faster)
     int mode = 0;
@@ -496,7 +497,7 @@ static uint32_t chain_entry(uint32_t* e, uint32_t key, uint32_t off, const std::
     return taken;
 }
 
-int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
+int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
                 const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
                 uint32_t nseq, uint32_t threshold) {
     const uint64_t m = keys.size();
@@ -587,29 +588,31 @@ int build_chain(skq_index* ix, const std::vector<uint32_t>& keys, const std::vec
         if (!built[x]) chain_entry(ent.data() + x * skq::CHAIN_WORDS, keys[x], vals[x], lists, nullptr, nullptr, 0);
     uint32_t* dk = nullptr;
     uint4* de = nullptr;
-    if (dev_alloc(&ix->d_chain, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
+    uint4*& dch = ix->d_chain[slot];
+    if (dev_alloc(&dch, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
         dev_free(dk);
         dev_free(de);
-        dev_free(ix->d_chain);
+        dev_free(dch);
         return fail(-3, "chained table allocation failed");
     }
     hipStream_t st = nullptr;
-    const bool ok = hipMemsetAsync(ix->d_chain, 0, len * 128, st) == hipSuccess &&
+    const bool ok = hipMemsetAsync(dch, 0, len * 128, st) == hipSuccess &&
                     hipMemcpy(dk, keys.data(), m * 4, hipMemcpyHostToDevice) == hipSuccess &&
                     hipMemcpy(de, ent.data(), m * 128, hipMemcpyHostToDevice) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(k_chain_scatter, dim3((unsigned)((m * 8 + 255) / 256)), dim3(256), 0, st, ix->d_chain, dk, de, m);
+        hipLaunchKernelGGL(k_chain_scatter, dim3((unsigned)((m * 8 + 255) / 256)), dim3(256), 0, st, dch, dk, de, m);
     }
     const bool done = ok && hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
     dev_free(dk);
     dev_free(de);
     if (!done) {
-        dev_free(ix->d_chain);
+        dev_free(dch);
         return fail(-3, "chained table build failed");
     }
-    ix->chain_len = len;
-    ix->chain_bytes = len * 128;
-    ix->chain_succ = (double)nsucc.load() / (double)m;
+    ix->chain_len[slot] = len;
+    ix->chain_bytes += len * 128;
+    ix->chain_succ = (ix->chain_succ * ix->chain_slots + (double)nsucc.load() / (double)m) / (ix->chain_slots + 1);
+    ++ix->chain_slots;
     return 0;
 }
 
@@ -845,19 +848,20 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
         skq_index_free(ix);
         return rc2;
     }
-    // chained tables (one k slot, ids within 22 bits, transcripts given): built only with SKQ_CHAIN
-    // = 1 (A/B at cfg3: 48 % fewer fabric read requests, 2 % faster map, 27.5 GB)
-    if (seqs && seq_offs && nk == 1 && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
+    // chained tables (per k slot, ids within 22 bits, transcripts given): built only with
+    // SKQ_CHAIN = 1; a slot whose table does not fit keeps the wide entries alone
+    if (seqs && seq_offs && nk <= (uint32_t)skq::NK_FAST && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
         ix->mode == 3) {  // (the entry list behind the chain step gathers wide entries)
         const char* e = std::getenv("SKQ_CHAIN");
         const int cm = e ? std::atoi(e) : 0;
         if (cm == 1)
-            for (uint32_t t = 0; t < ntables; ++t)
-                if (tables[t].k == ks[0])
-                    if (int rc2 = build_chain(ix, dkeys[t], dvals[t], lists, ks[0], seqs, seq_offs, nseq, threshold)) {
-                        skq_index_free(ix);
-                        return rc2;
-                    }
+            for (uint32_t i = 0; i < nk; ++i)
+                for (uint32_t t = 0; t < ntables; ++t)
+                    if (tables[t].k == ks[i])
+                        if (int rc2 = build_chain(ix, i, dkeys[t], dvals[t], lists, ks[i], seqs, seq_offs, nseq, threshold)) {
+                            skq_index_free(ix);
+                            return rc2;
+                        }
     }
     *out = ix;
     return 0;
@@ -883,7 +887,7 @@ int skq_index_free(skq_index* ix) {
     for (auto& d : ix->d_wpil_t) dev_free(d);
     for (auto& d : ix->d_rank_t) dev_free(d);
     for (auto& d : ix->d_rovf_t) dev_free(d);
-    dev_free(ix->d_chain);
+    for (auto& d : ix->d_chain) dev_free(d);
     dev_free(ix->d_buckets);
     dev_free(ix->d_lists);
     dev_free(ix->d_rolltab);
@@ -922,7 +926,7 @@ int skq_session_slow_counts(skq_session* s, uint32_t* counts) {
 }
 
 int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? ix->mode : 0; }
-double skq_index_chained(const skq_index* ix) { return ix && ix->d_chain ? 1.0 + ix->chain_succ : 0.0; }
+double skq_index_chained(const skq_index* ix) { return ix && ix->chain_slots ? 1.0 + ix->chain_succ : 0.0; }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
     if (!ix || !out) return fail(-1, "null argument");
@@ -1231,8 +1235,10 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
             p.wseed[i] = ix->wseed[i];
         }
     }
-    p.chain = reinterpret_cast<const uint32_t*>(ix->d_chain);
-    p.chain_len = ix->chain_len;
+    for (uint32_t i = 0; i < SKQ_MAX_K; ++i) {
+        p.chain[i] = reinterpret_cast<const uint32_t*>(ix->d_chain[i]);
+        p.chain_len[i] = ix->chain_len[i];
+    }
     p.stamps = s->stamps;
     if (const char* e = std::getenv("SKQ_ABLATE")) p.ablate = (uint32_t)std::strtoul(e, nullptr, 0);
     p.ntx = ix->ntx;
@@ -1322,10 +1328,11 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         return rc;
     // (chained records decode unused slots as the key 0x0FFFFFFF: reads sketched at a
     // threshold that reaches that far use the wide entries alone)
-    if (sp.threshold >= skq::CHN_KEY_LIMIT) {
-        cp.chain = nullptr;
-        cp.chain_len = 0;
-    }
+    if (sp.threshold >= skq::CHN_KEY_LIMIT)
+        for (uint32_t i = 0; i < SKQ_MAX_K; ++i) {
+            cp.chain[i] = nullptr;
+            cp.chain_len[i] = 0;
+        }
     // candidates packed too, unless the totals would be binned from the padded rows (k_bin)
     s->cand_packed = s->hash_packed && (!accumulate || cp.slow_totals);
     cp.cpack = s->cand_packed ? 1u : 0u;

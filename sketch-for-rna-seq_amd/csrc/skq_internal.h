@@ -212,8 +212,8 @@ struct ChainParams {
     // keys that follow it along the transcripts (nearest first), each naming the key's WHOLE
     // postings list as a set of the entry's transcripts, so one 128-B request settles a run of a
     // read's retained hashes
-    const uint32_t* chain;
-    uint64_t chain_len;
+    const uint32_t* chain[SKQ_MAX_K];  // per k slot (null: none for that slot)
+    uint64_t chain_len[SKQ_MAX_K];
 };
 
 // records the message returned by skq_last_error(); returns code (skq_capi.hip)

@@ -2054,7 +2054,6 @@ template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false>
 __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     constexpr bool CMP = TAB == 2, CHN = TAB == 3;
     static_assert(PASS || !FINAL, "the final pass is a pass");
-    static_assert(!(CHN && PASS), "chained tables serve one k slot");
     static_assert(!CHN || HCAP <= 32, "hit bits");
     const uint32_t ks = PASS ? p.kslot : 0u;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
@@ -2288,9 +2287,9 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     }
     if constexpr (CHN) {
         cq = s_raw[(HCAP + 1) * WG + tid];  // (the first retained window)
-        has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len;
+        has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len[ks];
         // words 0-26 of the entry (27-31 unused)
-        const uint4* ent = reinterpret_cast<const uint4*>(cp.chain) + (has_q ? (uint64_t)cq * 8 : 0ull);
+        const uint4* ent = reinterpret_cast<const uint4*>(cp.chain[ks]) + (has_q ? (uint64_t)cq * 8 : 0ull);
         if (cp.ablate & 64u) {  // (development A/B: the entry's loads with sc0, past the L1)
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -2434,7 +2433,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             for (int u = 0; u < 7; ++u) ce[u] = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
         }
         uint32_t w[28];
-        const bool inb = has_q && cq < cp.chain_len;  // (else the lane read entry 0 and drops it)
+        const bool inb = has_q && cq < cp.chain_len[ks];  // (else the lane read entry 0 and drops it)
 #pragma unroll
         for (int u = 0; u < 7; ++u) {
             w[4 * u] = inb ? ce[u].x : 0u;
@@ -3817,7 +3816,7 @@ static void map1_report_occupancy(const void* kern, size_t lds) {
 int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     if (p0.n == 0) return 0;
     const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
-    const bool chn = cp.chain != nullptr;
+    const bool chn = cp.chain[0] != nullptr;
     SketchParams p = p0;
     if (!chn && cp.wide != 1 && cp.wide != 3) return -4;
     const size_t lds = map1_layout(p, chn ? 3 : cp.wide == 3 ? 2 : 0, p.hcap);
@@ -3845,20 +3844,26 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
 
 int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
     if (p0.n == 0) return 0;
-    if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap) return -4;
+    if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.kslot >= SKQ_MAX_K) return -4;
     const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
     SketchParams p = p0;
-    const size_t lds = map1_layout(p, cp.wide == 3 ? 2 : 0, cap);
+    // (the pass's k slot has chained tables: TAB 3)
+    const int tab = cp.chain[p0.kslot] ? 3 : cp.wide == 3 ? 2 : 0;
+    const size_t lds = map1_layout(p, tab, cap);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    switch (cap * 8 + (cp.wide == 3 ? 2 : 0) + (final_pass ? 1 : 0)) {
+    switch (cap * 8 + tab + (final_pass ? 1 : 0) * 4) {
+    case 131: hipLaunchKernelGGL((k_map1<16, 4, 3, true, false>), grid, dim3(WG), lds, st, p, cp); break;
+    case 135: hipLaunchKernelGGL((k_map1<16, 4, 3, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 259: hipLaunchKernelGGL((k_map1<32, 4, 3, true, false>), grid, dim3(WG), lds, st, p, cp); break;
+    case 263: hipLaunchKernelGGL((k_map1<32, 4, 3, true, true>), grid, dim3(WG), lds, st, p, cp); break;
     case 128: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 129: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 132: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
     case 130: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 131: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 134: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
     case 256: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 257: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 260: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
     case 258: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 259: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 262: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -26,10 +26,10 @@ def probe_mode(request, monkeypatch):
     and wide direct tables gathered by the map or count kernel, 4-B direct and rank tables
     (transcript ids past 2^22) probed inside the sketch kernel, and the bucket table probed by k_probe
     (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map).
-    "chain": wide tables plus the chained tables (SKQ_CHAIN=1, indexes of one k built from
-    sequences); other indexes run as wide."""
+    "chain": wide tables plus the chained tables (SKQ_CHAIN=1, one per k slot of indexes built
+    from sequences, up to 4 slots); other indexes run as wide."""
     if request.param.startswith("chain"):
-        # chained tables (one k, indexes built from sequences) over wide tables
+        # chained tables (per k slot, indexes built from sequences) over wide tables
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
         monkeypatch.setenv("SKQ_PROBE", "wide")
         monkeypatch.setenv("SKQ_CHAIN", "1")
