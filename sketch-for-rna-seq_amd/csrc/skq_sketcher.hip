@@ -6,8 +6,9 @@
 // host memory the device maps, one kernel (one workgroup) stages them into LDS with 16-B loads
 // over the link, rolls ntHash over the windows (skq_sketch_seqs semantics: windows holding a byte
 // outside ACGTUacgtu are skipped, lowercase hashes like uppercase, U like T) and appends the
-// retained hashes to mapped pinned memory, and the host waits once on the call's stream. No
-// device-side copies, no session, no export round trips.
+// retained hashes to mapped pinned memory, then the count last (after a system-scope fence); the
+// host spins on that word instead of a stream synchronisation (the completion signal's round
+// trip cost ~10 us a call). No device-side copies, no session, no export round trips.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -93,8 +94,13 @@ __global__ __launch_bounds__(SK_WG) void k_sketch_one(const uint8_t* src, uint32
         }
     }
     __syncthreads();
-    if (t == 0) out[0] = s_cnt;
+    if (t == 0) {
+        __threadfence_system();  // (the hashes reach the host before the count that releases them)
+        __hip_atomic_store(out, s_cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
+
+constexpr uint32_t SK_PENDING = 0xFFFFFFFFu;  // out[0] until the kernel's count lands
 
 }  // namespace
 
@@ -172,12 +178,19 @@ int skq_sketcher_run(skq_sketcher* h, const char* seq, uint64_t len, uint32_t k,
         if (len) std::memcpy(h->hin, seq, len);
         const uint64_t nw = len >= k && k ? len - k + 1 : 0;
         const size_t lds = len <= SK_LDS_MAX ? (size_t)((len + 15) & ~15ull) : 0;
+        __atomic_store_n(h->hout, SK_PENDING, __ATOMIC_RELEASE);
         hipLaunchKernelGGL(k_sketch_one, dim3(1), dim3(SK_WG), lds, h->st, h->din, (uint32_t)len, k, threshold, h->dout,
                            (uint32_t)std::min<uint64_t>(nw, h->cap_len));
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(h->st) != hipSuccess) {
+        bool ok = hipGetLastError() == hipSuccess;
+        // the count word, polled (a bounded spin: the stream's own completion settles the rest)
+        uint32_t c = SK_PENDING;
+        for (int spin = 0; ok && spin < (1 << 16) && (c = __atomic_load_n(h->hout, __ATOMIC_ACQUIRE)) == SK_PENDING; ++spin)
+            __builtin_ia32_pause();
+        if (ok && c == SK_PENDING) ok = hipStreamSynchronize(h->st) == hipSuccess;
+        if (!ok) {
             rc = sfail(-3, "sketcher kernel failed");
         } else {
-            const uint64_t n = h->hout[0];
+            const uint64_t n = __atomic_load_n(h->hout, __ATOMIC_ACQUIRE);
             *count = n;
             if (hashes && cap) std::memcpy(hashes, h->hout + 1, std::min(n, cap) * 4);
         }

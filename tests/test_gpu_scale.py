@@ -113,8 +113,12 @@ def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-def test_cfg5_multi_k_200k_transcripts(tx200k):
-    cpu, _, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501)
+@pytest.mark.parametrize("mode", ["map1", "chain"])
+def test_cfg5_multi_k_200k_transcripts(tx200k, mode, monkeypatch):
+    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB)."""
+    monkeypatch.setenv("SKQ_CHAIN", "1" if mode == "chain" else "0")
+    cpu, st, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501, chained=mode == "chain")
+    assert (st["chained"] > 2) == (mode == "chain"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert sl[0] > 100  # the k = 21 pass's capacity sends reads to the slow path
 
