@@ -117,7 +117,9 @@ int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_off
  * createSketch_FracMinhash_direct once per transcript per k (src/main.cpp:79) and once per read
  * per k (src/main.cpp:143-144), and the C++ drop-in (include/dropin/sketch.h, kmer.h) serves those
  * calls here. skq_sketch_seqs semantics for one sequence; the bytes go through pinned host memory
- * the device maps, one kernel, one stream synchronisation per call. hashes receives up to cap of
+ * the device maps to a resident single-workgroup server (launched by the first call, gone after
+ * 2 ms without one, relaunched by the next), no launch or stream synchronisation per call: the
+ * caller spins on a mapped completion word. hashes receives up to cap of
  * the retained windows' hashes (unordered; a hash retained at two windows appears twice: the
  * caller's set removes repeats), *count how many there are. Handles are not thread-safe; one per
  * host thread. max_len only sizes the first buffers (longer sequences grow them). */

@@ -167,6 +167,24 @@ int dev_alloc(T** p, uint64_t count) {
     return 0;
 }
 
+// the gather tables (wide and chained entries, GBs read at random): physically contiguous when
+// SKQ_CONTIG=1 (development A/B: contiguous memory lets the page tables use their largest
+// fragments, so a translation covers more of the table), else hipMalloc
+template <typename T>
+int dev_alloc_table(T** p, uint64_t count) {
+    static const bool contig = [] {
+        const char* e = std::getenv("SKQ_CONTIG");
+        return e && std::atoi(e) == 1;
+    }();
+    *p = nullptr;
+    if (count == 0) count = 1;
+    if (contig && hipExtMallocWithFlags(reinterpret_cast<void**>(p), count * sizeof(T), hipDeviceMallocContiguous) == hipSuccess)
+        return 0;
+    (void)hipGetLastError();
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+    return 0;
+}
+
 template <typename T>
 void dev_free(T*& p) {
     if (p) (void)hipFree(p);
@@ -290,7 +308,7 @@ int build_wide(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables, co
     for (uint32_t t = 0; t < ntables; ++t) {
         const uint64_t m = dkeys[t].size();
         if (m && dvals[t].back() >= 0x80000000u) return fail(-1, "index too large for wide tables");
-        if (dev_alloc(&ix->d_wdir_t[t], len[t] * 8) || dev_alloc(&dk, m) || dev_alloc(&dv, m)) {
+        if (dev_alloc_table(&ix->d_wdir_t[t], len[t] * 8) || dev_alloc(&dk, m) || dev_alloc(&dv, m)) {
             dev_free(dk);
             dev_free(dv);
             return fail(-3, "wide table allocation failed");
@@ -589,7 +607,7 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
     uint32_t* dk = nullptr;
     uint4* de = nullptr;
     uint4*& dch = ix->d_chain[slot];
-    if (dev_alloc(&dch, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
+    if (dev_alloc_table(&dch, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
         dev_free(dk);
         dev_free(de);
         dev_free(dch);

@@ -32,6 +32,12 @@
 #include "skq_internal.h"
 
 
+// chained entries read eight lanes to an entry and handed over through LDS (1), or one lane per
+// entry (0: development A/B, profiles/r4_chain_coalesced_ab.log)
+#ifndef SKQ_CHN_COALESCED
+#define SKQ_CHN_COALESCED 1
+#endif
+
 namespace skq {
 
 // ---------------------------------------------------------------------------------------------
@@ -2203,7 +2209,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // read entry 0 and drop it — so no copy at a branch join waits for it)
     uint32_t cq = 0;
     bool has_q = false;
-    uint4 ce[CHN ? 7 : 1];
+    uint4 ce[CHN ? (SKQ_CHN_COALESCED ? 8 : 7) : 1];
     uint32_t nraw = 0;  // retained windows (position order) in the raw rows
     if (hashing) {
         const uint32_t T = p.threshold;
@@ -2288,20 +2294,27 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     if constexpr (CHN) {
         cq = s_raw[(HCAP + 1) * WG + tid];  // (the first retained window)
         has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len[ks];
-        // words 0-26 of the entry (27-31 unused)
-        const uint4* ent = reinterpret_cast<const uint4*>(cp.chain[ks]) + (has_q ? (uint64_t)cq * 8 : 0ull);
-        if (cp.ablate & 64u) {  // (development A/B: the entry's loads with sc0, past the L1)
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#if SKQ_CHN_COALESCED
+        // eight lanes read one entry, a 16-B piece each, eight entries per load: a load touches 8
+        // lines, not 64 (the texture addresser, busy ~75 % of k_map1's time, works per line), and
+        // the pieces reach their owners through LDS in the chain step below. The wave's region is
+        // free here: the hashing loop is done with the staged codes.
+        {
+            uint32_t* s_q = reinterpret_cast<uint32_t*>(s_wave);
+            s_q[lane] = has_q ? cq : 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint4* tab = reinterpret_cast<const uint4*>(cp.chain[ks]) + (lane & 7u);
 #pragma unroll
-            for (int u = 0; u < 7; ++u) {
-                u32x4 x;
-                asm volatile("global_load_dwordx4 %0, %1, off sc0" : "=v"(x) : "v"(ent + u) : "memory");
-                ce[u] = make_uint4(x.x, x.y, x.z, x.w);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < 7; ++u) ce[u] = ent[u];
+            for (int u = 0; u < 8; ++u) ce[u] = tab[(uint64_t)s_q[8 * u + (lane >> 3)] * 8];
         }
+#else
+        // words 0-27 of the entry (28-31 unused), one lane per entry
+        const uint4* ent = reinterpret_cast<const uint4*>(cp.chain[ks]) + (has_q ? (uint64_t)cq * 8 : 0ull);
+#pragma unroll
+        for (int u = 0; u < 7; ++u) ce[u] = ent[u];
+#endif
         has_q = hashing && nraw && nraw <= HCAP;  // (a query past the table: no such key)
     }
     if (hashing) {
@@ -2420,26 +2433,40 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // those into its own count table (no other lane writes it before the entry list below).
         // What no record holds goes through the entry list as before. An entry with no records (no
         // such key, or a query past the table) settles the query itself: no postings.
-        if (cp.ablate & 64u) {  // (the asm loads above: wait for them before their registers are read)
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 x[7];
+#if SKQ_CHN_COALESCED
+        // the loads' pieces to their owners, 16 entries (2 loads) a round through the wave's region:
+        // piece p of entry e at (e * 9 + p) * 16 (the pad: an owner's reads 144 B apart fall in
+        // distinct banks); the owners of a round read their entry's words 0-27
+        uint4 cw[7];
+        {
+            uint4* s_tr = reinterpret_cast<uint4*>(s_wave);
+            const uint32_t g = lane >> 3, pc = lane & 7u, el = lane & 15u;
 #pragma unroll
-            for (int u = 0; u < 7; ++u) x[u] = u32x4{ce[u].x, ce[u].y, ce[u].z, ce[u].w};
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6])
-                         :
-                         : "memory");
+            for (int rd = 0; rd < 4; ++rd) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                s_tr[g * 9 + pc] = ce[2 * rd];
+                s_tr[(8 + g) * 9 + pc] = ce[2 * rd + 1];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if ((lane >> 4) == (uint32_t)rd)
 #pragma unroll
-            for (int u = 0; u < 7; ++u) ce[u] = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
+                    for (int q = 0; q < 7; ++q) cw[q] = s_tr[el * 9 + q];
+            }
         }
+#else
+        const uint4* cw = ce;
+#endif
         uint32_t w[28];
         const bool inb = has_q && cq < cp.chain_len[ks];  // (else the lane read entry 0 and drops it)
 #pragma unroll
         for (int u = 0; u < 7; ++u) {
-            w[4 * u] = inb ? ce[u].x : 0u;
-            w[4 * u + 1] = inb ? ce[u].y : 0u;
-            w[4 * u + 2] = inb ? ce[u].z : 0u;
-            w[4 * u + 3] = inb ? ce[u].w : 0u;
+            w[4 * u] = inb ? cw[u].x : 0u;
+            w[4 * u + 1] = inb ? cw[u].y : 0u;
+            w[4 * u + 2] = inb ? cw[u].z : 0u;
+            w[4 * u + 3] = inb ? cw[u].w : 0u;
         }
         const bool absent = has_q && w[CHN_W_KEY] == 0u;
         uint32_t kh[CHN_KEYS];
@@ -3549,9 +3576,10 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
     __syncthreads();
     const uint32_t w0 = blockIdx.x * chunk, w1 = min(nW, w0 + chunk);
     // one lane per region (the header loads of WG regions are coalesced); a segment holds ~32
-    // entries, so 16 loads are issued together and the next region's header is read ahead: the
-    // kernel is latency-bound (two workgroups per CU, 64 KiB of bins each)
-    constexpr int U = 16;
+    // entries, read as 16-B words (a lane's load is one line-request for 4 entries, not 1: the
+    // texture addresser works per lane-request), 4 in flight, and the next region's header is
+    // read ahead (two workgroups per CU, 64 KiB of bins each)
+    constexpr int U = 4;
     uint32_t w = w0 + t;
     uint32_t s0 = 0, s1 = 0;
     if (w < w1) {
@@ -3566,13 +3594,21 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
             n0 = hdr[(uint64_t)b * nW + wn];
             n1 = hdr[(uint64_t)(b + 1) * nW + wn];
         }
-        for (uint32_t q = s0; q < s1; q += U) {
-            uint32_t x[U];
+        const uint4* reg4 = reinterpret_cast<const uint4*>(reg);  // (regions are 16-B aligned)
+        for (uint32_t q = s0 & ~3u; q < s1; q += 4 * U) {
+            uint4 x[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = reg[min(q + u, s1 - 1)];
+            for (int u = 0; u < U; ++u) x[u] = reg4[min(q / 4 + u, (s1 - 1) / 4)];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (q + u < s1) atomicAdd(&s_bins[x[u] & (bs - 1u)], (1ull << 40) | (unsigned long long)(x[u] >> bits));
+            for (int u = 0; u < U; ++u) {
+                const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t j = q + 4 * u + i;
+                    if (j >= s0 && j < s1)
+                        atomicAdd(&s_bins[xs[i] & (bs - 1u)], (1ull << 40) | (unsigned long long)(xs[i] >> bits));
+                }
+            }
         }
         w = wn;
         s0 = n0;

@@ -2,13 +2,15 @@
 // (src/main.cpp:79 index side, :143-144 read side: createSketch_FracMinhash_direct once per
 // sequence per k, through the C++ drop-in include/dropin/sketch.h).
 //
-// A call cannot amortise a launch, so it is built to cost one: the caller's bytes go into pinned
-// host memory the device maps, one kernel (one workgroup) stages them into LDS with 16-B loads
-// over the link, rolls ntHash over the windows (skq_sketch_seqs semantics: windows holding a byte
-// outside ACGTUacgtu are skipped, lowercase hashes like uppercase, U like T) and appends the
-// retained hashes to mapped pinned memory, then the count last (after a system-scope fence); the
-// host spins on that word instead of a stream synchronisation (the completion signal's round
-// trip cost ~10 us a call). No device-side copies, no session, no export round trips.
+// A call cannot amortise a launch, so it does not pay one: a resident single-workgroup server
+// (k_sketch_server) waits on a mailbox in pinned host memory the device maps. The caller's bytes
+// go into a mapped pinned buffer, the request word is bumped, the server stages the bytes into
+// LDS with 16-B loads over the link, rolls ntHash over the windows (skq_sketch_seqs semantics:
+// windows holding a byte outside ACGTUacgtu are skipped, lowercase hashes like uppercase, U like
+// T), appends the retained hashes to mapped pinned memory and releases them with the done word
+// (after a system-scope fence); the host spins on that word. The server leaves after 2 ms without
+// a request (or when stopped), and the next call launches it again. No device-side copies, no
+// session, no export round trips, no launch or stream synchronisation per call.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,62 +47,113 @@ __device__ __forceinline__ uint32_t sk_code(uint8_t b) {
     }
 }
 
-// out[0] = retained windows, out[1 ..] = their hashes (up to cap; unordered, repeats kept)
-__global__ __launch_bounds__(SK_WG) void k_sketch_one(const uint8_t* src, uint32_t len, uint32_t k, uint32_t thr,
-                                                      uint32_t* out, uint32_t cap) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_seq[];
-    __shared__ uint8_t s_code[256];
-    __shared__ uint32_t s_cnt;
-    const uint32_t t = threadIdx.x;
-    s_code[t] = (uint8_t)sk_code((uint8_t)t);
-    if (t == 0) s_cnt = 0;
-    const bool staged = len <= SK_LDS_MAX;
-    if (staged) {  // (the host buffer is 16-B aligned and padded to 16 B)
-        const uint4* s4 = reinterpret_cast<const uint4*>(src);
-        uint4* d4 = reinterpret_cast<uint4*>(s_seq);
-        for (uint32_t q = t; q < (len + 15) / 16; q += SK_WG) d4[q] = s4[q];
-    }
-    __syncthreads();
-    const uint8_t* s = staged ? s_seq : src;
-    const uint32_t nw = len >= k && k ? len - k + 1 : 0;
-    // a chunk of windows per thread, rolled from its first base
-    const uint32_t chunk = max(1u, (nw + SK_WG - 1) / SK_WG);
-    uint64_t seed[4], rk[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        seed[c] = skq::SEED33[c];
-        const uint32_t d = k % 33;
-        rk[c] = d ? (((skq::SEED33[c] << d) | (skq::SEED33[c] >> (33 - d))) & skq::M33) : skq::SEED33[c];
-    }
-    for (uint32_t w0 = t * chunk; w0 < nw; w0 += SK_WG * chunk) {
-        uint64_t h = 0;
-        uint32_t run = 0;  // valid bases ending at p, counted from w0
-        const uint32_t pend = min(len, w0 + chunk + k - 1);
-        for (uint32_t p = w0; p < pend; ++p) {
-            const uint32_t c = s_code[s[p]];
-            if (c == 4) {
-                run = 0;
-                h = 0;
-                continue;
-            }
-            ++run;
-            h = ((h << 1) | (h >> 32)) & skq::M33;
-            h ^= seed[c];
-            if (run > k) h ^= rk[s_code[s[p - k]]];
-            if (run >= k && (uint32_t)h <= thr) {  // src/sketch.cpp:33-35
-                const uint32_t at = atomicAdd(&s_cnt, 1u);
-                if (at < cap) out[1 + at] = (uint32_t)h;
-            }
-        }
-    }
-    __syncthreads();
-    if (t == 0) {
-        __threadfence_system();  // (the hashes reach the host before the count that releases them)
-        __hip_atomic_store(out, s_cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+// the mailbox in pinned mapped host memory (coherent): the host posts a request by writing the
+// parameters, then req; the server answers with the hashes and count in out, then done = req
+struct SkMail {
+    uint32_t req, done, alive, stop;
+    uint32_t len, k, thr, cap;
+};
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t* a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-constexpr uint32_t SK_PENDING = 0xFFFFFFFFu;  // out[0] until the kernel's count lands
+// idle time after which the server exits (s_memrealtime ticks at 100 MHz): 2 ms
+constexpr uint64_t SK_IDLE = 200000;
+
+// One resident workgroup serving the host's requests in order, one sequence each: out[0] =
+// retained windows, out[1 ..] = their hashes (up to cap; unordered, repeats kept). It exits when
+// the host sets stop or after SK_IDLE without a request (clearing alive first and looking once
+// more, so a request posted meanwhile is still served), so the grid always drains. `last` is the
+// request the host saw completed before this launch.
+__global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_t* src, uint32_t* out, uint32_t last) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_seq[];
+    __shared__ uint8_t s_code[256];
+    __shared__ uint32_t s_cnt, s_cmd[5];  // request (0: exit), len, k, thr, cap
+    const uint32_t t = threadIdx.x;
+    s_code[t] = (uint8_t)sk_code((uint8_t)t);
+    for (;;) {
+        if (t == 0) {
+            uint32_t r = last;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                r = sys_load(&m->req);
+                if (r != last || sys_load(&m->stop)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > SK_IDLE) {
+                    sys_store(&m->alive, 0u);
+                    __threadfence_system();
+                    r = sys_load(&m->req);
+                    if (r != last) sys_store(&m->alive, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            const bool go = r != last && !sys_load(&m->stop);
+            if (!go) sys_store(&m->alive, 0u);
+            s_cmd[0] = go ? 1u : 0u;
+            if (go) {
+                s_cmd[1] = sys_load(&m->len);
+                s_cmd[2] = sys_load(&m->k);
+                s_cmd[3] = sys_load(&m->thr);
+                s_cmd[4] = sys_load(&m->cap);
+                last = r;
+            }
+            s_cnt = 0;
+        }
+        __syncthreads();
+        if (!s_cmd[0]) return;
+        const uint32_t len = s_cmd[1], k = s_cmd[2], thr = s_cmd[3], cap = s_cmd[4];
+        const bool staged = len <= SK_LDS_MAX;
+        if (staged) {  // (the host buffer is 16-B aligned and padded to 16 B)
+            const uint4* s4 = reinterpret_cast<const uint4*>(src);
+            uint4* d4 = reinterpret_cast<uint4*>(s_seq);
+            for (uint32_t q = t; q < (len + 15) / 16; q += SK_WG)
+                d4[q] = s4[q];
+        }
+        __syncthreads();
+        const uint8_t* s = staged ? s_seq : src;
+        const uint32_t nw = len >= k && k ? len - k + 1 : 0;
+        // a chunk of windows per thread, rolled from its first base
+        const uint32_t chunk = max(1u, (nw + SK_WG - 1) / SK_WG);
+        uint64_t seed[4], rk[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            seed[c] = skq::SEED33[c];
+            const uint32_t d = k % 33;
+            rk[c] = d ? (((skq::SEED33[c] << d) | (skq::SEED33[c] >> (33 - d))) & skq::M33) : skq::SEED33[c];
+        }
+        for (uint32_t w0 = t * chunk; w0 < nw; w0 += SK_WG * chunk) {
+            uint64_t h = 0;
+            uint32_t run = 0;  // valid bases ending at p, counted from w0
+            const uint32_t pend = min(len, w0 + chunk + k - 1);
+            for (uint32_t p = w0; p < pend; ++p) {
+                const uint32_t c = s_code[s[p]];
+                if (c == 4) {
+                    run = 0;
+                    h = 0;
+                    continue;
+                }
+                ++run;
+                h = ((h << 1) | (h >> 32)) & skq::M33;
+                h ^= seed[c];
+                if (run > k) h ^= rk[s_code[s[p - k]]];
+                if (run >= k && (uint32_t)h <= thr) {  // src/sketch.cpp:33-35
+                    const uint32_t at = atomicAdd(&s_cnt, 1u);
+                    if (at < cap) out[1 + at] = (uint32_t)h;
+                }
+            }
+        }
+        __syncthreads();
+        if (t == 0) {
+            __threadfence_system();  // (the hashes reach the host before the words that release them)
+            sys_store(out, s_cnt);
+            sys_store(&m->done, last);
+        }
+    }
+}
 
 }  // namespace
 
@@ -110,11 +163,33 @@ struct skq_sketcher {
     uint64_t cap_len = 0;   // bytes the pinned input holds
     uint8_t* hin = nullptr;  // pinned, mapped: the sequence
     uint32_t* hout = nullptr;  // pinned, mapped: [count, hashes...], cap_len + 1 words
-    uint8_t* din = nullptr;   // device views of the two
+    SkMail* mail = nullptr;  // pinned, mapped
+    uint8_t* din = nullptr;   // device views of the three
     uint32_t* dout = nullptr;
+    SkMail* dmail = nullptr;
+    uint32_t seq = 0;        // the last request posted (and completed: calls are synchronous)
+    bool running = false;    // a server was launched and may still be resident
 };
 
 namespace {
+
+// stop the server (if any) and wait until it has left the device
+int stop_server(skq_sketcher* h) {
+    if (!h->running) return 0;
+    __atomic_store_n(&h->mail->stop, 1u, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(h->st);
+    __atomic_store_n(&h->mail->stop, 0u, __ATOMIC_RELEASE);
+    h->running = false;
+    return e == hipSuccess ? 0 : sfail(-3, "sketcher server failed");
+}
+
+int launch_server(skq_sketcher* h) {
+    __atomic_store_n(&h->mail->alive, 1u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(k_sketch_server, dim3(1), dim3(SK_WG), SK_LDS_MAX, h->st, h->dmail, h->din, h->dout, h->seq - 1);
+    if (hipGetLastError() != hipSuccess) return sfail(-3, "sketcher server launch failed");
+    h->running = true;
+    return 0;
+}
 
 void release(skq_sketcher* h) {
     if (h->hin) (void)hipHostFree(h->hin);
@@ -128,6 +203,7 @@ void release(skq_sketcher* h) {
 
 int grow(skq_sketcher* h, uint64_t len) {
     if (len <= h->cap_len) return 0;
+    if (int rc = stop_server(h)) return rc;  // (the server holds the old buffers)
     release(h);
     const uint64_t cap = std::max<uint64_t>(4096, (len + 4095) & ~4095ull);
     // coherent: the device reads the host's bytes and the host reads the device's words with no
@@ -153,8 +229,15 @@ int skq_sketcher_create(int device, uint64_t max_len, skq_sketcher** out) {
     h->device = device;
     int rc = 0;
     if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) rc = sfail(-3, "stream creation failed");
-    if (!rc) rc = grow(h, max_len);
-    if (!rc && hipFuncSetAttribute(reinterpret_cast<const void*>(k_sketch_one), hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (!rc && (hipHostMalloc(reinterpret_cast<void**>(&h->mail), sizeof(SkMail), hipHostMallocMapped | hipHostMallocCoherent) !=
+                    hipSuccess ||
+                hipHostGetDevicePointer(reinterpret_cast<void**>(&h->dmail), h->mail, 0) != hipSuccess))
+        rc = sfail(-3, "sketcher mailbox allocation failed");
+    if (!rc) {
+        std::memset(h->mail, 0, sizeof(SkMail));
+        rc = grow(h, max_len);
+    }
+    if (!rc && hipFuncSetAttribute(reinterpret_cast<const void*>(k_sketch_server), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)SK_LDS_MAX) != hipSuccess)
         rc = sfail(-3, "LDS attribute failed");
     (void)hipSetDevice(prev);
@@ -177,19 +260,41 @@ int skq_sketcher_run(skq_sketcher* h, const char* seq, uint64_t len, uint32_t k,
     if (!rc) {
         if (len) std::memcpy(h->hin, seq, len);
         const uint64_t nw = len >= k && k ? len - k + 1 : 0;
-        const size_t lds = len <= SK_LDS_MAX ? (size_t)((len + 15) & ~15ull) : 0;
-        __atomic_store_n(h->hout, SK_PENDING, __ATOMIC_RELEASE);
-        hipLaunchKernelGGL(k_sketch_one, dim3(1), dim3(SK_WG), lds, h->st, h->din, (uint32_t)len, k, threshold, h->dout,
-                           (uint32_t)std::min<uint64_t>(nw, h->cap_len));
-        bool ok = hipGetLastError() == hipSuccess;
-        // the count word, polled (a bounded spin: the stream's own completion settles the rest)
-        uint32_t c = SK_PENDING;
-        for (int spin = 0; ok && spin < (1 << 16) && (c = __atomic_load_n(h->hout, __ATOMIC_ACQUIRE)) == SK_PENDING; ++spin)
+        SkMail* m = h->mail;
+        m->len = (uint32_t)len;
+        m->k = k;
+        m->thr = threshold;
+        m->cap = (uint32_t)std::min<uint64_t>(nw, h->cap_len);
+        uint32_t r = h->seq + 1;
+        if (r == 0) r = 1;  // (never a request of 0... nor the previous one)
+        __atomic_store_n(&m->req, r, __ATOMIC_RELEASE);
+        h->seq = r;
+        if (!h->running || !__atomic_load_n(&m->alive, __ATOMIC_ACQUIRE)) {
+            // no server, or one that has gone idle: wait for it to leave unless it took this request
+            // on its way out, then launch one (it serves the pending request first)
+            while (h->running && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != r) {
+                const hipError_t q = hipStreamQuery(h->st);
+                if (q == hipSuccess) h->running = false;
+                else if (q != hipErrorNotReady) rc = sfail(-3, "sketcher server failed");
+                if (rc) break;
+            }
+            if (!rc && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != r) rc = launch_server(h);
+        }
+        // the answer: done = r (bounded: a server that left without it is relaunched once)
+        for (uint64_t spin = 0; !rc && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != r; ++spin) {
             __builtin_ia32_pause();
-        if (ok && c == SK_PENDING) ok = hipStreamSynchronize(h->st) == hipSuccess;
-        if (!ok) {
-            rc = sfail(-3, "sketcher kernel failed");
-        } else {
+            if ((spin & 4095) == 4095) {
+                const hipError_t q = hipStreamQuery(h->st);
+                if (q == hipSuccess) {  // the server left (idle race): launch one again
+                    h->running = false;
+                    if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != r) rc = launch_server(h);
+                } else if (q != hipErrorNotReady) {
+                    rc = sfail(-3, "sketcher server failed");
+                }
+            }
+            if (spin > (1ull << 28)) rc = sfail(-3, "sketcher server timed out");  // (~10 s)
+        }
+        if (!rc) {
             const uint64_t n = __atomic_load_n(h->hout, __ATOMIC_ACQUIRE);
             *count = n;
             if (hashes && cap) std::memcpy(hashes, h->hout + 1, std::min(n, cap) * 4);
@@ -204,8 +309,10 @@ int skq_sketcher_free(skq_sketcher* h) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(h->device);
+    if (h->mail) (void)stop_server(h);
     if (h->st) (void)hipStreamSynchronize(h->st);
     release(h);
+    if (h->mail) (void)hipHostFree(h->mail);
     if (h->st) (void)hipStreamDestroy(h->st);
     (void)hipSetDevice(prev);
     delete h;
