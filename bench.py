@@ -357,7 +357,8 @@ def main(args):
     t0 = time.time()
     tx = synth.transcriptome(cfg["ntx"], seed=1)  # identical on every rank: replicated index
     tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
-    index = skq.Index(ks, tx.ntx, tables, device=gpu)
+    # (the transcripts' sequences too: they let the index add the chained tables, SKQ_CHAIN)
+    index = skq.Index(ks, tx.ntx, tables, device=gpu, seqs=(tx.seqs, tx.offs))
     bases, _, _ = synth.reads(tx, n, L, seed=1000 + rank, err=0.001)  # rank's shard
     d_reads = torch.from_numpy(bases).to(dev)
     sess = skq.Session(index, n, L)

@@ -866,12 +866,13 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
         skq_index_free(ix);
         return rc2;
     }
-    // chained tables (per k slot, ids within 22 bits, transcripts given): built only with
-    // SKQ_CHAIN = 1; a slot whose table does not fit keeps the wide entries alone
+    // chained tables (per k slot, ids within 22 bits, transcripts given): the default wherever
+    // they fit (SKQ_CHAIN = 0 turns them off; cfg3: k_map1 1.15 against 1.35 ms over the wide
+    // entries); a slot whose table does not fit keeps the wide entries alone
     if (seqs && seq_offs && nk <= (uint32_t)skq::NK_FAST && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
         ix->mode == 3) {  // (the entry list behind the chain step gathers wide entries)
         const char* e = std::getenv("SKQ_CHAIN");
-        const int cm = e ? std::atoi(e) : 0;
+        const int cm = e ? std::atoi(e) : 1;
         if (cm == 1)
             for (uint32_t i = 0; i < nk; ++i)
                 for (uint32_t t = 0; t < ntables; ++t)

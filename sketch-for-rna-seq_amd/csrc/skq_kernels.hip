@@ -2002,6 +2002,36 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // round; profiles/r3_map1_writes.log)
 constexpr uint32_t MAP_P = 512;
 constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
+// A wave's packed output (lane-ordered runs: this lane's words from its exclusive offset `off`
+// of the wave's `tot`, word j present when has(j), valued val(j)) to 16-B aligned g through the
+// wave's LDS region in chunks of MAP1_OUT_CH words, each written back as 16-B coalesced stores: a
+// store of 64 lanes then touches 8 lines, where one store per word rank touched up to 64 (the
+// texture addresser works per line: the chained tables' coalesced loads showed it, round 4)
+constexpr uint32_t MAP1_OUT_CH = 640;  // (2560 B: below the per-read flags)
+template <int N, typename Has, typename Val>
+__device__ __forceinline__ void wave_out_packed(uint32_t* g, uint32_t off, uint32_t tot, uint32_t* s_buf, uint32_t lane,
+                                                Has has, Val val) {
+    for (uint32_t c0 = 0; c0 < tot; c0 += MAP1_OUT_CH) {  // (uniform)
+        uint32_t e = off;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (has(j)) {
+                if (e - c0 < MAP1_OUT_CH) s_buf[e - c0] = val(j);
+                ++e;
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t nq = (min(MAP1_OUT_CH, tot - c0) + 3) / 4;
+        uint4* g4 = reinterpret_cast<uint4*>(g + c0);
+        const uint4* s4 = reinterpret_cast<const uint4*>(s_buf);
+        for (uint32_t q = lane; q < nq; q += 64) g4[q] = s4[q];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 template <int HCAP>
 struct Map1Static {
     uint32_t raw[(HCAP + 2) * WG];  // (first: at LDS address 0, the kernel's only static LDS)
@@ -2345,12 +2375,12 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     uint32_t hoff = 0;  // (packed) this read's first hash in the wave's region of k slot ks
     if (p.hpack && !(cp.ablate & 8u)) {
         const uint32_t mw = (uint32_t)__builtin_popcountll(keepm);
-        hoff = wave_incl_scan(mw, lane) - mw;
-        uint32_t* out = p.hashes + (uint64_t)ks * p.hcap * p.n + (r - lane) * p.hcap + hoff;
-        uint32_t rank = 0;
-#pragma unroll
-        for (int j = 0; j < HCAP; ++j)
-            if ((keepm >> j) & 1ull) out[rank++] = v[j];
+        const uint32_t incl = wave_incl_scan(mw, lane);
+        hoff = incl - mw;
+        // (the wave's region: the staged codes are dead, the chain step's loads issued)
+        wave_out_packed<HCAP>(p.hashes + (uint64_t)ks * p.hcap * p.n + r0 * p.hcap, hoff, __shfl(incl, 63, 64),
+                              reinterpret_cast<uint32_t*>(s_wave), lane, [&](int j) { return ((keepm >> j) & 1ull) != 0; },
+                              [&](int j) { return v[j]; });
     }
     if (live && !sk_prev) {
         if (slow) {
@@ -2711,12 +2741,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             kneed[(uint64_t)ks * cp.n + r] = 0;
         }
         if (!FINAL && cp.hpack) {  // (uniform) packed: the wave's kept entries in lane order
-            const uint32_t ko = wave_incl_scan(km, lane) - km;
-            uint32_t* out = cp.ktab + (uint64_t)ks * TS * cp.n + (r - lane) * TS + ko;
-            uint32_t rank = 0;
-#pragma unroll
-            for (int sl = 0; sl < TS; ++sl)
-                if (kev[sl] != EMPTY) out[rank++] = kev[sl];
+            const uint32_t incl = wave_incl_scan(km, lane);
+            wave_out_packed<TS>(cp.ktab + (uint64_t)ks * TS * cp.n + r0 * TS, incl - km, __shfl(incl, 63, 64),
+                                reinterpret_cast<uint32_t*>(s_wave), lane, [&](int sl) { return kev[sl] != EMPTY; },
+                                [&](int sl) { return kev[sl]; });
         }
         // (last pass, packed) where each earlier pass's entries of this read start in its region
         uint32_t koff[NK_FAST - 1] = {};
@@ -2840,11 +2868,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 cp.cand_cnt[r] = 0;
             }
             if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
-                const uint32_t coff = wave_incl_scan(nc, lane) - nc;
-                uint32_t* out = cp.cand_tid + (r - lane) * CCAP + coff;
-#pragma unroll
-                for (int d = 0; d < TS; ++d)
-                    if ((uint32_t)d < nc) out[d] = (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22);
+                const uint32_t incl = wave_incl_scan(nc, lane);
+                wave_out_packed<TS>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64),
+                                    reinterpret_cast<uint32_t*>(s_wave), lane, [&](int d) { return (uint32_t)d < nc; },
+                                    [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
             }
         }
     } else {
@@ -2888,11 +2915,11 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             cp.cand_cnt[r] = 0;
         }
         if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
-            const uint32_t coff = wave_incl_scan(nc, lane) - nc;
-            uint32_t* out = cp.cand_tid + (r - lane) * CCAP + coff;
-#pragma unroll
-            for (int d = 0; d < TS; ++d)
-                if ((uint32_t)d < nc) out[d] = (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22);
+            const uint32_t incl = wave_incl_scan(nc, lane);
+            // (the wave's region: the entry list and the per-read flags are dead)
+            wave_out_packed<TS>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64), reinterpret_cast<uint32_t*>(s_wave),
+                                lane, [&](int d) { return (uint32_t)d < nc; },
+                                [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
         }
     }
     MAP1_STAMP(4);

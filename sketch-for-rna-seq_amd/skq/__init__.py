@@ -196,8 +196,8 @@ class Index:
     """Device-resident inverted index. tables: {k: (keys u32 asc, offs u64 [nkeys+1], tids u32)}."""
 
     def __init__(self, ks, ntx, tables, device=0, seqs=None, thr=None):
-        """seqs = (flat bytes, offs[ntx + 1]): the transcripts the tables were built from; with
-        one k they add the chained tables (skq_index_create_chained), sketched at thr."""
+        """seqs = (flat bytes, offs[ntx + 1]): the transcripts the tables were built from; they add
+        the chained tables, one per k slot (skq_index_create_chained; SKQ_CHAIN), sketched at thr."""
         self.ks = [int(k) for k in ks]
         self.ntx = int(ntx)
         self.device = device
