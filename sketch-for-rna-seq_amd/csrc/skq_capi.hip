@@ -525,7 +525,10 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
     uint64_t budget = 65536ull << 20;
     if (const char* e = std::getenv("SKQ_CHAIN_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || len * 128 > fr / 2 || len * 128 > budget) return 0;
+    // (half of what is free past a 32 GiB reserve for sessions: several indexes may share a device)
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < (32ull << 30) || len * 128 > (fr - (32ull << 30)) / 2 ||
+        len * 128 > budget)
+        return 0;
     const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // (key, successor, hop) triples, bucketed by key range, one sort per bucket
     constexpr uint32_t NB = 256;
@@ -608,10 +611,12 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
     uint4* de = nullptr;
     uint4*& dch = ix->d_chain[slot];
     if (dev_alloc_table(&dch, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
+        // (the device is shared, e.g. several indexes on it: this slot keeps the wide entries)
         dev_free(dk);
         dev_free(de);
         dev_free(dch);
-        return fail(-3, "chained table allocation failed");
+        (void)hipGetLastError();
+        return 0;
     }
     hipStream_t st = nullptr;
     const bool ok = hipMemsetAsync(dch, 0, len * 128, st) == hipSuccess &&

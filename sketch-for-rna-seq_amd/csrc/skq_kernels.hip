@@ -2008,9 +2008,19 @@ constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 // store of 64 lanes then touches 8 lines, where one store per word rank touched up to 64 (the
 // texture addresser works per line: the chained tables' coalesced loads showed it, round 4)
 constexpr uint32_t MAP1_OUT_CH = 640;  // (2560 B: below the per-read flags)
+#ifndef SKQ_OUT_LDS
+#define SKQ_OUT_LDS 1  // (0: each lane stores its own words, development A/B)
+#endif
 template <int N, typename Has, typename Val>
 __device__ __forceinline__ void wave_out_packed(uint32_t* g, uint32_t off, uint32_t tot, uint32_t* s_buf, uint32_t lane,
                                                 Has has, Val val) {
+    if (!SKQ_OUT_LDS) {
+        uint32_t e = off;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (has(j)) g[e++] = val(j);
+        return;
+    }
     for (uint32_t c0 = 0; c0 < tot; c0 += MAP1_OUT_CH) {  // (uniform)
         uint32_t e = off;
 #pragma unroll
