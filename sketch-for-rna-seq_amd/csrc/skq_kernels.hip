@@ -2009,7 +2009,7 @@ constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 // texture addresser works per line: the chained tables' coalesced loads showed it, round 4)
 constexpr uint32_t MAP1_OUT_CH = 640;  // (2560 B: below the per-read flags)
 #ifndef SKQ_OUT_LDS
-#define SKQ_OUT_LDS 1  // (0: each lane stores its own words, development A/B)
+#define SKQ_OUT_LDS 0  // (1: through LDS; measured: wide 3 % slower, chained the same, profiles/r4_out_lds_ab.log)
 #endif
 template <int N, typename Has, typename Val>
 __device__ __forceinline__ void wave_out_packed(uint32_t* g, uint32_t off, uint32_t tot, uint32_t* s_buf, uint32_t lane,
