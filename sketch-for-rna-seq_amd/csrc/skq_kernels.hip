@@ -2249,7 +2249,9 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     // read entry 0 and drop it — so no copy at a branch join waits for it)
     uint32_t cq = 0;
     bool has_q = false;
-    uint4 ce[CHN ? (SKQ_CHN_COALESCED ? 8 : 7) : 1];
+    // (clang vectors, not uint4: copies of the HIP vector struct kept this array in scratch)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 ce[CHN ? (SKQ_CHN_COALESCED ? 8 : 7) : 1];
     uint32_t nraw = 0;  // retained windows (position order) in the raw rows
     if (hashing) {
         const uint32_t T = p.threshold;
@@ -2345,13 +2347,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint4* tab = reinterpret_cast<const uint4*>(cp.chain[ks]) + (lane & 7u);
+            const u32x4* tab = reinterpret_cast<const u32x4*>(cp.chain[ks]) + (lane & 7u);
 #pragma unroll
             for (int u = 0; u < 8; ++u) ce[u] = tab[(uint64_t)s_q[8 * u + (lane >> 3)] * 8];
         }
 #else
         // words 0-27 of the entry (28-31 unused), one lane per entry
-        const uint4* ent = reinterpret_cast<const uint4*>(cp.chain[ks]) + (has_q ? (uint64_t)cq * 8 : 0ull);
+        const u32x4* ent = reinterpret_cast<const u32x4*>(cp.chain[ks]) + (has_q ? (uint64_t)cq * 8 : 0ull);
 #pragma unroll
         for (int u = 0; u < 7; ++u) ce[u] = ent[u];
 #endif
@@ -2477,12 +2479,13 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // the loads' pieces to their owners, 16 entries (2 loads) a round through the wave's region:
         // piece p of entry e at (e * 9 + p) * 16 (the pad: an owner's reads 144 B apart fall in
         // distinct banks); the owners of a round read their entry's words 0-27
-        uint4 cw[7];
+        u32x4 cw[7];
         {
-            uint4* s_tr = reinterpret_cast<uint4*>(s_wave);
+            u32x4* s_tr = reinterpret_cast<u32x4*>(s_wave);
             const uint32_t g = lane >> 3, pc = lane & 7u, el = lane & 15u;
-#pragma unroll
-            for (int rd = 0; rd < 4; ++rd) {
+            // (static_for: a rolled loop would index ce at run time, i.e. through scratch)
+            static_for<4>([&](auto rdc) {
+                constexpr int rd = decltype(rdc)::value;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2494,10 +2497,10 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 if ((lane >> 4) == (uint32_t)rd)
 #pragma unroll
                     for (int q = 0; q < 7; ++q) cw[q] = s_tr[el * 9 + q];
-            }
+            });
         }
 #else
-        const uint4* cw = ce;
+        const u32x4* cw = ce;
 #endif
         uint32_t w[28];
         const bool inb = has_q && cq < cp.chain_len[ks];  // (else the lane read entry 0 and drops it)
