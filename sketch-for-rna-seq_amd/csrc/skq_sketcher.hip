@@ -48,17 +48,25 @@ __device__ __forceinline__ uint32_t sk_code(uint8_t b) {
 }
 
 // the mailbox in pinned mapped host memory (coherent): the host posts a request by writing the
-// parameters, then req; the server answers with the hashes and count in out, then done = req
-struct SkMail {
-    uint32_t req, done, alive, stop;
-    uint32_t len, k, thr, cap;
+// parameters, then req (0: stop), in one 16-B word the server reads with one load (a request's
+// parameters arrive with it: one link round trip, not five); the server answers with the hashes
+// and count in out, then done = req, on a line of its own
+struct alignas(64) SkMail {
+    uint32_t req, len, k, thr;
+    uint32_t pad0[12];
+    uint32_t done, alive;
+    uint32_t pad1[14];
 };
 
-__device__ __forceinline__ uint32_t sys_load(const uint32_t* a) {
-    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ void sys_store(uint32_t* a, uint32_t v) {
     __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// the mailbox word (req, len, k, thr): one 16-B load past the caches, waited on
+__device__ __forceinline__ u32x4 mail_load(const SkMail* m) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(&m->req) : "memory");
+    return v;
 }
 
 // idle time after which the server exits (s_memrealtime ticks at 100 MHz): 2 ms
@@ -66,46 +74,51 @@ constexpr uint64_t SK_IDLE = 200000;
 
 // One resident workgroup serving the host's requests in order, one sequence each: out[0] =
 // retained windows, out[1 ..] = their hashes (up to cap; unordered, repeats kept). It exits when
-// the host sets stop or after SK_IDLE without a request (clearing alive first and looking once
+// the host posts request 0 or after SK_IDLE without a request (clearing alive first and looking once
 // more, so a request posted meanwhile is still served), so the grid always drains. `last` is the
 // request the host saw completed before this launch.
-__global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_t* src, uint32_t* out, uint32_t last) {
+__global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_t* src, uint32_t* out, uint32_t last,
+                                                          uint32_t ocap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_seq[];
     __shared__ uint8_t s_code[256];
-    __shared__ uint32_t s_cnt, s_cmd[5];  // request (0: exit), len, k, thr, cap
+    __shared__ uint32_t s_cnt, s_cmd[4];  // go, len, k, thr
     const uint32_t t = threadIdx.x;
     s_code[t] = (uint8_t)sk_code((uint8_t)t);
     for (;;) {
         if (t == 0) {
-            uint32_t r = last;
+            bool go = false;
+            u32x4 mb;
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
-                r = sys_load(&m->req);
-                if (r != last || sys_load(&m->stop)) break;
+                mb = mail_load(m);
+                if (mb.x != last) {
+                    go = mb.x != 0;  // (0: stop)
+                    break;
+                }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > SK_IDLE) {
                     sys_store(&m->alive, 0u);
                     __threadfence_system();
-                    r = sys_load(&m->req);
-                    if (r != last) sys_store(&m->alive, 1u);
+                    mb = mail_load(m);
+                    go = mb.x != last && mb.x != 0;
+                    if (go) sys_store(&m->alive, 1u);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            const bool go = r != last && !sys_load(&m->stop);
             if (!go) sys_store(&m->alive, 0u);
             s_cmd[0] = go ? 1u : 0u;
-            if (go) {
-                s_cmd[1] = sys_load(&m->len);
-                s_cmd[2] = sys_load(&m->k);
-                s_cmd[3] = sys_load(&m->thr);
-                s_cmd[4] = sys_load(&m->cap);
-                last = r;
-            }
+            s_cmd[1] = mb.y;
+            s_cmd[2] = mb.z;
+            s_cmd[3] = mb.w;
+            last = mb.x;
             s_cnt = 0;
+            // (acquire at system scope: the sequence's bytes are read after the request word)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         __syncthreads();
         if (!s_cmd[0]) return;
-        const uint32_t len = s_cmd[1], k = s_cmd[2], thr = s_cmd[3], cap = s_cmd[4];
+        const uint32_t len = s_cmd[1], k = s_cmd[2], thr = s_cmd[3];
+        const uint32_t cap = min(len >= k && k ? len - k + 1 : 0u, ocap);
         const bool staged = len <= SK_LDS_MAX;
         if (staged) {  // (the host buffer is 16-B aligned and padded to 16 B)
             const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -176,16 +189,16 @@ namespace {
 // stop the server (if any) and wait until it has left the device
 int stop_server(skq_sketcher* h) {
     if (!h->running) return 0;
-    __atomic_store_n(&h->mail->stop, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&h->mail->req, 0u, __ATOMIC_RELEASE);  // (0: stop)
     const hipError_t e = hipStreamSynchronize(h->st);
-    __atomic_store_n(&h->mail->stop, 0u, __ATOMIC_RELEASE);
     h->running = false;
     return e == hipSuccess ? 0 : sfail(-3, "sketcher server failed");
 }
 
 int launch_server(skq_sketcher* h) {
     __atomic_store_n(&h->mail->alive, 1u, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(k_sketch_server, dim3(1), dim3(SK_WG), SK_LDS_MAX, h->st, h->dmail, h->din, h->dout, h->seq - 1);
+    hipLaunchKernelGGL(k_sketch_server, dim3(1), dim3(SK_WG), SK_LDS_MAX, h->st, h->dmail, h->din, h->dout, h->seq - 1,
+                       (uint32_t)std::min<uint64_t>(h->cap_len, 0xFFFFFFFFull));
     if (hipGetLastError() != hipSuccess) return sfail(-3, "sketcher server launch failed");
     h->running = true;
     return 0;
@@ -259,12 +272,10 @@ int skq_sketcher_run(skq_sketcher* h, const char* seq, uint64_t len, uint32_t k,
     int rc = grow(h, len);
     if (!rc) {
         if (len) std::memcpy(h->hin, seq, len);
-        const uint64_t nw = len >= k && k ? len - k + 1 : 0;
         SkMail* m = h->mail;
         m->len = (uint32_t)len;
         m->k = k;
         m->thr = threshold;
-        m->cap = (uint32_t)std::min<uint64_t>(nw, h->cap_len);
         uint32_t r = h->seq + 1;
         if (r == 0) r = 1;  // (never a request of 0... nor the previous one)
         __atomic_store_n(&m->req, r, __ATOMIC_RELEASE);
