@@ -34,6 +34,9 @@
 
 // chained entries read eight lanes to an entry and handed over through LDS (1), or one lane per
 // entry (0: development A/B, profiles/r4_chain_coalesced_ab.log)
+#ifndef SKQ_LIST_NU
+#define SKQ_LIST_NU 1  // (0: every entry-list pass runs MB rounds, development A/B)
+#endif
 #ifndef SKQ_CHN_COALESCED
 #define SKQ_CHN_COALESCED 1
 #endif
@@ -2634,10 +2637,14 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             uint4 w[R];
             uint32_t own[R], hk[R];
             bool ok[R];
+            // rounds this pass really has (uniform): behind the chained tables a wave lists ~30
+            // hashes, one round, and the other three would only issue predicated-off inserts
+            const uint32_t nu = SKQ_LIST_NU ? min((uint32_t)R, S - e0) : (uint32_t)R;
             if constexpr (CMP) {
                 // one entry each, at the slot listed with the hash
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
+                    if ((uint32_t)u >= nu) break;
                     const uint32_t e = (lane >> 1) * S + e0 + u;
                     ok[u] = e0 + u < S && e < ne;
                     const uint32_t ee = ok[u] ? e : 0;
@@ -2649,6 +2656,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             } else {
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
+                    if ((uint32_t)u >= nu) break;
                     const uint32_t e = (lane >> 1) * S + e0 + u;
                     const bool in = e0 + u < S && e < ne;
                     hk[u] = s_h[in ? e : 0];
@@ -2664,6 +2672,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             // to the probing loop
 #pragma unroll
             for (int u = 0; u < R; ++u) {
+                if ((uint32_t)u >= nu) break;
                 // tids in the entry, pair-uniform (> 7: the list continues at lists[offset];
                 // wide: [0x80000000 | offset]); compact: the even lane's half holds key and F
                 const uint32_t mine = CMP ? (w[u].x == hk[u] ? w[u].y >> 22 : 0u) : w[u].x;
