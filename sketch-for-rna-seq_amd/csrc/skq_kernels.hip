@@ -34,6 +34,9 @@
 
 // chained entries read eight lanes to an entry and handed over through LDS (1), or one lane per
 // entry (0: development A/B, profiles/r4_chain_coalesced_ab.log)
+#ifndef SKQ_HASH_SDWA
+#define SKQ_HASH_SDWA 1  // (0: roll-term offsets by shift and mask, development A/B)
+#endif
 #ifndef SKQ_LIST_NU
 #define SKQ_LIST_NU 1  // (0: every entry-list pass runs MB rounds, development A/B)
 #endif
@@ -2307,10 +2310,32 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             const uint32_t ce = (A2 & 0xCCCCCCCCu) | (B & 0x33333333u);
             const uint32_t co = (A2 & 0x33333333u) | (B & 0xCCCCCCCCu);
             uint32_t off[16];
+#if SKQ_HASH_SDWA
+            // the 15 offsets as bytes of four masked words (window 4b + c in byte b of word c),
+            // each taken by one byte-select move instead of a shift and a mask
+            const uint32_t wq[4] = {(ce << 3) & 0x78787878u, (co << 1) & 0x78787878u, (ce >> 1) & 0x78787878u,
+                                    (co >> 3) & 0x78787878u};
+            static_for<15>([&](auto jc) {
+                constexpr int j = decltype(jc)::value, b = j >> 2;
+                const uint32_t x = wq[j & 3];
+                uint32_t r;
+                if constexpr (b == 0) {
+                    r = x & 0xFFu;
+                } else if constexpr (b == 1) {
+                    asm("v_mov_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(r) : "v"(x));
+                } else if constexpr (b == 2) {
+                    asm("v_mov_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(r) : "v"(x));
+                } else {
+                    r = x >> 24;
+                }
+                off[j] = r;
+            });
+#else
             off[0] = (ce << 3) & 0x78u;
             off[1] = (co << 1) & 0x78u;
 #pragma unroll
             for (int j = 2; j < 15; ++j) off[j] = ((j & 1 ? co : ce) >> (2 * j - 3)) & 0x78u;
+#endif
             off[15] = ((A >> 30) << 5) | ((B >> 30) << 3);
             uint2 e[16];
 #pragma unroll
