@@ -2664,7 +2664,9 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             bool ok[R];
             // rounds this pass really has (uniform): behind the chained tables a wave lists ~30
             // hashes, one round, and the other three would only issue predicated-off inserts
-            const uint32_t nu = SKQ_LIST_NU ? min((uint32_t)R, S - e0) : (uint32_t)R;
+            // (chained: 1 % faster; wide tables, whose passes have all four: 2 % slower with the
+            // guard, so they keep the fixed rounds: profiles/r4_list_rounds_sdwa_ab.log)
+            const uint32_t nu = (SKQ_LIST_NU && CHN) ? min((uint32_t)R, S - e0) : (uint32_t)R;
             if constexpr (CMP) {
                 // one entry each, at the slot listed with the hash
 #pragma unroll
