@@ -439,27 +439,36 @@ def main(args):
     achieved = n * b_basis / (avg[kname] * 1e-3) / 1e9
     kio = n * b_kern[kname] / (avg[kname] * 1e-3) / 1e9
     traffic, traffic_src = None, None
-    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % cname)
+    # (cfg4 is cfg3's reads, index and k at 12.5M reads per GPU: its per-read traffic is cfg3's)
+    tname = "cfg3" if cname == "cfg4" and not os.path.exists(os.path.join(ROOT, "profiles", "traffic_cfg4.json")) else cname
+    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % tname)
     probe = index.stats()["probe"]
     if os.path.exists(tf):                               # PMC FETCH/WRITE passes (tools/traffic.py)
         tr = json.load(open(tf))
         if kname in tr.get("kernels", {}) and tr.get("probe", probe) == probe and "calibration" in tr:
             traffic = tr["kernels"][kname]["hbm_bytes_per_read"] * n
-            traffic_src = "profiles/traffic_%s.json (%s); %s" % (cname, tr.get("measured", "builder's PMC passes"),
-                                                                tr["calibration"])
+            traffic_src = "profiles/traffic_%s.json (%s)%s; %s" % (
+                tname, tr.get("measured", "builder's PMC passes"),
+                ", per read, scaled to this launch's reads (cfg4 = cfg3's reads, index and k)" if tname != cname else "",
+                tr["calibration"])
     requests = None
     if map1:  # random index requests per launch against the measured gather ceiling
         rps = n * h / (avg[kname] * 1e-3) / 1e9
         requests = {"random_per_read": h, "achieved": rps, "ceiling": GATHER_CEIL_GPS, "unit": "G/s",
                     "frac": rps / GATHER_CEIL_GPS,
                     "ceiling_source": "tools/micro/gather_bench: random pair-cooperative 32-B gathers, 8 GiB table"}
+        if index.stats()["chained"] > 0:
+            requests["note"] = ("chained tables: random_per_read counts the hashes looked up; one 128-B chained "
+                                "entry per read (read by eight lanes together) settles ~2/3 of them and the rest "
+                                "gather 32-B wide entries, so the memory-side requests are all_per_read; the bound "
+                                "is the VALU and the CUs' per-line address work, not this rate (DESIGN.md section 5)")
         if traffic is not None:  # every memory-side request of the launch, from the calibrated PMC passes
             kt_ = json.load(open(tf))["kernels"][kname]
             per = kt_["fetch_size_bytes_per_read"] / 64.0 + kt_["write_bytes_per_read"] / 64.0
             requests.update(all_per_read=per, all_achieved=n * per / (avg[kname] * 1e-3) / 1e9,
                             all_note="read + write requests per read from profiles/traffic_%s.json (FETCH_SIZE "
                                      "and WRITE_SIZE tally 64 B per request); random-gather rates measured: "
-                                     "46-49 G/s from HBM, 54-56 G/s from the Infinity Cache (DESIGN.md §5)" % cname)
+                                     "46-49 G/s from HBM, 54-56 G/s from the Infinity Cache (DESIGN.md §5)" % tname)
     total_reads = n * world * args.steps
     value = total_reads / elapsed
 
