@@ -134,6 +134,7 @@ struct skq_session {
     uint32_t* bin_region[2] = {};
     uint32_t bin_par = 0;
     uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
+    uint64_t* tx_slab = nullptr;  // k_bin_sum's per-workgroup bins (ChainParams::tx_slab), 512 << bin_bits
     uint32_t* ktab = nullptr;    // multi-k map by passes: per-k count tables (allocated on first use)
     uint8_t* kcnt = nullptr;
     uint32_t* stash = nullptr;   // multi-k map by passes: the first pass's staged bases (SketchParams::stash)
@@ -997,6 +998,13 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
             skq_session_free(s);
             return rc;
         }
+    // (k_bin_sum's grid holds at most 512 (chunk, bucket) workgroups: 32 MiB at 2^13 ids a bucket;
+    // SKQ_SLAB=0: the bins go to tx_acc by atomics instead, development A/B)
+    const char* sl = std::getenv("SKQ_SLAB");
+    if (s->bin_nb && !(sl && std::atoi(sl) == 0) && (rc = dev_alloc(&s->tx_slab, 512ull << s->bin_bits))) {
+        skq_session_free(s);
+        return rc;
+    }
     if (hipMemset(s->tx_reads, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->tx_acc, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess ||
@@ -1043,6 +1051,7 @@ int skq_session_free(skq_session* s) {
         dev_free(s->bin_region[b]);
     }
     dev_free(s->tx_acc);
+    dev_free(s->tx_slab);
     dev_free(s->ktab);
     dev_free(s->kcnt);
     dev_free(s->stash);
@@ -1236,6 +1245,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.scratch = s->scratch;
     p.scratch_cap = s->scratch_cap;
     p.tx_acc = s->tx_acc;
+    p.tx_slab = s->tx_slab;
     p.ktab = s->ktab;
     p.kcnt = s->kcnt;
     p.tx_reads = s->tx_reads;

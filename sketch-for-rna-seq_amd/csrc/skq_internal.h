@@ -165,6 +165,10 @@ struct ChainParams {
     uint64_t* scratch;
     uint64_t scratch_cap;      // u64 words
     uint64_t* tx_acc;          // per batch: (reads << 40) | score (k_bin_sum), folded by k_fold_totals
+    // (null: k_bin_sum adds its bins to tx_acc with atomics) per k_bin_sum workgroup (chunk, bucket)
+    // its whole bucket of bins, plain stores, (chunk * nb + bucket) << bin_bits; k_fold_slab sums
+    // the chunks into tx_acc
+    uint64_t* tx_slab;
     uint64_t* tx_reads;
     uint64_t* tx_score;
     uint32_t* ctrl;

@@ -3642,9 +3642,28 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
     for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
+// the workgroup's bins out: to its slab slot with plain coalesced stores (k_fold_slab sums the
+// chunks: ~0.2M atomics in all instead of ~4M, one per non-empty bin of every workgroup), or
+// with atomics into tx_acc
+__device__ __forceinline__ void bins_out(const unsigned long long* s_bins, uint32_t bs, uint32_t b, uint32_t nb,
+                                         uint32_t ntx, uint64_t* tx_acc, uint64_t* slab) {
+    if (slab) {
+        uint64_t* o = slab + ((uint64_t)blockIdx.x * nb + b) * bs;
+        for (uint32_t i = threadIdx.x; i < bs; i += WG) o[i] = s_bins[i];
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < bs; i += WG) {
+        const unsigned long long a = s_bins[i];
+        const uint32_t tx = b * bs + i;
+        // one packed atomic per bin ((reads << 40) | score: a batch holds < 2^24 reads of score
+        // <= 2^10); k_fold_totals unpacks the batch's sums once
+        if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
+    }
+}
+
 __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nb, uint32_t nW,
                                                uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
-                                               uint32_t rstride) {
+                                               uint32_t rstride, uint64_t* slab) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
     const uint32_t bs = 1u << bits;
@@ -3691,13 +3710,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
         s1 = n1;
     }
     __syncthreads();
-    for (uint32_t i = t; i < bs; i += WG) {
-        const unsigned long long a = s_bins[i];
-        const uint32_t tx = b * bs + i;
-        // one packed atomic per bin ((reads << 40) | score: a batch holds < 2^24 reads of score
-        // <= 2^10); k_fold_totals unpacks the batch's sums once
-        if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
-    }
+    bins_out(s_bins, bs, b, nb, ntx, tx_acc, slab);
 }
 
 // k_bin_sum for few, long bucket segments (small transcript sets: a region's segment of a bucket
@@ -3707,7 +3720,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
 template <int GS>
 __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nW,
                                                   uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
-                                                  uint32_t rstride) {
+                                                  uint32_t rstride, uint64_t* slab) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
     const uint32_t bs = 1u << bits;
@@ -3729,10 +3742,16 @@ __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx
         }
     }
     __syncthreads();
-    for (uint32_t i = t; i < bs; i += WG) {
-        const unsigned long long a = s_bins[i];
-        const uint32_t tx = b * bs + i;
-        if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
+    bins_out(s_bins, bs, b, gridDim.y, ntx, tx_acc, slab);
+}
+
+// the slab's chunks summed per transcript into the batch's packed sums (coalesced over t)
+__global__ __launch_bounds__(WG) void k_fold_slab(const uint64_t* slab, uint32_t chunks, uint64_t stride, uint64_t* acc,
+                                                 uint32_t ntx) {
+    for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < ntx; t += gridDim.x * WG) {
+        unsigned long long a = 0;
+        for (uint32_t c = 0; c < chunks; ++c) a += slab[c * stride + t];
+        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t]), a);
     }
 }
 
@@ -4025,10 +4044,17 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum_g<16>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_bin_sum_g<16>, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx,
-                           bits, nW, chunk, hdr, region, (uint32_t)(WG * CCAP));
+                           bits, nW, chunk, hdr, region, (uint32_t)(WG * CCAP), p.tx_slab);
     } else {
         hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits,
-                           nb, nW, chunk, hdr, region, (uint32_t)(WG * CCAP));
+                           nb, nW, chunk, hdr, region, (uint32_t)(WG * CCAP), p.tx_slab);
+    }
+    if (hipGetLastError() != hipSuccess) return -2;
+    if (p.tx_slab) {  // (the slab holds (chunks * nb) << bits words: session-sized for 512 of them)
+        const uint32_t nch = (nW + chunk - 1) / chunk;
+        const unsigned grid = (unsigned)std::min<uint32_t>((p.ntx + WG - 1) / WG, 1024);
+        hipLaunchKernelGGL(k_fold_slab, dim3(grid), dim3(WG), 0, st, p.tx_slab, nch, (uint64_t)nb << bits, p.tx_acc,
+                           p.ntx);
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
