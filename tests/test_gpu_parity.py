@@ -316,6 +316,20 @@ def test_slow_reads_past_the_wave_path():
         np.testing.assert_array_equal(out["totals"][1], ts)
 
 
+def test_long_read_at_the_maximal_threshold(tx300):
+    """A read longer than the slow sketch path's LDS holds, with every window retained (threshold
+    UINT32_MAX): its packed run needs the two header words past its windows (round-3 advice: the
+    run was sized for the windows alone and the map failed with E_HASH_EXT)."""
+    gi, oi = build([31], tx=tx300)
+    rng = np.random.default_rng(5)
+    long = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 5000))
+    reads = [long, tx300.seq(0)[:150], long[:4200], tx300.seq(1)[:150]]
+    thr = 0xFFFFFFFF
+    out = run_gpu(gi, reads, thr=thr)
+    ref = oi.map_batch(reads, thr=thr)
+    compare(out, ref, len(reads), 1)
+
+
 def test_list_lengths_around_the_inline_limit():
     # hand-built index whose lists hold 1..12 transcripts: wide entries keep 7 inline and read
     # the rest from the postings list; each read stays within 16 distinct transcripts (the
