@@ -999,9 +999,9 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
             return rc;
         }
     // (k_bin_sum's grid holds at most 512 (chunk, bucket) workgroups: 32 MiB at 2^13 ids a bucket;
-    // SKQ_SLAB=0: the bins go to tx_acc by atomics instead, development A/B)
+    // SKQ_SLAB=1: through the slab, else the bins go to tx_acc by atomics; development A/B)
     const char* sl = std::getenv("SKQ_SLAB");
-    if (s->bin_nb && !(sl && std::atoi(sl) == 0) && (rc = dev_alloc(&s->tx_slab, 512ull << s->bin_bits))) {
+    if (s->bin_nb && (sl && std::atoi(sl) == 1) && (rc = dev_alloc(&s->tx_slab, 512ull << s->bin_bits))) {
         skq_session_free(s);
         return rc;
     }

@@ -464,7 +464,10 @@ def test_chain_sketches_entry_point(tx300):
         assert list(out["cand_score"][co[r]:co[r + 1]]) == list(sc[:c])
 
 
-def test_repeated_batches_accumulate_totals(tx300):
+@pytest.mark.parametrize("slab", ["0", "1"])
+def test_repeated_batches_accumulate_totals(tx300, slab, monkeypatch):
+    """slab: the totals' bins through k_bin_sum's per-chunk slab and k_fold_slab (SKQ_SLAB=1)."""
+    monkeypatch.setenv("SKQ_SLAB", slab)
     gi, oi = build([31], tx=tx300)
     bases, _, _ = synth.reads(tx300, 1000, 150, seed=44)
     reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(1000)]

@@ -94,20 +94,24 @@ def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
     return cpu, st, slow
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab"])
 def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
-    monkeypatch.setenv("SKQ_CHAIN", "1" if mode == "chain" else "0")
-    cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode == "chain")
+    """chain-slab: the totals through k_bin_sum's per-chunk slab (SKQ_SLAB=1)."""
+    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "1")
+    monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
+    cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode != "map1")
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab"])
 def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
-    """chain: k_map1 over the chained tables (SKQ_CHAIN=1)."""
-    monkeypatch.setenv("SKQ_CHAIN", "1" if mode == "chain" else "0")
-    cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode == "chain")
-    assert (st["chained"] > 2) == (mode == "chain"), st
+    """chain: k_map1 over the chained tables (SKQ_CHAIN=1); chain-slab: and the totals through
+    k_bin_sum's per-chunk slab (SKQ_SLAB=1)."""
+    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "1")
+    monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
+    cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode != "map1")
+    assert (st["chained"] > 2) == (mode != "map1"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert st["max_list"] >= 10  # GENCODE-scale postings (long lists take the inline overflow)
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
