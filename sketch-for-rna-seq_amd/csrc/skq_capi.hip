@@ -1160,7 +1160,17 @@ static int wait_totals(skq_session* s, hipStream_t st) {
 // the side stream (totals binning) and its events
 static int ensure_side(skq_session* s) {
     if (s->side) return 0;
-    HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+    // (SKQ_SIDE_PRIO=1: the side stream at the lowest priority, so the next batch's map is
+    // dispatched ahead of the totals; development A/B)
+    const char* pe = std::getenv("SKQ_SIDE_PRIO");
+    if (pe && std::atoi(pe) == 1) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        std::fprintf(stderr, "[skq] side stream priority %d (range %d..%d)\n", lo, lo, hi);
+        HIP_TRY(hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo));
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+    }
     HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_join[0], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_join[1], hipEventDisableTiming));

@@ -4032,8 +4032,14 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
         if (hipGetLastError() != hipSuccess) return -2;
     }
     if (nb == 0) return 0;
-    // about two workgroups per CU in flight: chunks * nb ~ 512
-    const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nW, 512 / nb));
+    // about two workgroups per CU in flight: chunks * nb ~ 512 (SKQ_BIN_WGS: fewer, development
+    // A/B — the totals run beside the next batch's map, whose workgroups they displace)
+    static const uint32_t wgs = [] {
+        const char* e = std::getenv("SKQ_BIN_WGS");
+        const int v = e ? std::atoi(e) : 512;
+        return (uint32_t)std::max(1, std::min(512, v));
+    }();
+    const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nW, wgs / nb));
     const uint32_t chunk = (nW + chunks - 1) / chunks;
     const size_t lds = (size_t)8 << bits;
     if (lds > 64 * 1024)
