@@ -2017,14 +2017,17 @@ constexpr uint32_t MAP1_OUT_CH = 640;  // (2560 B: below the per-read flags)
 #ifndef SKQ_OUT_LDS
 #define SKQ_OUT_LDS 0  // (1: through LDS; measured: wide 3 % slower, chained the same, profiles/r4_out_lds_ab.log)
 #endif
-template <int N, typename Has, typename Val>
+// (MONO: has(j) implies has(j - 1) in every lane, so the words stop at the wave's longest run)
+template <int N, bool MONO = false, typename Has, typename Val>
 __device__ __forceinline__ void wave_out_packed(uint32_t* g, uint32_t off, uint32_t tot, uint32_t* s_buf, uint32_t lane,
                                                 Has has, Val val) {
     if (!SKQ_OUT_LDS) {
         uint32_t e = off;
 #pragma unroll
-        for (int j = 0; j < N; ++j)
+        for (int j = 0; j < N; ++j) {
+            if (MONO && !__any(has(j))) break;  // (uniform)
             if (has(j)) g[e++] = val(j);
+        }
         return;
     }
     for (uint32_t c0 = 0; c0 < tot; c0 += MAP1_OUT_CH) {  // (uniform)
@@ -2918,7 +2921,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             }
             if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
                 const uint32_t incl = wave_incl_scan(nc, lane);
-                wave_out_packed<TS>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64),
+                wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64),
                                     reinterpret_cast<uint32_t*>(s_wave), lane, [&](int d) { return (uint32_t)d < nc; },
                                     [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
             }
@@ -2947,6 +2950,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 uint32_t* cs = cp.cand_score + r;
 #pragma unroll
                 for (int d = 0; d < TS; ++d) {
+                    if (!__any(key[d] != ~0u)) break;  // (uniform: sorted, the kept keys come first)
                     if (key[d] != ~0u) {
                         if (!cp.cpack) {
                             ct[(uint64_t)d * cp.n] = key[d] & 0x3FFFFFu;
@@ -2966,7 +2970,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
             const uint32_t incl = wave_incl_scan(nc, lane);
             // (the wave's region: the entry list and the per-read flags are dead)
-            wave_out_packed<TS>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64), reinterpret_cast<uint32_t*>(s_wave),
+            wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64), reinterpret_cast<uint32_t*>(s_wave),
                                 lane, [&](int d) { return (uint32_t)d < nc; },
                                 [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
         }
