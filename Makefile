@@ -20,7 +20,7 @@ ref: $(OUT)/libskq.so
 .PHONY: ref
 
 HIPFLAGS := $(CXXFLAGS_COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o \
+LIB_OBJS := $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_map1.o $(OUT)/obj/skq_map1_pass.o $(OUT)/obj/skq_capi.o $(OUT)/obj/skq_tables.o $(OUT)/obj/skq_dropin.o \
             $(OUT)/obj/skq_io.o $(OUT)/obj/skq_ingest.o $(OUT)/obj/skq_em.o \
             $(OUT)/obj/skq_build.o $(OUT)/obj/skq_dropin_io.o $(OUT)/obj/skq_sketcher.o
 HOST_CXX ?= g++
@@ -33,6 +33,8 @@ $(OUT)/obj/%.o: $(CSRC)/%.hip $(CSRC)/skq_internal.h include/skq.h include/skq_h
 $(OUT)/obj/%.o: $(CSRC)/%.cpp $(CSRC)/skq_internal.h include/skq.h include/skq_host.h $(wildcard include/dropin/*.h)
 	@mkdir -p $(OUT)/obj
 	$(HOST_CXX) $(HOSTFLAGS) -c $< -o $@
+# (the two map parts are translation units of skq_kernels.hip)
+$(OUT)/obj/skq_map1.o $(OUT)/obj/skq_map1_pass.o: $(CSRC)/skq_kernels.hip
 $(OUT)/libskq.so: $(LIB_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(LIB_OBJS)
 

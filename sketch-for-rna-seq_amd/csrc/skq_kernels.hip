@@ -31,6 +31,14 @@
 
 #include "skq_internal.h"
 
+// One source, three translation units built side by side (make -j): part 0 (this file) is
+// everything but the fused map's launchers; part 1 (skq_map1.hip) instantiates the one-k map,
+// part 2 (skq_map1_pass.hip) the multi-k passes. Templates and inline helpers are visible to all
+// three; every other definition sits in exactly one part.
+#ifndef SKQ_PART
+#define SKQ_PART 0
+#endif
+
 
 // chained entries read eight lanes to an entry and handed over through LDS (1), or one lane per
 // entry (0: development A/B, profiles/r4_chain_coalesced_ab.log)
@@ -269,12 +277,14 @@ __host__ __device__ inline size_t sketch_bad_bytes(uint32_t wc, bool nthash) {
     return nthash ? ((((size_t)wc + 1) * 2 + 15) & ~(size_t)15) : (((size_t)wc + 127) / 128) * 16;
 }
 
+#if SKQ_PART == 0
 size_t sketch_lds_bytes(uint32_t nk, uint32_t wave_chunks, uint32_t hcap, bool nthash) {
     size_t b = sketch_tab_bytes(nk);
     b += (WG / 64) * (sketch_codes_bytes(wave_chunks) + sketch_bad_bytes(wave_chunks, nthash));
     b += ((size_t)hcap + 1) * WG * 4;  // + one spare slot per lane for windows not retained
     return b;
 }
+#endif  // SKQ_PART == 0
 
 template <int HCAP, bool NTH>
 __global__ __launch_bounds__(WG) void k_sketch(SketchParams p) {
@@ -573,6 +583,7 @@ __device__ __forceinline__ uint32_t packed_share(const uint32_t* hash_cnt, const
 // and de-duplicated by the workgroup.
 constexpr uint32_t SLOW_CAP = 4096;
 
+#if SKQ_PART == 0
 __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
     __shared__ uint32_t s_buf[SLOW_CAP];
     __shared__ uint32_t s_scan[WG];
@@ -712,6 +723,7 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
         __syncthreads();
     }
 }
+#endif  // SKQ_PART == 0
 
 // ---------------------------------------------------------------------------------------------
 // K2: chain
@@ -898,7 +910,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 // probes per wave held in LDS: 512 per k slot (a 64-read wave of 150 bp reads averages ~384
 // at k = 31; a read that does not fit takes the slow path)
 __host__ __device__ inline uint32_t probe_cap(uint32_t nk) { return 512u * (nk < 1 ? 1 : (nk > 4 ? 4 : nk)); }
+#if SKQ_PART == 0
 size_t chain_lds_bytes(uint32_t nk) { return 256 + (size_t)(WG / 64) * probe_cap(nk) * 5; }
+#endif  // SKQ_PART == 0
 
 // k_probe: every retained hash -> the offset of its postings list (equivalence class).
 //   1. each wave lists its 64 reads' retained hashes (the probes) in LDS (wave prefix sum);
@@ -907,6 +921,7 @@ size_t chain_lds_bytes(uint32_t nk) { return 256 + (size_t)(WG / 64) * probe_cap
 //      with DPP quad permutes; QU loads per quad are kept in flight;
 //   3. each lane writes its read's list offsets out, SoA like the hashes (lofs[(i*lcap + j)*n
 //      + r]), and flags reads the fast path cannot take (pflag = 1, listed for k_chain_slow).
+#if SKQ_PART == 0
 __global__ __launch_bounds__(WG) void k_probe(ChainParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t PW_CAP = probe_cap(p.nk);
@@ -1030,6 +1045,7 @@ __global__ __launch_bounds__(WG) void k_probe(ChainParams p) {
     for (int i = 0; i < NK_FAST; ++i)
         for (uint32_t j = 0; j < cnt[i]; ++j) p.lofs[((uint64_t)i * p.lcap + j) * p.n + r] = sp[q++];
 }
+#endif  // SKQ_PART == 0
 
 // k_count: one lane per read. Counts the read's list offsets per distinct list (usually 1-3),
 // expands each distinct list into the per-transcript table with its packed per-k counts —
@@ -1173,6 +1189,7 @@ __global__ __launch_bounds__(WG) void k_count(ChainParams p) {
 
 // More k slots than the count kernels take (NK_FAST): every sketched read goes to the slow chain
 // path; the others get no candidates.
+#if SKQ_PART == 0
 __global__ __launch_bounds__(WG) void k_route_slow(ChainParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * WG + threadIdx.x;
     if (r >= p.n) return;
@@ -1180,6 +1197,7 @@ __global__ __launch_bounds__(WG) void k_route_slow(ChainParams p) {
     if (!p.status || (p.status[r] & SKQ_STATUS_MASK) == SKQ_READ_OK)
         list_push(p.ctrl, C_OVF2, C_ERR2, p.ovf2, p.ovf_cap, (uint32_t)r, E_OVF2_FULL);
 }
+#endif  // SKQ_PART == 0
 
 // k_count3: one lane per read, like k_count, with
 //   * the read's list offsets de-duplicated by a register sorting network (equal offsets form
@@ -2073,7 +2091,7 @@ inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
 }
 
 // sets p.map_wave_bytes / p.map_flag_at; returns the launch's LDS bytes
-size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
+inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
     p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
     p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
     // (the binning epilogue's bucket counters first, their own so they are zeroed up front; the
@@ -2986,6 +3004,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
 // LDS (global scratch beyond SLOW_CAP), sorted, and counted per transcript run.
+#if SKQ_PART == 0
 __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
     __shared__ uint64_t s_ent[SLOW_CAP];
     __shared__ uint32_t s_max[SKQ_MAX_K];
@@ -3769,11 +3788,13 @@ __global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* rea
         }
     }
 }
+#endif  // SKQ_PART == 0
 
 
 // ---------------------------------------------------------------------------------------------
 // launchers
 
+#if SKQ_PART == 0
 static bool use_count3(const ChainParams& p) { return p.ntx <= (1u << 22); }
 
 bool count_bins(const ChainParams& p) { return use_count3(p) && p.nk <= (uint32_t)NK_FAST && p.bin_nb > 0; }
@@ -3929,7 +3950,9 @@ int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals
     hipLaunchKernelGGL(k_dir_scatter, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), dir, keys, vals, n);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+#endif  // SKQ_PART == 0
 
+#if SKQ_PART == 1
 // SKQ_MAP1_OCC=1: print each k_map1 launch shape's resident workgroups per CU once (stderr)
 static void map1_report_occupancy(const void* kern, size_t lds) {
     static const bool on = [] {
@@ -3976,7 +3999,9 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     hipLaunchKernelGGL(kern, grid, dim3(WG), lds + pad, st, p, cp);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+#endif  // SKQ_PART == 1
 
+#if SKQ_PART == 2
 int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
     if (p0.n == 0) return 0;
     if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.kslot >= SKQ_MAX_K) return -4;
@@ -4003,9 +4028,11 @@ int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+#endif  // SKQ_PART == 2
 
 
 
+#if SKQ_PART == 0
 int launch_wdir_scatter(uint32_t* wdir, const uint32_t* keys, const uint32_t* vals, const uint32_t* lists,
                         uint64_t n, void* stream) {
     if (n == 0) return 0;
@@ -4068,6 +4095,7 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+#endif  // SKQ_PART == 0
 
 
 }  // namespace skq

@@ -129,28 +129,37 @@ def test_cfg5_multi_k_200k_transcripts(tx200k, mode, monkeypatch):
 
 @pytest.mark.parametrize("n,seed,ks", [(10_000_000, 1000, [31]), (12_500_000, 1003, [31]), (10_000_000, 1000, [21, 25, 31])],
                          ids=["cfg3_10M", "cfg4_rank3_12.5M", "cfg5_10M"])
-def test_full_batch_totals(tx200k, n, seed, ks):
+def test_full_batch_totals(tx200k, n, seed, ks, monkeypatch):
     """The bench's own batches, one skq_map each: cfg3 (10M x 150 bp, rank 0), cfg4's per-GPU
     shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it) and cfg5's batch (10M,
     multi-k passes, ~37k slow reads whose runs the slow wave writes while it reads other reads'
-    packed offsets): per-transcript totals equal the oracle's over the same reads as FASTQ text."""
+    packed offsets): per-transcript totals equal the oracle's over the same reads as FASTQ text.
+    Each batch runs twice against one oracle pass: over the wide entries, and over the chained
+    tables the bench and the CLI default to (an index given the transcripts' sequences), whose
+    marker entries (lists > 8 ids), queries past the table, slow-read hand-off and totals binning
+    are then checked at the full batch too."""
     L = 150
+    monkeypatch.setenv("SKQ_CHAIN", "1")
     tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
-    index = skq.Index(ks, tx200k.ntx, tables)
     bases, _, _ = synth.reads(tx200k, n, L, seed=seed, err=0.001)  # bench.py's batch of rank seed - 1000
-    s = skq.Session(index, n, L)
-    d = skq.DeviceBuffer.from_numpy(bases)
-    s.map(d.ptr, None, n, L, fixed_len=L)
-    s.check()
-    tot = s.totals()
-    slow = s.slow_reads()
-    s.free()
-    d.free()
-    index.free()
     cpu = orc.fastq_map(_oracle(tables, ks, tx200k.ntx), synth.fastq_bytes(bases, L), nthreads=NTHREADS,
                         outputs=False, totals=True)
     assert cpu["n"] == n
-    np.testing.assert_array_equal(tot[0], cpu["tx_reads"])
-    np.testing.assert_array_equal(tot[1], cpu["tx_score"])
-    assert int(tot[0].sum()) > 3 * n  # ~3.1 candidates per read
-    assert slow[0] + slow[1] > 100
+    d = skq.DeviceBuffer.from_numpy(bases)
+    del bases
+    for chained in (False, True):
+        index = skq.Index(ks, tx200k.ntx, tables, seqs=(tx200k.seqs, tx200k.offs) if chained else None)
+        st = index.stats()
+        assert (st["chained"] > 2) == chained, st  # (1 + the mean records per entry; 0: none)
+        s = skq.Session(index, n, L)
+        s.map(d.ptr, None, n, L, fixed_len=L)
+        s.check()
+        tot = s.totals()
+        slow = s.slow_reads()
+        s.free()
+        index.free()
+        np.testing.assert_array_equal(tot[0], cpu["tx_reads"], err_msg="chained=%s" % chained)
+        np.testing.assert_array_equal(tot[1], cpu["tx_score"], err_msg="chained=%s" % chained)
+        assert int(tot[0].sum()) > 3 * n  # ~3.1 candidates per read
+        assert slow[0] + slow[1] > 100
+    d.free()
