@@ -33,10 +33,24 @@ $(OUT)/obj/%.o: $(CSRC)/%.hip $(CSRC)/skq_internal.h include/skq.h include/skq_h
 $(OUT)/obj/%.o: $(CSRC)/%.cpp $(CSRC)/skq_internal.h include/skq.h include/skq_host.h $(wildcard include/dropin/*.h)
 	@mkdir -p $(OUT)/obj
 	$(HOST_CXX) $(HOSTFLAGS) -c $< -o $@
-# (the two map parts are translation units of skq_kernels.hip)
-$(OUT)/obj/skq_map1.o $(OUT)/obj/skq_map1_pass.o: $(CSRC)/skq_kernels.hip
+# (the two map parts include skq_kernels.hip's helpers and skq_map1.h)
+$(OUT)/obj/skq_map1.o $(OUT)/obj/skq_map1_pass.o: $(CSRC)/skq_kernels.hip $(CSRC)/skq_map1.h
 $(OUT)/libskq.so: $(LIB_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(LIB_OBJS)
+
+# development A/B builds (never the product): the kernel parts compiled with ABDEFS into
+# $(OUT)/ab/$(AB)/libskq.so, loaded with SKQ_LIB; e.g. make ab AB=oldhash ABDEFS=-DSKQ_HASH_PAIR=0
+AB ?= x
+ABDEFS ?=
+ABDIR := $(OUT)/ab/$(AB)
+AB_KOBJS := $(ABDIR)/skq_kernels.o $(ABDIR)/skq_map1.o $(ABDIR)/skq_map1_pass.o
+$(ABDIR)/%.o: $(CSRC)/%.hip $(CSRC)/skq_kernels.hip $(CSRC)/skq_map1.h $(CSRC)/skq_internal.h include/skq.h
+	@mkdir -p $(ABDIR)
+	$(HIPCC) $(HIPFLAGS) $(ABDEFS) -c $< -o $@
+$(ABDIR)/libskq.so: $(AB_KOBJS) $(filter-out $(OUT)/obj/skq_kernels.o $(OUT)/obj/skq_map1.o $(OUT)/obj/skq_map1_pass.o,$(LIB_OBJS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $^
+ab: $(ABDIR)/libskq.so
+.PHONY: ab
 
 # the command line (index / quant), src/main.cpp's interface
 # (several GPUs: HIP streams and RCCL from the host program; the HIP headers want the platform named)

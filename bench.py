@@ -48,6 +48,8 @@ def _args(argv=None):
     ap.add_argument("--chunk-mb", type=int, default=64, help="end to end: FASTQ chunk (MiB)")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the FASTQ-file -> EM leg reported beside the kernel path")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="N = 1, default config: skip the cfg2 and cfg5 legs reported under `configs`")
     ap.add_argument("--dist-backend", default="nccl",
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -89,6 +91,7 @@ from skq import synth  # noqa: E402
 METRIC = "reads/sec (quant, 150 bp, k=31) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GATHER_CEIL_GPS = 48.1  # random 32-B gathers per ns from an 8 GiB table (profiles/r1_gather_bench.log)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s (MI355X_MICROARCH.md: SIMD-32, 2 cycles each)
 
 CONFIGS = {
     "cfg2": dict(ntx=10_000, reads=1_000_000, read_len=100, ks=[31],
@@ -335,24 +338,16 @@ def cpu_model():
     return "unknown"
 
 
-def main(args):
-    cname = args.config or ("cfg3" if args.gpus == 1 else "cfg4")
-    cfg = dict(CONFIGS[cname])
-    if args.reads:
-        cfg["reads"] = args.reads
+def load_profile_json(name):
+    f = os.path.join(ROOT, "profiles", name)
+    return (json.load(open(f)), "profiles/" + name) if os.path.exists(f) else (None, None)
 
-    rank, world, local = sdist.world()
-    if world != args.gpus:
-        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
-    gpu = local % max(torch.cuda.device_count(), 1)  # one GPU per rank on a full node
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
 
+def measure(cname, cfg, args, rank, world, dev, gpu, sample, totals_dev=True):
+    """One config's leg on this rank's shard: setup (replicated index, seeded reads resident in HBM),
+    W untimed + K timed steps bracketed by a barrier and a device sync, then the sample (the first
+    `sample` reads mapped alone and exported) and the roofline figures. Returns (line fields,
+    context for the checks)."""
     L, ks, n = cfg["read_len"], cfg["ks"], cfg["reads"]
     t0 = time.time()
     tx = synth.transcriptome(cfg["ntx"], seed=1)  # identical on every rank: replicated index
@@ -366,8 +361,8 @@ def main(args):
     sp = C.c_void_p(stream.cuda_stream)
     totals = torch.zeros(2, tx.ntx, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
-    log("setup %.1fs: %d transcripts, %d reads x %d bp, index %s" % (
-        time.time() - t0, tx.ntx, n, L, index.stats()))
+    log("%s setup %.1fs: %d transcripts, %d reads x %d bp, index %s" % (
+        cname, time.time() - t0, tx.ntx, n, L, index.stats()))
 
     def step():
         sess.map(d_reads.data_ptr(), None, n, L, fixed_len=L, stream=sp)
@@ -399,7 +394,7 @@ def main(args):
     slow = sess.slow_counts()
 
     # the sample: the first m reads of this rank's batch, mapped alone (fresh totals), exported
-    m = min(n, args.cpu_reads)
+    m = min(n, sample)
     sess.reset_totals(sp)
     sess.map(d_reads.data_ptr(), None, m, L, fixed_len=L, stream=sp, accumulate=True)
     sess.check(sp)
@@ -441,55 +436,140 @@ def main(args):
     traffic, traffic_src = None, None
     # (cfg4 is cfg3's reads, index and k at 12.5M reads per GPU: its per-read traffic is cfg3's)
     tname = "cfg3" if cname == "cfg4" and not os.path.exists(os.path.join(ROOT, "profiles", "traffic_cfg4.json")) else cname
-    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % tname)
     probe = index.stats()["probe"]
-    if os.path.exists(tf):                               # PMC FETCH/WRITE passes (tools/traffic.py)
-        tr = json.load(open(tf))
+    chained = index.stats()["chained"] > 0
+    tr, tf = load_profile_json("traffic_%s.json" % tname)
+    if tr is not None:                                   # PMC FETCH/WRITE passes (tools/traffic.py)
         if kname in tr.get("kernels", {}) and tr.get("probe", probe) == probe and "calibration" in tr:
             traffic = tr["kernels"][kname]["hbm_bytes_per_read"] * n
-            traffic_src = "profiles/traffic_%s.json (%s)%s; %s" % (
-                tname, tr.get("measured", "builder's PMC passes"),
+            traffic_src = "%s (%s)%s; %s" % (
+                tf, tr.get("measured", "builder's PMC passes"),
                 ", per read, scaled to this launch's reads (cfg4 = cfg3's reads, index and k)" if tname != cname else "",
                 tr["calibration"])
+    # the second bound (K1 "may be ALU- rather than HBM-bound; report both"): the
+    # dominant kernel's vector instructions per read from committed PMC passes (SQ_INSTS_VALU over
+    # SQ_WAVES x 64 reads, tools/valu_counts.py) over this line's own launch time, against the
+    # chip's VALU issue peak
+    valu = None
+    vj, vf = load_profile_json("valu_%s.json" % tname)
+    if vj is not None and kname in vj.get("kernels", {}) and vj.get("probe", probe) == probe \
+            and vj.get("chained", chained) == chained:
+        vk = vj["kernels"][kname]
+        per_launch = vk["valu_per_read"] * n
+        va = per_launch / (avg[kname] * 1e-3)
+        valu = {"instructions_per_read": vk["valu_per_read"], "per_wave": vk["valu_per_read"] * 64,
+                "per_launch": per_launch, "achieved": va, "peak": VALU_PEAK, "unit": "wave64 VALU instructions/s",
+                "frac": va / VALU_PEAK, "salu_per_read": vk.get("salu_per_read"),
+                "source": "%s (%s)" % (vf, vj.get("measured", "builder's PMC passes")),
+                "peak_source": "MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction issues over 2 "
+                               "cycles, 2.4 GHz -> 1.229e12 wave-instructions/s"}
+    hbm_frac = achieved / HBM_PEAK_GBS
+    bound = "valu" if valu is not None and valu["frac"] > hbm_frac else "hbm"
     requests = None
     if map1:  # random index requests per launch against the measured gather ceiling
         rps = n * h / (avg[kname] * 1e-3) / 1e9
         requests = {"random_per_read": h, "achieved": rps, "ceiling": GATHER_CEIL_GPS, "unit": "G/s",
                     "frac": rps / GATHER_CEIL_GPS,
                     "ceiling_source": "tools/micro/gather_bench: random pair-cooperative 32-B gathers, 8 GiB table"}
-        if index.stats()["chained"] > 0:
+        if chained:
             requests["note"] = ("chained tables: random_per_read counts the hashes looked up; one 128-B chained "
-                                "entry per read (read by eight lanes together) settles ~2/3 of them and the rest "
+                                "entry per read (read by eight lanes together) settles most of them and the rest "
                                 "gather 32-B wide entries, so the memory-side requests are all_per_read; the bound "
                                 "is the VALU and the CUs' per-line address work, not this rate (DESIGN.md section 5)")
         if traffic is not None:  # every memory-side request of the launch, from the calibrated PMC passes
-            kt_ = json.load(open(tf))["kernels"][kname]
+            kt_ = tr["kernels"][kname]
             per = kt_["fetch_size_bytes_per_read"] / 64.0 + kt_["write_bytes_per_read"] / 64.0
             requests.update(all_per_read=per, all_achieved=n * per / (avg[kname] * 1e-3) / 1e9,
-                            all_note="read + write requests per read from profiles/traffic_%s.json (FETCH_SIZE "
-                                     "and WRITE_SIZE tally 64 B per request); random-gather rates measured: "
-                                     "46-49 G/s from HBM, 54-56 G/s from the Infinity Cache (DESIGN.md §5)" % tname)
-    total_reads = n * world * args.steps
-    value = total_reads / elapsed
+                            all_note="read + write requests per read from %s (FETCH_SIZE and WRITE_SIZE tally 64 B "
+                                     "per request); random-gather rates measured: 46-49 G/s from HBM, 54-56 G/s "
+                                     "from the Infinity Cache (DESIGN.md §5)" % tf)
+    value = n * world * args.steps / elapsed
+    line = {
+        "value": value, "ms_per_step": elapsed / args.steps * 1e3,
+        "roofline": {"bound": bound, "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": hbm_frac, "traffic": traffic,
+                     "bound_note": ("achieved / peak / frac are the HBM roofline on SURVEY.md 8(d)'s algorithmic "
+                                    "bytes; valu is the same launch against the VALU issue peak; bound names the "
+                                    "larger fraction"),
+                     "algorithmic_bytes": n * b_basis, "avg_launch_ms": avg[kname],
+                     "bytes_basis": ("SURVEY.md 8(d): L + 8h + 4P + 4h + 8C per read" if b_basis == b_path
+                                     else "kernel input/output bytes"),
+                     "kernel_io_bytes": n * b_kern[kname], "kernel_io_frac": kio / HBM_PEAK_GBS,
+                     "valu": valu, "requests": requests,
+                     "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None,
+                     "traffic_source": traffic_src},
+        "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + index gathers + count fused)" if map1 else
+                                            "fused in k_sketch" if fused else "k_probe"),
+                 "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
+                 "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
+                 "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn,
+                 "slow_reads_per_batch": {"sketch": slow[0], "chain": slow[1],
+                                          "past_the_wave_path": {"sketch": slow[2], "chain": slow[3]}}},
+    }
+    ctx = dict(tx=tx, tables=tables, index=index, bases=bases, d_reads=d_reads, sess=sess, sp=sp, gout=gout,
+               gtot=gtot, m=m, L=L, ks=ks, n=n)
+    return line, ctx
 
+
+def oracle_index(ctx):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc  # the CPU oracle: the checker and the CPU baseline, never the measured path
+    pairs = []
+    for k in ctx["ks"]:
+        keys, offs, tids = ctx["tables"][k]
+        pairs.append((np.repeat(keys, np.diff(offs.astype(np.int64))), tids))
+    return orc, orc.Index(ctx["ks"], pairs=pairs, ntx=ctx["tx"].ntx)
+
+
+def parity_sample(ctx, threads):
+    """The sample through the oracle from FASTQ text, bit-exact against the GPU's export; returns
+    (verdict, oracle index, FASTQ bytes, oracle seconds)."""
+    orc, oi = oracle_index(ctx)
+    m, L = ctx["m"], ctx["L"]
+    fq = synth.fastq_bytes(ctx["bases"][:m * L], L)
+    tc = time.perf_counter()
+    cout = orc.fastq_map(oi, fq, nthreads=threads, outputs=True, hcap=64, ccap=64)
+    dt = time.perf_counter() - tc
+    bad = parity_check(ctx["gout"], ctx["gtot"], cout, len(ctx["ks"]))
+    verdict = ("bit-exact, %d reads (status, retained-hash sets, candidate lists, per-transcript totals)" % m
+               if not bad else "MISMATCH: " + "; ".join(bad))
+    return verdict, (orc, oi), fq, dt
+
+
+def release(ctx):
+    ctx["sess"].free()
+    ctx["index"].free()
+    del ctx["d_reads"]
+    ctx.clear()
+    torch.cuda.empty_cache()
+
+
+def main(args):
+    cname = args.config or ("cfg3" if args.gpus == 1 else "cfg4")
+    cfg = dict(CONFIGS[cname])
+    if args.reads:
+        cfg["reads"] = args.reads
+
+    rank, world, local = sdist.world()
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    gpu = local % max(torch.cuda.device_count(), 1)  # one GPU per rank on a full node
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+
+    line, ctx = measure(cname, cfg, args, rank, world, dev, gpu, args.cpu_reads)
+    n, L = ctx["n"], ctx["L"]
     parity, cpu = None, None
     if rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import orc  # the CPU oracle: the checker and the CPU baseline, never the measured path
-        pairs = []
-        for k in ks:
-            keys, offs, tids = tables[k]
-            pairs.append((np.repeat(keys, np.diff(offs.astype(np.int64))), tids))
-        oi = orc.Index(ks, pairs=pairs, ntx=tx.ntx)
-        fq = synth.fastq_bytes(bases[:m * L], L)
         P_thr, ncpu, share_how = cpu_share(args, world)
-        tc = time.perf_counter()
-        cout = orc.fastq_map(oi, fq, nthreads=P_thr, outputs=True, hcap=64, ccap=64)
-        dt_p = time.perf_counter() - tc
-        bad = parity_check(gout, gtot, cout, nk)
-        parity = ("bit-exact, %d reads (status, retained-hash sets, candidate lists, per-transcript totals)" % m
-                  if not bad else "MISMATCH: " + "; ".join(bad))
+        parity, (orc, oi), fq, dt_p = parity_sample(ctx, P_thr)
         log("parity sample: %s" % parity)
+        m = ctx["m"]
         # (every N: rank 0 times the same oracle path on its host-core share while the other ranks
         # wait at the barrier below)
         cpu = {"value": m / dt_p, "unit": "reads/s", "cores": P_thr, "kind": "port",
@@ -511,50 +591,57 @@ def main(args):
         cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
         if os.path.exists(cal):  # reference sparse_chain vs the oracle's, timed in the build container
             cpu["calibration"] = json.load(open(cal)).get("summary")
+        del fq
     e2e = None
     if not args.no_end_to_end:
         try:
-            e2e = end_to_end(index, tx.ntx, bases, d_reads.data_ptr(), n, L, sess, sp, rank, world, dev,
-                             io_cfg=(args.io_threads, args.chunk_mb))
+            e2e = end_to_end(ctx["index"], ctx["tx"].ntx, ctx["bases"], ctx["d_reads"].data_ptr(), n, L, ctx["sess"],
+                             ctx["sp"], rank, world, dev, io_cfg=(args.io_threads, args.chunk_mb))
         except (OSError, skq.SkqError) as ex:  # (e.g. no room for the FASTQ file): the metric line still prints
             e2e = {"error": "%s: %s" % (type(ex).__name__, ex)}
         log("end to end: %s" % json.dumps(e2e))
     if world > 1:
         dist.barrier()
+    release(ctx)
+
+    # the other single-GPU configs of BASELINE.json, each with its own timed steps, roofline and
+    # parity sample (never `value`): cfg2 (100 bp, 10k transcripts) and cfg5 (multi-k)
+    extra = {}
+    bad_extra = False
+    if world == 1 and args.config is None and not args.reads and not args.no_extra_configs:
+        for xc, xs in (("cfg2", 1_000_000), ("cfg5", 1_000_000)):
+            xl, xctx = measure(xc, dict(CONFIGS[xc]), args, rank, world, dev, gpu, xs)
+            xp, _, _, _ = parity_sample(xctx, cpu_share(args, world)[0])
+            log("%s: %.3g reads/s, %.3f ms per step, parity sample: %s" % (xc, xl["value"], xl["ms_per_step"], xp))
+            bad_extra |= xp.startswith("MISMATCH")
+            xl.update(config={"workload": xc + ": " + CONFIGS[xc]["desc"], "reads_per_gpu": CONFIGS[xc]["reads"],
+                              "read_len": CONFIGS[xc]["read_len"], "transcripts": CONFIGS[xc]["ntx"],
+                              "ks": CONFIGS[xc]["ks"]},
+                      steps=args.steps, warmup=args.warmup, parity_sample=xp)
+            extra[xc] = xl
+            release(xctx)
 
     if rank == 0:
         res = {
-            "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "metric": METRIC, "value": line["value"], "unit": "reads/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": line["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": cname + ": " + cfg["desc"], "reads_per_gpu": n, "read_len": L,
-                       "transcripts": tx.ntx, "ks": ks, "sketch_fraction": "(double)0.05f",
+                       "transcripts": cfg["ntx"], "ks": cfg["ks"], "sketch_fraction": "(double)0.05f",
                        "chain_fraction": 0.9, "parallelism": "read-sharded x%d, index replicated" % world
                        + (", 1 all-reduce of per-transcript totals per step" if world > 1 else "")},
-            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes": n * b_basis, "avg_launch_ms": avg[kname],
-                         "bytes_basis": ("SURVEY.md 8(d): L + 8h + 4P + 4h + 8C per read" if b_basis == b_path
-                                         else "kernel input/output bytes"),
-                         "kernel_io_bytes": n * b_kern[kname], "kernel_io_frac": kio / HBM_PEAK_GBS,
-                         "requests": requests,
-                         "traffic_GBps": traffic / (avg[kname] * 1e-3) / 1e9 if traffic else None,
-                         "traffic_source": traffic_src},
-            "path": {"bytes_per_read": b_path, "probe": (fused_name + " (sketch + index gathers + count fused)" if map1 else
-                                                "fused in k_sketch" if fused else "k_probe"),
-                     "index": index.stats(), "achieved_GBps": value / world * b_path / 1e9,
-                     "frac": value / world * b_path / 1e9 / HBM_PEAK_GBS,
-                     "kernel_ms": avg, "kernel_bytes_per_read": b_kern, "h": h, "P": P, "C": Cn,
-                     "slow_reads_per_batch": {"sketch": slow[0], "chain": slow[1],
-                                              "past_the_wave_path": {"sketch": slow[2], "chain": slow[3]}}},
+            "roofline": line["roofline"],
+            "path": line["path"],
             "parity_sample": parity,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
         }
+        if extra:
+            res["configs"] = extra
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if parity is not None and parity.startswith("MISMATCH"):
+    if (parity is not None and parity.startswith("MISMATCH")) or bad_extra:
         raise SystemExit(3)
     if e2e is not None and e2e.get("check") == "MISMATCH":
         raise SystemExit(4)

@@ -91,6 +91,9 @@ int skq_index_create_chained(int device, uint32_t ntx, uint32_t nk, const uint32
                              uint32_t nseq, uint32_t threshold, skq_index** out);
 /* 0: no chained tables; else 1 + the mean successor records per entry */
 double skq_index_chained(const skq_index* ix);
+/* the chained tables' host build: seconds this index spent building entries (0 when it took them
+ * from another device's build of the same tables), and the host peak of one k slot's build (bytes) */
+int skq_index_chain_build(const skq_index* ix, double* host_seconds, uint64_t* host_peak_bytes);
 
 /* A session owns the device workspace for batches of up to max_reads reads of at most
  * max_len bases each (longer reads are still handled exactly, by the slow path). Indexes of

@@ -5,7 +5,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <future>
 #include <cmath>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -83,6 +86,8 @@ struct skq_index {
     uint64_t chain_len[SKQ_MAX_K] = {};
     uint64_t chain_bytes = 0;
     double chain_succ = 0;  // mean successor records per entry over the slots' tables (stats)
+    double chain_build_s = 0;      // host seconds building the chained entries (this index's share)
+    uint64_t chain_host_bytes = 0;  // host peak of one slot's build: entries + sorted candidates
     uint32_t chain_slots = 0;
     // 1 = dir tables, 2 = rank tables (the sketch probes), 3 = wide tables, 5 = compact tables
     // (4 was the block tables, retired in round 3: compact tables are smaller and faster)
@@ -516,20 +521,42 @@ static uint32_t chain_entry(uint32_t* e, uint32_t key, uint32_t off, const std::
     return taken;
 }
 
-int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
-                const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
-                uint32_t nseq, uint32_t threshold) {
+// The host side of one k slot's chained table: the entries of the present keys (128 B each) and
+// their successor count. Indexes built at once on several devices from the same tables (the CLI's
+// one thread per device) share one build: the first caller builds, the others wait for it, and the
+// entries are dropped when the last of them has uploaded its table.
+struct ChainHost {
+    std::vector<uint32_t> ent;
+    uint64_t nsucc = 0;
+    double seconds = 0;  // host build time
+    uint64_t triples = 0;  // (key, successor, hop) candidates sorted (host peak: 12 B each + ent)
+};
+struct ChainKey {
+    const void* seqs;
+    const void* offs;
+    const void* lists;
+    uint64_t nseq, k, thr, m, last, nlists;
+    bool operator==(const ChainKey& o) const {
+        return seqs == o.seqs && offs == o.offs && lists == o.lists && nseq == o.nseq && k == o.k && thr == o.thr &&
+               m == o.m && last == o.last && nlists == o.nlists;
+    }
+};
+struct ChainShare {
+    ChainKey key;
+    std::shared_future<std::shared_ptr<const ChainHost>> fut;
+    int users;
+};
+static std::mutex g_chain_mu;
+static std::vector<ChainShare> g_chain_share;
+
+static std::shared_ptr<const ChainHost> chain_host_build(const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
+                                                        const std::vector<uint32_t>& lists, uint32_t k,
+                                                        const uint8_t* seqs, const uint64_t* offs, uint32_t nseq,
+                                                        uint32_t threshold) {
+    const auto t0 = std::chrono::steady_clock::now();
+    auto out = std::make_shared<ChainHost>();
     const uint64_t m = keys.size();
-    if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key ^ CHN_KEY_LIMIT)
     const uint64_t len = (uint64_t)keys.back() + 1;
-    // 128 B per possible key, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
-    uint64_t budget = 65536ull << 20;
-    if (const char* e = std::getenv("SKQ_CHAIN_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
-    size_t fr = 0, tot = 0;
-    // (half of what is free past a 32 GiB reserve for sessions: several indexes may share a device)
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < (32ull << 30) || len * 128 > (fr - (32ull << 30)) / 2 ||
-        len * 128 > budget)
-        return 0;
     const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // (key, successor, hop) triples, bucketed by key range, one sort per bucket
     constexpr uint32_t NB = 256;
@@ -559,7 +586,10 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
             });
         for (auto& t : pool) t.join();
     }
-    std::vector<uint32_t> ent(m * skq::CHAIN_WORDS, 0);
+    for (auto& pw : part)
+        for (auto& pb : pw) out->triples += pb.size();
+    std::vector<uint32_t>& ent = out->ent;
+    ent.assign(m * skq::CHAIN_WORDS, 0);
     std::vector<uint8_t> built(m, 0);
     std::atomic<uint64_t> nsucc{0};
     auto index_of = [&](uint32_t key) -> int64_t {
@@ -608,6 +638,82 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
     // keys no transcript of `seqs` retained still get their own record
     for (uint64_t x = 0; x < m; ++x)
         if (!built[x]) chain_entry(ent.data() + x * skq::CHAIN_WORDS, keys[x], vals[x], lists, nullptr, nullptr, 0);
+    out->nsucc = nsucc.load();
+    out->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return out;
+}
+
+// one line on stderr per (k, reason) the first time a k slot keeps the wide entries alone
+static void chain_note(uint32_t k, const char* why, uint64_t need, uint64_t fr) {
+    static std::mutex mu;
+    static std::vector<std::pair<uint32_t, std::string>> seen;
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& x : seen)
+        if (x.first == k && x.second == why) return;
+    seen.emplace_back(k, why);
+    std::fprintf(stderr, "[skq] k=%u: no chained table (%s: %.1f GB needed, %.1f GB free on the device); the k slot "
+                 "keeps the wide entries\n", k, why, need / 1e9, fr / 1e9);
+}
+
+int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
+                const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
+                uint32_t nseq, uint32_t threshold) {
+    const uint64_t m = keys.size();
+    if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key ^ CHN_KEY_LIMIT)
+    const uint64_t len = (uint64_t)keys.back() + 1;
+    // 128 B per possible key, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
+    uint64_t budget = 65536ull << 20;
+    if (const char* e = std::getenv("SKQ_CHAIN_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
+    size_t fr = 0, tot = 0;
+    // (half of what is free past a 32 GiB reserve for sessions: several indexes may share a device)
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < (32ull << 30) || len * 128 > (fr - (32ull << 30)) / 2 ||
+        len * 128 > budget) {
+        chain_note(k, len * 128 > budget ? "over SKQ_CHAIN_MB" : "past half the free memory above 32 GiB", len * 128, fr);
+        return 0;
+    }
+    // the host entries: shared with the other devices building the same tables at the same time
+    const ChainKey key{seqs, offs, &lists, nseq, k, threshold, m, len, lists.size()};
+    std::shared_future<std::shared_ptr<const ChainHost>> fut;
+    std::promise<std::shared_ptr<const ChainHost>> prom;
+    bool builder = false;
+    {
+        std::lock_guard<std::mutex> g(g_chain_mu);
+        for (auto& x : g_chain_share)
+            if (x.key == key) {
+                fut = x.fut;
+                ++x.users;
+            }
+        if (!fut.valid()) {
+            fut = prom.get_future().share();
+            g_chain_share.push_back({key, fut, 1});
+            builder = true;
+        }
+    }
+    if (builder) {
+        try {
+            prom.set_value(chain_host_build(keys, vals, lists, k, seqs, offs, nseq, threshold));
+        } catch (...) {
+            prom.set_exception(std::current_exception());
+        }
+    }
+    std::shared_ptr<const ChainHost> hc;
+    try {
+        hc = fut.get();
+    } catch (...) {
+        hc = nullptr;
+    }
+    auto done_with = [&] {
+        std::lock_guard<std::mutex> g(g_chain_mu);
+        for (size_t i = 0; i < g_chain_share.size(); ++i)
+            if (g_chain_share[i].key == key && --g_chain_share[i].users == 0) {
+                g_chain_share.erase(g_chain_share.begin() + (ptrdiff_t)i);
+                break;
+            }
+    };
+    if (!hc) {
+        done_with();
+        return fail(-3, "chained table build failed (host)");
+    }
     uint32_t* dk = nullptr;
     uint4* de = nullptr;
     uint4*& dch = ix->d_chain[slot];
@@ -617,25 +723,32 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
         dev_free(de);
         dev_free(dch);
         (void)hipGetLastError();
+        done_with();
+        chain_note(k, "allocation failed", len * 128, fr);
         return 0;
     }
     hipStream_t st = nullptr;
     const bool ok = hipMemsetAsync(dch, 0, len * 128, st) == hipSuccess &&
                     hipMemcpy(dk, keys.data(), m * 4, hipMemcpyHostToDevice) == hipSuccess &&
-                    hipMemcpy(de, ent.data(), m * 128, hipMemcpyHostToDevice) == hipSuccess;
+                    hipMemcpy(de, hc->ent.data(), m * 128, hipMemcpyHostToDevice) == hipSuccess;
     if (ok) {
         hipLaunchKernelGGL(k_chain_scatter, dim3((unsigned)((m * 8 + 255) / 256)), dim3(256), 0, st, dch, dk, de, m);
     }
     const bool done = ok && hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
     dev_free(dk);
     dev_free(de);
+    const uint64_t nsucc = hc->nsucc;
+    ix->chain_build_s += builder ? hc->seconds : 0.0;
+    ix->chain_host_bytes = std::max<uint64_t>(ix->chain_host_bytes, hc->ent.size() * 4 + hc->triples * 12);
+    hc.reset();
+    done_with();
     if (!done) {
         dev_free(dch);
         return fail(-3, "chained table build failed");
     }
     ix->chain_len[slot] = len;
     ix->chain_bytes += len * 128;
-    ix->chain_succ = (ix->chain_succ * ix->chain_slots + (double)nsucc.load() / (double)m) / (ix->chain_slots + 1);
+    ix->chain_succ = (ix->chain_succ * ix->chain_slots + (double)nsucc / (double)m) / (ix->chain_slots + 1);
     ++ix->chain_slots;
     return 0;
 }
@@ -953,6 +1066,13 @@ int skq_session_slow_counts(skq_session* s, uint32_t* counts) {
 int skq_index_direct(const skq_index* ix) { return ix && ix->direct ? ix->mode : 0; }
 double skq_index_chained(const skq_index* ix) { return ix && ix->chain_slots ? 1.0 + ix->chain_succ : 0.0; }
 
+int skq_index_chain_build(const skq_index* ix, double* host_seconds, uint64_t* host_peak_bytes) {
+    if (!ix) return fail(-1, "null index");
+    if (host_seconds) *host_seconds = ix->chain_build_s;
+    if (host_peak_bytes) *host_peak_bytes = ix->chain_host_bytes;
+    return 0;
+}
+
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
     if (!ix || !out) return fail(-1, "null argument");
     *out = nullptr;
@@ -1223,6 +1343,24 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
     return 0;
 }
 
+// SKQ_ABLATE (development phase pricing: k_map1 skips phases, so results are WRONG) is honoured
+// only beside SKQ_DEV=1, and announced once on stderr whenever it is active
+static uint32_t ablate_mask() {
+    static const uint32_t m = [] {
+        const char* e = std::getenv("SKQ_ABLATE");
+        const char* dev = std::getenv("SKQ_DEV");
+        if (!e || !*e) return 0u;
+        const uint32_t v = (uint32_t)std::strtoul(e, nullptr, 0);
+        if (!dev || std::atoi(dev) != 1) {
+            std::fprintf(stderr, "[skq] SKQ_ABLATE=%s ignored (a development switch: set SKQ_DEV=1 as well)\n", e);
+            return 0u;
+        }
+        if (v) std::fprintf(stderr, "[skq] SKQ_ABLATE=0x%x ACTIVE: k_map1 skips phases, results are wrong\n", v);
+        return v;
+    }();
+    return m;
+}
+
 static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const uint32_t* hash_cnt,
                       const uint32_t* hashes, const uint64_t* hash_offs, const uint8_t* present,
                       uint32_t hcap, double fraction, int accumulate, bool probed, void* stream,
@@ -1284,7 +1422,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
         p.chain_len[i] = ix->chain_len[i];
     }
     p.stamps = s->stamps;
-    if (const char* e = std::getenv("SKQ_ABLATE")) p.ablate = (uint32_t)std::strtoul(e, nullptr, 0);
+    p.ablate = ablate_mask();
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
     p.bin_nb = s->bin_nb;

@@ -59,9 +59,20 @@ std::mutex g_mu;
 skq_sketcher* g_sk = nullptr;
 std::vector<uint32_t> g_buf;
 
+// at exit the resident server is told to leave and waited for (registered after the HIP runtime
+// initialised, so it runs before the runtime's own teardown)
+void free_sketcher() {
+    std::lock_guard<std::mutex> lock(g_mu);
+    if (g_sk) skq_sketcher_free(g_sk);
+    g_sk = nullptr;
+}
+
 std::unordered_set<uint32_t> gpu_sketch(const std::string& seq, int k, uint32_t threshold) {
     std::lock_guard<std::mutex> lock(g_mu);
-    if (!g_sk) check(skq_sketcher_create(device(), 4096, &g_sk));
+    if (!g_sk) {
+        check(skq_sketcher_create(device(), 4096, &g_sk));
+        std::atexit(free_sketcher);
+    }
     const uint64_t nw = seq.size() >= (size_t)k ? seq.size() - (size_t)k + 1 : 0;
     if (g_buf.size() < nw + 1) g_buf.resize(nw + 1);
     uint64_t n = 0;

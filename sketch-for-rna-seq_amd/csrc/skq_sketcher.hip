@@ -34,7 +34,7 @@ int sfail(int code, const std::string& msg) {
     } while (0)
 
 constexpr uint32_t SK_WG = 256;
-constexpr uint32_t SK_LDS_MAX = 48 * 1024;  // sequences staged in LDS; longer ones are read in place
+constexpr uint32_t SK_LDS_MAX = 48 * 1024;  // the LDS tile of a sequence's bytes
 
 // bytes -> 2-bit code, 4 = a byte ntHash skips
 __device__ __forceinline__ uint32_t sk_code(uint8_t b) {
@@ -119,18 +119,7 @@ __global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_
         if (!s_cmd[0]) return;
         const uint32_t len = s_cmd[1], k = s_cmd[2], thr = s_cmd[3];
         const uint32_t cap = min(len >= k && k ? len - k + 1 : 0u, ocap);
-        const bool staged = len <= SK_LDS_MAX;
-        if (staged) {  // (the host buffer is 16-B aligned and padded to 16 B)
-            const uint4* s4 = reinterpret_cast<const uint4*>(src);
-            uint4* d4 = reinterpret_cast<uint4*>(s_seq);
-            for (uint32_t q = t; q < (len + 15) / 16; q += SK_WG)
-                d4[q] = s4[q];
-        }
-        __syncthreads();
-        const uint8_t* s = staged ? s_seq : src;
         const uint32_t nw = len >= k && k ? len - k + 1 : 0;
-        // a chunk of windows per thread, rolled from its first base
-        const uint32_t chunk = max(1u, (nw + SK_WG - 1) / SK_WG);
         uint64_t seed[4], rk[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -138,30 +127,51 @@ __global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_
             const uint32_t d = k % 33;
             rk[c] = d ? (((skq::SEED33[c] << d) | (skq::SEED33[c] >> (33 - d))) & skq::M33) : skq::SEED33[c];
         }
-        for (uint32_t w0 = t * chunk; w0 < nw; w0 += SK_WG * chunk) {
-            uint64_t h = 0;
-            uint32_t run = 0;  // valid bases ending at p, counted from w0
-            const uint32_t pend = min(len, w0 + chunk + k - 1);
-            for (uint32_t p = w0; p < pend; ++p) {
-                const uint32_t c = s_code[s[p]];
-                if (c == 4) {
-                    run = 0;
-                    h = 0;
-                    continue;
-                }
-                ++run;
-                h = ((h << 1) | (h >> 32)) & skq::M33;
-                h ^= seed[c];
-                if (run > k) h ^= rk[s_code[s[p - k]]];
-                if (run >= k && (uint32_t)h <= thr) {  // src/sketch.cpp:33-35
-                    const uint32_t at = atomicAdd(&s_cnt, 1u);
-                    if (at < cap) out[1 + at] = (uint32_t)h;
+        // the windows in tiles whose bytes (the tile's windows and the k - 1 bases after them) are
+        // staged in LDS once, so a long sequence (a transcript at the index side) is read from the
+        // link in 16-B pieces, not byte by byte per window (k past half the LDS: read in place)
+        const bool tiled = k <= SK_LDS_MAX / 2;
+        const uint32_t tw = tiled ? (SK_LDS_MAX - k) & ~15u : (nw ? nw : 1u);  // windows per tile (16-B aligned)
+        for (uint32_t t0 = 0; t0 < nw; t0 += tw) {
+            const uint32_t tn = min(tw, nw - t0);
+            if (tiled) {  // (the host buffer is 16-B aligned and padded to 16 B)
+                const uint32_t b1 = min(len, t0 + tn + k - 1);
+                const uint4* s4 = reinterpret_cast<const uint4*>(src + t0);
+                uint4* d4 = reinterpret_cast<uint4*>(s_seq);
+                for (uint32_t q = t; q < (b1 - t0 + 15) / 16; q += SK_WG) d4[q] = s4[q];
+                __syncthreads();
+            }
+            const uint8_t* s = tiled ? s_seq - t0 : src;  // (indexed by sequence position)
+            // a chunk of the tile's windows per thread, rolled from its first base
+            const uint32_t chunk = max(1u, (tn + SK_WG - 1) / SK_WG);
+            for (uint32_t w0 = t0 + t * chunk; w0 < t0 + tn; w0 += SK_WG * chunk) {
+                uint64_t h = 0;
+                uint32_t run = 0;  // valid bases ending at p, counted from w0
+                const uint32_t pend = min(min(len, w0 + chunk + k - 1), t0 + tn + k - 1);
+                for (uint32_t p = w0; p < pend; ++p) {
+                    const uint32_t c = s_code[s[p]];
+                    if (c == 4) {
+                        run = 0;
+                        h = 0;
+                        continue;
+                    }
+                    ++run;
+                    h = ((h << 1) | (h >> 32)) & skq::M33;
+                    h ^= seed[c];
+                    if (run > k) h ^= rk[s_code[s[p - k]]];
+                    if (run >= k && (uint32_t)h <= thr) {  // src/sketch.cpp:33-35
+                        const uint32_t at = atomicAdd(&s_cnt, 1u);
+                        if (at < cap) out[1 + at] = (uint32_t)h;
+                    }
                 }
             }
+            __syncthreads();  // (the tile's bytes are dead)
         }
+        // every thread releases its own hash stores at system scope before the barrier, so thread
+        // 0's count and done words, stored after it, reach the host after all of them
+        __threadfence_system();
         __syncthreads();
         if (t == 0) {
-            __threadfence_system();  // (the hashes reach the host before the words that release them)
             sys_store(out, s_cnt);
             sys_store(&m->done, last);
         }
@@ -278,9 +288,12 @@ int skq_sketcher_run(skq_sketcher* h, const char* seq, uint64_t len, uint32_t k,
         m->thr = threshold;
         uint32_t r = h->seq + 1;
         if (r == 0) r = 1;  // (never a request of 0... nor the previous one)
-        __atomic_store_n(&m->req, r, __ATOMIC_RELEASE);
+        // (sequentially consistent: a release store followed by an acquire load may be reordered
+        // on x86, and the server does the mirror image — clears alive, then rereads req — so both
+        // sides could read stale words and the request would wait for the slow-path check)
+        __atomic_store_n(&m->req, r, __ATOMIC_SEQ_CST);
         h->seq = r;
-        if (!h->running || !__atomic_load_n(&m->alive, __ATOMIC_ACQUIRE)) {
+        if (!h->running || !__atomic_load_n(&m->alive, __ATOMIC_SEQ_CST)) {
             // no server, or one that has gone idle: wait for it to leave unless it took this request
             // on its way out, then launch one (it serves the pending request first)
             while (h->running && __atomic_load_n(&m->done, __ATOMIC_ACQUIRE) != r) {

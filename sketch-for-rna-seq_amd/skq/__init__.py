@@ -54,6 +54,7 @@ def lib():
             "skq_index_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32)]),
             "skq_index_direct": (i32, [vp]),
             "skq_index_chained": (C.c_double, [vp]),
+            "skq_index_chain_build": (i32, [vp, C.POINTER(C.c_double), C.POINTER(u64)]),
             "skq_index_create_chained": (i32, [i32, u32, u32, vp, u32, vp, vp, vp, u32, u32, C.POINTER(vp)]),
             "skq_session_slow_reads": (i32, [vp, C.POINTER(u32), C.POINTER(u32)]),
             "skq_session_slow_counts": (i32, [vp, C.POINTER(u32)]),
@@ -225,10 +226,13 @@ class Index:
     def stats(self):
         b, n, m = C.c_uint64(), C.c_uint64(), C.c_uint32()
         _check(lib().skq_index_stats(self.h, C.byref(b), C.byref(n), C.byref(m)))
+        cs, cb = C.c_double(), C.c_uint64()
+        _check(lib().skq_index_chain_build(self.h, C.byref(cs), C.byref(cb)))
         return dict(device_bytes=b.value, postings=n.value, max_list=m.value,
                     direct=bool(lib().skq_index_direct(self.h)),
                     probe={0: "bucket", 1: "dir", 2: "rank", 3: "wide", 5: "compact"}[lib().skq_index_direct(self.h)],
-                    chained=lib().skq_index_chained(self.h))
+                    chained=lib().skq_index_chained(self.h), chain_build_s=round(cs.value, 3),
+                    chain_host_peak_bytes=cb.value)
 
     def free(self):
         if self.h:

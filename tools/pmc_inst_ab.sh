@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for pr in $probes; do
   for v in $vals; do
     tag=$(echo "$pr" | tr '/' '_')_$v
-    SKQ_ABLATE=$v timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/$tag/p1" -o run -- python3 tools/kbench.py --probes "$pr" --rounds 2 > "$out/$tag.log" 2>&1 || { echo "pass $tag failed rc=$?"; tail -5 "$out/$tag.log"; exit 1; }
+    SKQ_DEV=1 SKQ_ABLATE=$v timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/$tag/p1" -o run -- python3 tools/kbench.py --probes "$pr" --rounds 2 > "$out/$tag.log" 2>&1 || { echo "pass $tag failed rc=$?"; tail -5 "$out/$tag.log"; exit 1; }
     echo "== $tag"; python3 tools/pmc_summary.py "$out/$tag" | grep -A12 "k_map1"
   done
 done
