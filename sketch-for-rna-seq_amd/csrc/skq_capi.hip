@@ -127,6 +127,11 @@ struct skq_session {
     uint32_t* cand_cnt = nullptr;
     uint32_t* cand_tid = nullptr;
     uint32_t* cand_score = nullptr;
+    // the fused map's packed candidates, by batch parity when the totals run on the side stream
+    // (k_bin_packed there reads one batch's pair while the next batch's map writes the other):
+    // [0] the arrays above, [1] allocated on first use; cand_cnt / cand_tid point at the current pair
+    uint32_t* cand_cnt_b[2] = {};
+    uint32_t* cand_tid_b[2] = {};
     uint32_t* cand_ext = nullptr;
     uint64_t cand_ext_cap = 0;
     uint64_t* scratch = nullptr;
@@ -1106,6 +1111,8 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
         skq_session_free(s);
         return rc;
     }
+    s->cand_cnt_b[0] = s->cand_cnt;
+    s->cand_tid_b[0] = s->cand_tid;
     // totals buckets: at most WG buckets of at most 2^14 ids (the LDS histogram), else direct
     if (const char* e = std::getenv("SKQ_BIN_BITS")) s->bin_bits = (uint32_t)std::max(8, std::min(14, std::atoi(e)));  // (A/B)
     while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
@@ -1161,9 +1168,13 @@ int skq_session_free(skq_session* s) {
     dev_free(s->ovf2);
     dev_free(s->ovf3);
     dev_free(s->ovf4);
+    if (s->cand_cnt_b[0]) s->cand_cnt = s->cand_cnt_b[0];  // (the current pair may be the second)
+    if (s->cand_tid_b[0]) s->cand_tid = s->cand_tid_b[0];
     dev_free(s->cand_cnt);
     dev_free(s->cand_tid);
     dev_free(s->cand_score);
+    dev_free(s->cand_cnt_b[1]);
+    dev_free(s->cand_tid_b[1]);
     dev_free(s->cand_ext);
     dev_free(s->scratch);
     for (int b = 0; b < 2; ++b) {
@@ -1297,18 +1308,26 @@ static int ensure_side(skq_session* s) {
     return 0;
 }
 
+// (small batches: the extra stream hand-offs cost more than the overlap gains; with the grouped
+// k_bin_sum for few buckets, 1M reads run 5 % faster forked, 10M reads too)
+static bool totals_fork(const skq::ChainParams& p, int accumulate) {
+    return accumulate && p.slow_totals && p.n >= (1u << 19);
+}
+
+// bins already written for this batch (the count kernels' epilogue, or k_map1's with map_bins);
+// else launch_bin writes them (k_bin, or k_bin_packed over the fused map's packed candidates)
+static int binned(const skq::ChainParams& p) { return p.slow_totals && (!p.cpack || p.map_bins) ? 1 : 0; }
+
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
                       hipStream_t st) {
-    // (small batches: the extra stream hand-offs cost more than the overlap gains; with the
-    // grouped k_bin_sum for few buckets, 1M reads run 5 % faster forked, 10M reads too)
-    const bool fork = accumulate && p.slow_totals && p.n >= (1u << 19);
+    const bool fork = totals_fork(p, accumulate);
     hipEvent_t t0{};
     if (fork) {
         if (int rc = ensure_side(s)) return rc;
         HIP_TRY(hipEventRecord(s->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
         record(s, 3, &t0, s->side);
-        if (skq::launch_bin(p, 1, s->side) ||
+        if (skq::launch_bin(p, binned(p), s->side) ||
             skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, s->side))
             return fail(-3, "totals launch failed");
         record_stop(s, 3, t0, s->side);
@@ -1334,13 +1353,23 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
     if (accumulate && !fork) {
         if (int rc = wait_totals(s, st)) return rc;  // (tx_acc: an earlier batch's fold may be pending)
         record(s, 3, &t0, st);
-        if (skq::launch_bin(p, p.slow_totals, st) ||
+        if (skq::launch_bin(p, binned(p), st) ||
             skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, st))
             return fail(-3, "totals launch failed");
         record_stop(s, 3, t0, st);
     }
     if (accumulate && p.bin_nb) s->bin_par ^= 1;  // this batch's bins were written
     return 0;
+}
+
+// SKQ_MAP_BINS=1 (development A/B): k_map1 bins its candidates in its own epilogue (round 4)
+// instead of k_bin_packed after it
+static int map_bins_dev() {
+    static const int v = [] {
+        const char* e = std::getenv("SKQ_MAP_BINS");
+        return e && std::atoi(e) == 1 ? 1 : 0;
+    }();
+    return v;
 }
 
 // SKQ_ABLATE (development phase pricing: k_map1 skips phases, so results are WRONG) is honoured
@@ -1368,6 +1397,11 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const skq_index* ix = s->idx;
+    if (!prep && s->cand_tid_b[0]) {  // (two-kernel path: the first candidate pair, once no side-stream reader has it)
+        if (int rc = wait_totals(s, st)) return rc;
+        s->cand_cnt = s->cand_cnt_b[0];
+        s->cand_tid = s->cand_tid_b[0];
+    }
     skq::ChainParams p{};
     p.n = n;
     p.nk = ix->nk;
@@ -1518,10 +1552,30 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     // candidates packed too, unless the totals would be binned from the padded rows (k_bin)
     s->cand_packed = s->hash_packed && (!accumulate || cp.slow_totals);
     cp.cpack = s->cand_packed ? 1u : 0u;
+    cp.map_bins = map_bins_dev();
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
     if (int rc = wait_bins(s, st)) return rc;
+    // the candidate pair: this batch's parity when k_bin_packed will read it on the side stream
+    // (wait_bins above has waited for the batch two back, the last reader of that pair); else the
+    // first pair, once every side-stream reader is done
+    uint32_t par = 0;
+    const bool side_bins = totals_fork(cp, accumulate) && cp.cpack && !cp.map_bins;
+    if (side_bins && s->bin_par == 1) {
+        if (!s->cand_tid_b[1]) {
+            if (dev_alloc(&s->cand_tid_b[1], s->max_reads * skq::CCAP) || dev_alloc(&s->cand_cnt_b[1], s->max_reads)) {
+                dev_free(s->cand_tid_b[1]);
+                dev_free(s->cand_cnt_b[1]);
+                (void)hipGetLastError();
+            }
+        }
+        if (s->cand_tid_b[1]) par = 1;
+    }
+    if (!side_bins || par != s->bin_par)
+        if (int rc = wait_totals(s, st)) return rc;
+    s->cand_cnt = cp.cand_cnt = s->cand_cnt_b[par];
+    s->cand_tid = cp.cand_tid = s->cand_tid_b[par];
     hipEvent_t t0{};
     record(s, 0, &t0, st);
     int rc = 0;

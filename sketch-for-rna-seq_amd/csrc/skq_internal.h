@@ -185,6 +185,9 @@ struct ChainParams {
     uint32_t* bin_hdr;
     uint32_t* bin_region;
     int slow_totals;
+    // the fused map bins its candidates in its own epilogue (1; round 4) or leaves them packed for
+    // k_bin_packed, which runs after it (0: the default)
+    int map_bins;
     uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
     uint32_t ablate;           // development (SKQ_ABLATE, results WRONG when set): k_map1 phases
                                // skipped to price them: 2 entry-list gathers, 4 filter/order/candidate

@@ -2682,6 +2682,72 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
     for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
+// The fused map's candidates (per-wave packed layout, ChainParams::cpack: tid | score << 22) binned
+// for the totals, one workgroup per map workgroup (the same regions and headers k_map1 used to fill
+// in its epilogue): the map kernel ends at its last candidate store and this runs after it (on the
+// session's side stream for large batches, beside the next batch's map; the candidate buffers
+// alternate by batch parity, so that map writes the other pair). A read the slow paths took has
+// no share of its wave's region (its count word is 0 or, once they have run, a CAND_EXT mark) and
+// adds its totals itself.
+__global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW,
+                                                   uint32_t* hdr, uint32_t* region) {
+    __shared__ uint32_t s_bc[WG + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s_reg[WG * CCAP];
+    const uint32_t t = threadIdx.x, w = blockIdx.x, lane = t & 63;
+    const uint64_t r = (uint64_t)w * WG + t;
+    s_bc[t] = 0;
+    if (t == 0) s_bc[WG] = 0;
+    const uint32_t c = r < p.n ? p.cand_cnt[r] : 0u;
+    const uint32_t nc = (c & CAND_EXT) ? 0u : min(c, (uint32_t)CCAP);
+    const uint32_t incl = wave_incl_scan(nc, lane);
+    const uint32_t* src = p.cand_tid + (r - lane) * CCAP + (incl - nc);
+    uint32_t key[CCAP];
+#pragma unroll
+    for (int d = 0; d < CCAP; ++d) {
+        if (!__any((uint32_t)d < nc)) break;  // (uniform: the wave's longest list)
+        key[d] = (uint32_t)d < nc ? src[d] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < CCAP; ++d)
+        if ((uint32_t)d < nc) atomicAdd(&s_bc[(key[d] & 0x3FFFFFu) >> bits], 1u);
+    __syncthreads();
+    if (t < 64) {  // one wave scans the (<= 256) bucket counts, 4 per lane
+        uint32_t c4[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = 4 * t + u;
+            c4[u] = b < nb ? s_bc[b] : 0u;
+            sum += c4[u];
+        }
+        const uint32_t bi = wave_incl_scan(sum, t);
+        uint32_t run = bi - sum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = 4 * t + u;
+            if (b < nb) {
+                hdr[(uint64_t)b * nW + w] = run;
+                s_bc[b] = run;
+            }
+            run += c4[u];
+        }
+        if (t == 63) hdr[(uint64_t)nb * nW + w] = bi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < CCAP; ++d) {
+        if ((uint32_t)d >= nc) continue;
+        const uint32_t tid = key[d] & 0x3FFFFFu, score = key[d] >> 22;
+        const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
+        s_reg[pos] = (tid & ((1u << bits) - 1u)) | (score << bits);
+    }
+    __syncthreads();
+    const uint32_t total = s_bc[nb - 1];
+    uint4* reg = reinterpret_cast<uint4*>(region + (uint64_t)w * (WG * CCAP));
+    const uint4* sr = reinterpret_cast<const uint4*>(s_reg);
+    for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
+}
+
 // the workgroup's bins out: to its slab slot with plain coalesced stores (k_fold_slab sums the
 // chunks: ~0.2M atomics in all instead of ~4M, one per non-empty bin of every workgroup), or
 // with atomics into tx_acc
@@ -3000,7 +3066,10 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     const uint32_t* region = p.bin_region;
     if (nb > (uint32_t)WG) return -1;
     if (!binned) {
-        hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+        if (p.cpack && nb)  // (the fused map's packed candidates)
+            hipLaunchKernelGGL(k_bin_packed, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+        else
+            hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
         if (hipGetLastError() != hipSuccess) return -2;
     }
     if (nb == 0) return 0;

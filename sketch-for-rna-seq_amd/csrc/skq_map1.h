@@ -141,7 +141,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     uint32_t* s_raw = s_st.raw;
     uint32_t* s_rows = s_raw + WG;
     uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + (HCAP + 1) * WG + wv * 64);  // (the wave's columns, last row)
-    const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals;  // uniform (else k_bin bins)
+    // (uniform; else k_bin_packed bins the packed candidates after this kernel)
+    const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals && cp.map_bins;
     for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot ks's roll terms, then the seeds
         const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);

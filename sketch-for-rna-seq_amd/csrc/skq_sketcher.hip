@@ -141,7 +141,9 @@ __global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_
                 for (uint32_t q = t; q < (b1 - t0 + 15) / 16; q += SK_WG) d4[q] = s4[q];
                 __syncthreads();
             }
-            const uint8_t* s = tiled ? s_seq - t0 : src;  // (indexed by sequence position)
+            // (indexed by position - t0: a pointer formed as s_seq - t0 would leave the LDS
+            // aperture — the compiler moves only its low word — and fault when p is added)
+            const uint8_t* s = tiled ? s_seq : src;  // (untiled: one tile, t0 = 0)
             // a chunk of the tile's windows per thread, rolled from its first base
             const uint32_t chunk = max(1u, (tn + SK_WG - 1) / SK_WG);
             for (uint32_t w0 = t0 + t * chunk; w0 < t0 + tn; w0 += SK_WG * chunk) {
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_
                 uint32_t run = 0;  // valid bases ending at p, counted from w0
                 const uint32_t pend = min(min(len, w0 + chunk + k - 1), t0 + tn + k - 1);
                 for (uint32_t p = w0; p < pend; ++p) {
-                    const uint32_t c = s_code[s[p]];
+                    const uint32_t c = s_code[s[p - t0]];
                     if (c == 4) {
                         run = 0;
                         h = 0;
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(SK_WG) void k_sketch_server(SkMail* m, const uint8_
                     ++run;
                     h = ((h << 1) | (h >> 32)) & skq::M33;
                     h ^= seed[c];
-                    if (run > k) h ^= rk[s_code[s[p - k]]];
+                    if (run > k) h ^= rk[s_code[s[p - t0 - k]]];
                     if (run >= k && (uint32_t)h <= thr) {  // src/sketch.cpp:33-35
                         const uint32_t at = atomicAdd(&s_cnt, 1u);
                         if (at < cap) out[1 + at] = (uint32_t)h;

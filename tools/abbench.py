@@ -30,6 +30,8 @@ ap.add_argument("--config", default="cfg3", choices=["cfg2", "cfg3", "cfg5"])
 ap.add_argument("--rounds", type=int, default=20)
 ap.add_argument("--acc", action="store_true", help="time with the per-transcript totals accumulated")
 ap.add_argument("--chain", type=int, default=1, help="SKQ_CHAIN for both indexes")
+ap.add_argument("--env-b", default="", help="K=V[,K=V]: environment set only around B's first map (a library "
+                "reads its switches once; LIB_B may then be LIB_A itself, loaded as a second copy)")
 a = ap.parse_args()
 CFG = {"cfg2": (10_000, 1_000_000, 100, [31]), "cfg3": (200_000, 10_000_000, 150, [31]),
        "cfg5": (200_000, 10_000_000, 150, [21, 25, 31])}
@@ -37,7 +39,12 @@ ntx, n, L, ks = CFG[a.config]
 
 
 def load(path, name):
-    os.environ["SKQ_LIB"] = os.path.abspath(path)
+    # (a private copy of the file: dlopen of a path already loaded would return the same library)
+    import shutil
+    import tempfile
+    cp = os.path.join(tempfile.mkdtemp(prefix="skq_ab_"), "libskq.so")
+    shutil.copy(path, cp)
+    os.environ["SKQ_LIB"] = cp
     spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, "skq", "__init__.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
@@ -57,11 +64,18 @@ ix, ss = {}, {}
 for v, m in mods.items():
     ix[v] = m.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs))
     ss[v] = m.Session(ix[v], n, L)
-    print(v, m.LIB_PATH, ix[v].stats(), flush=True)
+    print(v, {"A": a.lib_a, "B": a.lib_b}[v], ix[v].stats(), flush=True)
 res = {v: [] for v in mods}
+envb = dict(kv.split("=", 1) for kv in a.env_b.split(",") if kv)
 for rnd in range(a.rounds + 2):
     for v in (("A", "B") if rnd % 2 == 0 else ("B", "A")):
         s = ss[v]
+        if rnd == 0:  # (each copy reads its switches at its first map)
+            for k_, v_ in envb.items():
+                if v == "B":
+                    os.environ[k_] = v_
+                else:
+                    os.environ.pop(k_, None)
         s.enable_timing(True)
         torch.cuda.synchronize()
         t = time.perf_counter()
