@@ -259,6 +259,8 @@ int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid = 2048);
 // fused sketch + chain (k_map1: quant mode, one k slot, wide tables, hcap 16 or 32; -4 otherwise)
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
+// whether k_map1 runs four-wave workgroups, which can bin in their epilogue (map_bins)
+bool map1_bins_ok();
 // fused sketch + chain for 2..4 k slots (wide or compact tables) by passes: k_map1 in pass mode
 // for each k slot (p.kslot; a raw capacity `cap` of 16 or 32 hashes, at most the hashes' layout
 // stride p.hcap); the last (final_pass) merges the per-k tables, filters, orders and bins

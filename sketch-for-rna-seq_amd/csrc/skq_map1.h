@@ -15,6 +15,13 @@ namespace skq {
 // the waves listed their hashes in two passes, the second one a dependent reload and gather
 // round; profiles/r3_map1_writes.log)
 constexpr uint32_t MAP_P = 512;
+// threads per k_map1 workgroup (one k and the multi-k passes): 64 (one wave: a workgroup's LDS is
+// released when ITS wave ends) or WG (four waves, which may bin the candidates in the kernel's
+// epilogue: ChainParams::map_bins)
+#ifndef SKQ_MAP_WG
+#define SKQ_MAP_WG 256
+#endif
+constexpr int MAP_MW = SKQ_MAP_WG;
 constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 // A wave's packed output (lane-ordered runs: this lane's words from its exclusive offset `off`
 // of the wave's `tot`, word j present when has(j), valued val(j)) to 16-B aligned g through the
@@ -59,12 +66,12 @@ __device__ __forceinline__ void wave_out_packed(uint32_t* g, uint32_t off, uint3
     }
 }
 
-template <int HCAP>
+template <int HCAP, int MW = WG>
 struct Map1Static {
-    uint32_t raw[(HCAP + 2) * WG];  // (first: at LDS address 0, the kernel's only static LDS)
+    uint32_t raw[(HCAP + 2) * MW];  // (first: at LDS address 0, the kernel's only static LDS)
     uint2 tab[16 + 4];              // the roll terms, then the seeds
 #if SKQ_HASH_PAIR
-    uint32_t te[256];               // the pair terms (hashing loop, below)
+    uint2 tb[16];                   // the roll terms with bit 32 in bit 0 of .y (hashing loop, below)
 #endif
 };
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
@@ -83,14 +90,15 @@ inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
     return ((m > c ? m : c) + 15) & ~(size_t)15;
 }
 
-// sets p.map_wave_bytes / p.map_flag_at; returns the launch's LDS bytes
-inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
+// sets p.map_wave_bytes / p.map_flag_at; returns the launch's LDS bytes (mw: threads per workgroup;
+// the epilogue's bucket counters only where it may bin, mw = WG)
+inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap, uint32_t mw = WG) {
     p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
     p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
     // (the binning epilogue's bucket counters first, their own so they are zeroed up front; the
     // raw rows are static)
     (void)hcap;
-    return MAP1_BC_BYTES + (WG / 64) * (size_t)p.map_wave_bytes;
+    return (mw == (uint32_t)WG ? MAP1_BC_BYTES : 0) + (mw / 64) * (size_t)p.map_wave_bytes;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
@@ -105,7 +113,7 @@ inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
 #define MAP1_STAMP(i)                                                                           \
     do {                                                                                        \
         if (cp.stamps && lane == 0)                                                             \
-            cp.stamps[((uint64_t)blockIdx.x * (WG / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+            cp.stamps[((uint64_t)blockIdx.x * (MW / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
 // TAB: 0 = wide tables, 2 = compact tables, 3 = chained tables over wide ones. PASS: one k slot (p.kslot) of a
@@ -116,8 +124,10 @@ inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap) {
 // skipped. FINAL (the last k slot's pass): the earlier passes' entries are merged in registers with
 // this pass's table (matched only, when this k slot filters), then filtered, ordered, written and
 // binned as in the one-k map.
-template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false>
-__global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
+template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false, int MW = WG>
+__global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
+    static_assert(MW == WG || MW == 64, "a workgroup of 256 threads (4 waves) or of one wave");
+    constexpr size_t BC = MW == WG ? MAP1_BC_BYTES : 0;  // (the binning's bucket counters: WG only)
     constexpr bool CMP = TAB == 2, CHN = TAB == 3;
     static_assert(PASS || !FINAL, "the final pass is a pass");
     static_assert(!CHN || HCAP <= 32, "hit bits");
@@ -130,37 +140,35 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint32_t wc = p.tile_chunks;  // chunks per wave
     const size_t wave_bytes = p.map_wave_bytes;
     // (static LDS: the raw rows' and the roll terms' addresses fold into the instructions' offsets)
-    __shared__ __attribute__((aligned(16))) Map1Static<HCAP> s_st;
+    __shared__ __attribute__((aligned(16))) Map1Static<HCAP, MW> s_st;
     uint2* s_tab = s_st.tab;
     const uint2* s_seed = s_tab + 16;
     uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem);  // the binning's bucket counters (map1_layout)
-    unsigned char* s_wave = smem + MAP1_BC_BYTES + wv * wave_bytes;
+    unsigned char* s_wave = smem + BC + wv * wave_bytes;
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
     // raw rows: row 0 the sink, retained window i of the read (position order) in row HCAP + 1 - i;
     // after the hashing, rows 1..TS hold the count tables (s_rows)
     uint32_t* s_raw = s_st.raw;
-    uint32_t* s_rows = s_raw + WG;
-    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + (HCAP + 1) * WG + wv * 64);  // (the wave's columns, last row)
+    uint32_t* s_rows = s_raw + MW;
+    uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + (HCAP + 1) * MW + wv * 64);  // (the wave's columns, last row)
     // (uniform; else k_bin_packed bins the packed candidates after this kernel)
-    const bool bin = (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals && cp.map_bins;
-    for (uint32_t e = tid; e < 16 + 4; e += WG) {  // k slot ks's roll terms, then the seeds
+    const bool bin = MW == WG && (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals && cp.map_bins;
+    for (uint32_t e = tid; e < 16 + 4; e += MW) {  // k slot ks's roll terms, then the seeds
         const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
     }
 #if SKQ_HASH_PAIR
-    // the pair terms: te[a | b << 4] = the low 32 bits of window w's roll term (its (in, out)
-    // nibble b) with bit 0 flipped by bit 32 of window w - 1's (nibble a): see the hashing loop
-    {
-        static_assert(WG == 256, "one pair term per thread");
-        const uint64_t* rt = p.rolltab + ks * 16;
-        s_st.te[tid] = (uint32_t)rt[tid >> 4] ^ (uint32_t)((rt[tid & 15] >> 32) & 1u);
+    // the roll terms again, bit 32 in bit 0 (the hashing loop folds it into the next window's XOR)
+    if (tid < 16) {
+        const uint64_t v = p.rolltab[ks * 16 + tid];
+        s_st.tb[tid] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) & 1u);
     }
 #endif
     if (bin)
-        for (uint32_t e = tid; e <= (uint32_t)WG; e += WG) s_bc[e] = 0;
+        for (uint32_t e = tid; e <= (uint32_t)WG; e += MW) s_bc[e] = 0;
     __syncthreads();
 
-    const uint64_t r0 = (uint64_t)blockIdx.x * WG + wv * 64;  // this wave's first read
+    const uint64_t r0 = (uint64_t)blockIdx.x * MW + wv * 64;  // this wave's first read
     const uint32_t nr = r0 < p.n ? (uint32_t)min((uint64_t)64, p.n - r0) : 0u;  // wave-uniform
     const uintptr_t base = reinterpret_cast<uintptr_t>(p.reads);
     const uintptr_t abase = base & ~(uintptr_t)15;
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                     if (b + j < k) roll33b(hlo, hhi, e[j]);
             }
         }
-        s_raw[(HCAP + 1) * WG + tid] = hlo;
+        s_raw[(HCAP + 1) * MW + tid] = hlo;
         const uint32_t nw = L - k + 1;
         const uint32_t qin = (uint32_t)q0 + k, qout = (uint32_t)q0;
         // windows 1..nw-1, 16 per block (in-base at w + k - 1, out-base at w - 1). A window's roll
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // full-rate VALU form (tools/micro/valu_mix: compares, min/max and the three-operand
         // integer forms issue at half rate).
         const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)s_raw;
-        constexpr uint32_t ROW = (uint32_t)WG * 4u;
+        constexpr uint32_t ROW = (uint32_t)MW * 4u;
         const uint32_t d0 = (uint32_t)tid * 4u + (uint32_t)(HCAP + 1) * ROW;
         uint32_t d = d0 - (hlo <= T ? ROW : 0u);
 #if SKQ_HASH_PAIR
@@ -332,24 +340,22 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         // of window w (lo_w its low 32 bits) and t_w its roll term (in, out bases), the roll
         // x_w = rot33(x_{w-1}) ^ t_w gives bit 32 of x_{w-1} as (lo_{w-2} >> 31) ^ bit 32 of
         // t_{w-1}, so
-        //     lo_w = alignbit(lo_{w-1}, lo_{w-2}, 31) ^ te[nib_{w-1} | nib_w << 4],
-        // the pair term te folding bit 32 of t_{w-1} into bit 0 of t_w's low word (nib = in << 2 |
-        // out). Window 1's "previous" word is window 0's high lane (hhi, bit 31) and its previous
-        // nibble z one whose roll term has bit 32 clear (one always exists: G's seed has bit 32
-        // clear and A's set, so G or A pairs with any out-base). The 16 pair indexes of a block
-        // are the bytes of four words built from the in- and out-base codes (eight operations),
-        // each taken scaled to its LDS offset by one byte-select shift. The slot counter moves
-        // by a plain subtract: a lane past row 0 stores below LDS address 0, which wraps past the
-        // allocation, and such stores are dropped (tools/micro/lds_oob, profiles/r5_lds_oob.log).
-        uint32_t zm = 0;
-#pragma unroll
-        for (int a = 0; a < 16; ++a) zm |= ((p.rolltab[ks * 16 + a] >> 32) & 1u) ? 0u : 1u << a;
-        uint32_t oprev = (uint32_t)__builtin_ctz(zm) << 28;
-        uint32_t lprev = hhi;
+        //     lo_w = alignbit(lo_{w-1}, lo_{w-2}, 31) ^ lo(t_w) ^ bit32(t_{w-1}),
+        // one funnel shift and one three-way XOR (v_bitop3), bit 32 of each term kept in bit 0 of
+        // its table entry's second word. Window 1's "previous" word is window 0's high lane (hhi,
+        // bit 31) and its previous term none. The terms stay a 16-entry table read at the (in,
+        // out) nibble's offset: 64 lanes hit at most 16 distinct 8-B entries, so a read is a
+        // broadcast, never a bank conflict (a 256-entry table of pair terms, one XOR fewer, measured
+        // 3 % slower: random reads of 1 KB conflict). The nibbles: ex (even windows) and ox (odd)
+        // from the in- and out-base codes, each offset one byte select of four masked words. The
+        // slot counter moves by a plain subtract: a lane past row 0 stores below LDS address 0,
+        // which wraps past the allocation, and such stores are dropped (tools/micro/lds_oob,
+        // profiles/r5_lds_oob.log).
+        uint32_t lprev = hhi, yprev = 0;
         const uint32_t* pa = s_codes + (qin >> 4);
         const uint32_t* pb = s_codes + (qout >> 4);
         const uint32_t sa = (qin & 15u) * 2u, sb = (qout & 15u) * 2u;
-        const unsigned char* teb = reinterpret_cast<const unsigned char*>(s_st.te);
+        const unsigned char* tbb = reinterpret_cast<const unsigned char*>(s_st.tb);
         auto bfi = [](uint32_t m, uint32_t x, uint32_t y) {  // (x & m) | (y & ~m), one v_bfi_b32
             uint32_t r;
             asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
@@ -358,35 +364,34 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         auto block = [&](uint32_t bi, uint32_t jn, auto full, auto small) {
             const uint32_t A = __builtin_amdgcn_alignbit(pa[bi + 1], pa[bi], sa);
             const uint32_t B = __builtin_amdgcn_alignbit(pb[bi + 1], pb[bi], sb);
-            // nibbles: ex m = window 2m, ox m = window 2m + 1; os = ox one nibble up, the previous
-            // block's last nibble below
+            // nibble m of ex = (in << 2 | out) of window 2m, of ox of window 2m + 1
             const uint32_t ex = bfi(0xCCCCCCCCu, A << 2, B);
             const uint32_t ox = bfi(0xCCCCCCCCu, A, B >> 2);
-            const uint32_t os = __builtin_amdgcn_alignbit(ox, oprev, 28);
-            oprev = ox;
-            // byte b of word c: the pair index of window 4b + c
-            const uint32_t wq[4] = {bfi(0x0F0F0F0Fu, os, ex << 4), bfi(0x0F0F0F0Fu, ex, os), bfi(0x0F0F0F0Fu, ox, ex),
-                                    bfi(0x0F0F0F0Fu, ex >> 4, ox)};
-            uint32_t e[16];
+            // byte b of word c: window 4b + c's nibble times 8 (its term's offset)
+            const uint32_t wq[4] = {(ex << 3) & 0x78787878u, (ox << 3) & 0x78787878u, (ex >> 1) & 0x78787878u,
+                                    (ox >> 1) & 0x78787878u};
+            uint2 e[16];
             static_for<16>([&](auto jc) {
                 constexpr int j = decltype(jc)::value, b = j >> 2;
                 const uint32_t x = wq[j & 3];
                 uint32_t o;
-                if constexpr (b == 0)
-                    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(o) : "v"(x));
-                else if constexpr (b == 1)
-                    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(o) : "v"(x));
-                else if constexpr (b == 2)
-                    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(o) : "v"(x));
-                else
-                    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(o) : "v"(x));
-                e[j] = *reinterpret_cast<const uint32_t*>(teb + o);
+                if constexpr (b == 0) {
+                    o = x & 0xFFu;
+                } else if constexpr (b == 1) {
+                    asm("v_mov_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(o) : "v"(x));
+                } else if constexpr (b == 2) {
+                    asm("v_mov_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(o) : "v"(x));
+                } else {
+                    o = x >> 24;
+                }
+                e[j] = *reinterpret_cast<const uint2*>(tbb + o);
             });
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const uint32_t h = __builtin_amdgcn_alignbit(hlo, lprev, 31) ^ e[j];
+                const uint32_t h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(hlo, lprev, 31), e[j].x, yprev, 0x96);
                 lprev = hlo;
                 hlo = h;
+                yprev = e[j].y;
                 *(__attribute__((address_space(3))) uint32_t*)(size_t)(rbase + d) = h;
                 uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - h, h, 0x80000000u, 0x02) >> 21
                                                       : (h <= T ? ROW : 0u);
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         nraw = (d0 - d) / ROW;  // (> HCAP: more than HCAP retained; exact, d0 - d < 2^32)
     }
     if constexpr (CHN) {
-        cq = s_raw[(HCAP + 1) * WG + tid];  // (the first retained window)
+        cq = s_raw[(HCAP + 1) * MW + tid];  // (the first retained window)
         has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len[ks];
 #if SKQ_CHN_COALESCED
         // eight lanes read one entry, a 16-B piece each, eight entries per load: a load touches 8
@@ -494,7 +499,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
         } else {
             nraw_out = nraw;
 #pragma unroll
-            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[(HCAP + 1 - j) * WG + tid] : 0xFFFFFFFFu;
+            for (int j = 0; j < HCAP; ++j) v[j] = (uint32_t)j < nraw ? s_raw[(HCAP + 1 - j) * MW + tid] : 0xFFFFFFFFu;
             sort_prefix<HCAP>(v, nraw);
             uint32_t* out = p.hashes + (uint64_t)ks * p.hcap * p.n + r;
             uint32_t m = 0;
@@ -558,7 +563,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     const uint64_t keepm_all = keepm;  // the read's distinct retained hashes (as written out)
     constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 #pragma unroll
-    for (int sl = 0; sl < TS; ++sl) s_rows[sl * WG + tid] = EMPTY;
+    for (int sl = 0; sl < TS; ++sl) s_rows[sl * MW + tid] = EMPTY;
     uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_wave + p.map_flag_at);  // per read: > TS transcripts
     s_flag[lane] = 0;
     uint32_t* s_h = reinterpret_cast<uint32_t*>(s_wave);
@@ -578,7 +583,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll 1
         for (int z = 1; z < TS; ++z) {
             sl = (sl + 1) & (TS - 1);
-            uint32_t* a = colbase + sl * WG + ((o + sl) & 63u);
+            uint32_t* a = colbase + sl * MW + ((o + sl) & 63u);
             const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | c);
             if (old == EMPTY) return;
             if ((old >> 8) == x) {
@@ -590,7 +595,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     };
     auto ains = [&](uint32_t x, uint32_t o) {
         const uint32_t sl = Counter<1, WG>::slot_of(x);
-        uint32_t* a = colbase + sl * WG + ((o + sl) & 63u);
+        uint32_t* a = colbase + sl * MW + ((o + sl) & 63u);
         const uint32_t old = atomicCAS(a, EMPTY, (x << 8) | 1u);
         if (old == EMPTY) return;
         if ((old >> 8) == x) atomicAdd(a, 1u);
@@ -677,7 +682,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
             cs[q] = (uint32_t)__builtin_popcount(hm & (w[CHN_W_SET + q / 2] >> (16 * (q & 1))));
             xs[q] = w[CHN_W_TID + q];
             const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
-            olds[q] = cs[q] ? atomicCAS(colbase + sl * WG + ((lane + sl) & 63u), EMPTY, (xs[q] << 8) | cs[q]) : EMPTY;
+            olds[q] = cs[q] ? atomicCAS(colbase + sl * MW + ((lane + sl) & 63u), EMPTY, (xs[q] << 8) | cs[q]) : EMPTY;
         }
 #pragma unroll
         for (int q = 0; q < (int)CHN_TIDS; ++q)
@@ -820,14 +825,14 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t sl = Counter<1, WG>::slot_of(xs[q]);
-                    olds[q] = vs[q] ? atomicCAS(colbase + sl * WG + ((own[u] + sl) & 63u), EMPTY, (xs[q] << 8) | 1u)
+                    olds[q] = vs[q] ? atomicCAS(colbase + sl * MW + ((own[u] + sl) & 63u), EMPTY, (xs[q] << 8) | 1u)
                                     : EMPTY;
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t x = xs[q], sl = Counter<1, WG>::slot_of(x), o = olds[q];
                     if (o == EMPTY) continue;
-                    if ((o >> 8) == x) atomicAdd(colbase + sl * WG + ((own[u] + sl) & 63u), 1u);
+                    if ((o >> 8) == x) atomicAdd(colbase + sl * MW + ((own[u] + sl) & 63u), 1u);
                     else ains_probe(x, own[u]);
                 }
                 // lists longer than 7 (rare): the lane holding the offset (wide: even, compact:
@@ -871,7 +876,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 uint32_t mx = 0;
 #pragma unroll
                 for (int sl = 0; sl < TS; ++sl) {
-                    kev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
+                    kev[sl] = colbase[sl * MW + ((lane + sl) & 63u)];
                     mx = max(mx, kev[sl] != EMPTY ? kev[sl] & 0xFFu : 0u);
                 }
                 const uint32_t need = need_of(mx);
@@ -916,7 +921,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 uint32_t ut[TS], uc[TS], mxf = 0;
 #pragma unroll
                 for (int sl = 0; sl < TS; ++sl) {
-                    const uint32_t ev = colbase[sl * WG + ((lane + sl) & 63u)];
+                    const uint32_t ev = colbase[sl * MW + ((lane + sl) & 63u)];
                     ut[sl] = ev != EMPTY ? ev >> 8 : EMPTY;
                     uc[sl] = ev != EMPTY ? (ev & 0xFFu) << (8 * ks) : 0u;
                     mxf = max(mxf, ev != EMPTY ? ev & 0xFFu : 0u);
@@ -1032,7 +1037,7 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
                 uint32_t mx = 0;
 #pragma unroll
                 for (int sl = 0; sl < TS; ++sl) {
-                    ev[sl] = colbase[sl * WG + ((lane + sl) & 63u)];
+                    ev[sl] = colbase[sl * MW + ((lane + sl) & 63u)];
                     mx = max(mx, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
                 }
                 const double thr = cp.fraction * (double)mx;
@@ -1076,7 +1081,8 @@ __global__ __launch_bounds__(WG) void k_map1(SketchParams p, ChainParams cp) {
     MAP1_STAMP(4);
     // (bin_candidates places entries only after its barriers, when every wave's count tables
     // are dead)
-    if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
+    if constexpr (MW == WG)
+        if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
     MAP1_STAMP(5);
 }
 

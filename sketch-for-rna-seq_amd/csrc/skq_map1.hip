@@ -6,6 +6,9 @@
 
 namespace skq {
 
+constexpr int MW = MAP_MW;
+bool map1_bins_ok() { return MW == WG; }
+
 // SKQ_MAP1_OCC=1: print each k_map1 launch shape's resident workgroups per CU once (stderr)
 static void map1_report_occupancy(const void* kern, size_t lds) {
     static const bool on = [] {
@@ -20,28 +23,28 @@ static void map1_report_occupancy(const void* kern, size_t lds) {
         if (x.first == kern && x.second == lds) return;
     seen.emplace_back(kern, lds);
     int nb = -1;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, WG, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, MW, lds);
     std::fprintf(stderr, "[skq] k_map1 %p: %zu B LDS, %d workgroups per CU\n", kern, lds, nb);
 }
 
 int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     if (p0.n == 0) return 0;
-    const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
+    const dim3 grid((unsigned)((p0.n + MW - 1) / MW));
     const bool chn = cp.chain[0] != nullptr;
     SketchParams p = p0;
     if (!chn && cp.wide != 1 && cp.wide != 3) return -4;
-    const size_t lds = map1_layout(p, chn ? 3 : cp.wide == 3 ? 2 : 0, p.hcap);
+    const size_t lds = map1_layout(p, chn ? 3 : cp.wide == 3 ? 2 : 0, p.hcap, MW);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     using K = void (*)(SketchParams, ChainParams);
     K kern = nullptr;
     // (MB: gather rounds in flight)
     switch (p.hcap * 4 + (chn ? 3 : cp.wide == 3 ? 2 : 0)) {
-    case 67: kern = k_map1<16, 4, 3>; break;
-    case 131: kern = k_map1<32, 4, 3>; break;
-    case 64: kern = k_map1<16, 4, 0>; break;
-    case 66: kern = k_map1<16, 4, 2>; break;
-    case 128: kern = k_map1<32, 4, 0>; break;
-    case 130: kern = k_map1<32, 4, 2>; break;
+    case 67: kern = k_map1<16, 4, 3, false, false, MW>; break;
+    case 131: kern = k_map1<32, 4, 3, false, false, MW>; break;
+    case 64: kern = k_map1<16, 4, 0, false, false, MW>; break;
+    case 66: kern = k_map1<16, 4, 2, false, false, MW>; break;
+    case 128: kern = k_map1<32, 4, 0, false, false, MW>; break;
+    case 130: kern = k_map1<32, 4, 2, false, false, MW>; break;
     default: return -4;
     }
     // (development: SKQ_LDS_PAD bytes of unused LDS per workgroup lower the occupancy, to price it)
@@ -49,7 +52,7 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     if (lds + pad > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds + pad));
     map1_report_occupancy(reinterpret_cast<const void*>(kern), lds + pad);
-    hipLaunchKernelGGL(kern, grid, dim3(WG), lds + pad, st, p, cp);
+    hipLaunchKernelGGL(kern, grid, dim3(MW), lds + pad, st, p, cp);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

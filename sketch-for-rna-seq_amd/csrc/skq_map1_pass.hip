@@ -9,25 +9,26 @@ namespace skq {
 int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
     if (p0.n == 0) return 0;
     if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.kslot >= SKQ_MAX_K) return -4;
-    const dim3 grid((unsigned)((p0.n + WG - 1) / WG));
+    constexpr int MW = MAP_MW;
+    const dim3 grid((unsigned)((p0.n + MW - 1) / MW));
     SketchParams p = p0;
     // (the pass's k slot has chained tables: TAB 3)
     const int tab = cp.chain[p0.kslot] ? 3 : cp.wide == 3 ? 2 : 0;
-    const size_t lds = map1_layout(p, tab, cap);
+    const size_t lds = map1_layout(p, tab, cap, MW);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (cap * 8 + tab + (final_pass ? 1 : 0) * 4) {
-    case 131: hipLaunchKernelGGL((k_map1<16, 4, 3, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 135: hipLaunchKernelGGL((k_map1<16, 4, 3, true, true>), grid, dim3(WG), lds, st, p, cp); break;
-    case 259: hipLaunchKernelGGL((k_map1<32, 4, 3, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 263: hipLaunchKernelGGL((k_map1<32, 4, 3, true, true>), grid, dim3(WG), lds, st, p, cp); break;
-    case 128: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 132: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
-    case 130: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 134: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
-    case 256: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 260: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true>), grid, dim3(WG), lds, st, p, cp); break;
-    case 258: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false>), grid, dim3(WG), lds, st, p, cp); break;
-    case 262: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true>), grid, dim3(WG), lds, st, p, cp); break;
+    case 131: hipLaunchKernelGGL((k_map1<16, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 135: hipLaunchKernelGGL((k_map1<16, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 259: hipLaunchKernelGGL((k_map1<32, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 263: hipLaunchKernelGGL((k_map1<32, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 128: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 132: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 130: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 134: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 256: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 260: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 258: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 262: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
