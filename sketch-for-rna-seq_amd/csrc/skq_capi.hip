@@ -79,8 +79,11 @@ struct skq_index {
     const uint16_t* wpil[SKQ_MAX_K] = {};
     uint32_t wnb[SKQ_MAX_K] = {}, wseed[SKQ_MAX_K] = {};
     uint64_t dir_bytes = 0;
+    // (build time only) per distinct k, each key's compact slot: the chained entries over compact
+    // tables sit at the same slots; cleared once the chained tables are built
+    std::vector<uint32_t> cmp_slots_t[SKQ_MAX_K];
     // chained tables (per k slot; ChainParams::chain): a 128-B entry per possible key up to the
-    // largest, carrying the key's postings list and those of the keys that follow it in the
+    // largest (over compact tables: per present key, at its compact slot), carrying the key's postings list and those of the keys that follow it in the
     // transcripts; k_map1 then settles a read with ~1.5 entry requests instead of one per hash
     uint4* d_chain[SKQ_MAX_K] = {};
     uint64_t chain_len[SKQ_MAX_K] = {};
@@ -430,6 +433,7 @@ int build_compact(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
             seed = skq::cmp_mix(seed + 0x9E3779B9u);
         }
         std::vector<uint32_t> ent(nslots * 8, 0);
+        ix->cmp_slots_t[t] = slot;
         for (uint64_t j = 0; j < m; ++j) {
             const uint32_t off = dvals[t][j], n = lists[off];
             uint32_t* e = ent.data() + (uint64_t)slot[j] * 8;
@@ -640,9 +644,12 @@ static std::shared_ptr<const ChainHost> chain_host_build(const std::vector<uint3
             });
         for (auto& t : pool) t.join();
     }
-    // keys no transcript of `seqs` retained still get their own record
-    for (uint64_t x = 0; x < m; ++x)
+    // keys no transcript of `seqs` retained still get their own record; word 28 names the entry's
+    // key (read by k_map1 over compact tables, where a slot may be asked for a key it does not hold)
+    for (uint64_t x = 0; x < m; ++x) {
         if (!built[x]) chain_entry(ent.data() + x * skq::CHAIN_WORDS, keys[x], vals[x], lists, nullptr, nullptr, 0);
+        ent[x * skq::CHAIN_WORDS + skq::CHN_W_SELF] = keys[x] ^ skq::CHN_KEY_LIMIT;
+    }
     out->nsucc = nsucc.load();
     out->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return out;
@@ -660,20 +667,24 @@ static void chain_note(uint32_t k, const char* why, uint64_t need, uint64_t fr) 
                  "keeps the wide entries\n", k, why, need / 1e9, fr / 1e9);
 }
 
+// slots: the keys' compact slots (chained entries over compact tables, nslots of them), or null
+// (one entry per possible key up to the largest)
 int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
                 const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
-                uint32_t nseq, uint32_t threshold) {
+                uint32_t nseq, uint32_t threshold, const std::vector<uint32_t>* slots, uint64_t nslots) {
     const uint64_t m = keys.size();
     if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key ^ CHN_KEY_LIMIT)
+    if (slots && slots->size() != m) return fail(-3, "chained table: compact slots missing");
     const uint64_t len = (uint64_t)keys.back() + 1;
-    // 128 B per possible key, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
+    const uint64_t ents = slots ? nslots : len;  // (entries allocated)
+    // 128 B per entry, up to SKQ_CHAIN_MB (default 64 GiB) and half the free memory
     uint64_t budget = 65536ull << 20;
     if (const char* e = std::getenv("SKQ_CHAIN_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     size_t fr = 0, tot = 0;
     // (half of what is free past a 32 GiB reserve for sessions: several indexes may share a device)
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < (32ull << 30) || len * 128 > (fr - (32ull << 30)) / 2 ||
-        len * 128 > budget) {
-        chain_note(k, len * 128 > budget ? "over SKQ_CHAIN_MB" : "past half the free memory above 32 GiB", len * 128, fr);
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < (32ull << 30) || ents * 128 > (fr - (32ull << 30)) / 2 ||
+        ents * 128 > budget) {
+        chain_note(k, ents * 128 > budget ? "over SKQ_CHAIN_MB" : "past half the free memory above 32 GiB", ents * 128, fr);
         return 0;
     }
     // the host entries: shared with the other devices building the same tables at the same time
@@ -722,19 +733,20 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
     uint32_t* dk = nullptr;
     uint4* de = nullptr;
     uint4*& dch = ix->d_chain[slot];
-    if (dev_alloc_table(&dch, len * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
+    if (dev_alloc_table(&dch, ents * 8) || dev_alloc(&dk, m) || dev_alloc(&de, m * 8)) {
         // (the device is shared, e.g. several indexes on it: this slot keeps the wide entries)
         dev_free(dk);
         dev_free(de);
         dev_free(dch);
         (void)hipGetLastError();
         done_with();
-        chain_note(k, "allocation failed", len * 128, fr);
+        chain_note(k, "allocation failed", ents * 128, fr);
         return 0;
     }
     hipStream_t st = nullptr;
-    const bool ok = hipMemsetAsync(dch, 0, len * 128, st) == hipSuccess &&
-                    hipMemcpy(dk, keys.data(), m * 4, hipMemcpyHostToDevice) == hipSuccess &&
+    // (the scatter's destinations: the keys themselves, or their compact slots)
+    const bool ok = hipMemsetAsync(dch, 0, ents * 128, st) == hipSuccess &&
+                    hipMemcpy(dk, slots ? slots->data() : keys.data(), m * 4, hipMemcpyHostToDevice) == hipSuccess &&
                     hipMemcpy(de, hc->ent.data(), m * 128, hipMemcpyHostToDevice) == hipSuccess;
     if (ok) {
         hipLaunchKernelGGL(k_chain_scatter, dim3((unsigned)((m * 8 + 255) / 256)), dim3(256), 0, st, dch, dk, de, m);
@@ -751,8 +763,8 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
         dev_free(dch);
         return fail(-3, "chained table build failed");
     }
-    ix->chain_len[slot] = len;
-    ix->chain_bytes += len * 128;
+    ix->chain_len[slot] = len;  // (k_map1: a query past the largest key is no key)
+    ix->chain_bytes += ents * 128;
     ix->chain_succ = (ix->chain_succ * ix->chain_slots + (double)nsucc / (double)m) / (ix->chain_slots + 1);
     ++ix->chain_slots;
     return 0;
@@ -766,7 +778,7 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
 // transcript ids past 2^22, which the wide and compact entries cannot hold.
 int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
                  const std::vector<uint32_t>* dkeys, const std::vector<uint32_t>* dvals,
-                 const std::vector<uint32_t>& lists) {
+                 const std::vector<uint32_t>& lists, bool prefer_compact) {
     uint64_t budget = 49152ull << 20;
     if (const char* e = std::getenv("SKQ_DIRECT_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     if (budget == 0) return 0;
@@ -778,7 +790,7 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
         if (!known) return fail(-1, std::string("SKQ_PROBE: unknown probe kind ") + force);
         if (!std::strcmp(force, "bucket")) return 0;
     } else {
-        force = nullptr;
+        force = prefer_compact ? "compact" : nullptr;  // (SKQ_CHAIN=2)
     }
     if (force && !std::strcmp(force, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
     uint64_t need = 0, len[SKQ_MAX_K] = {};
@@ -986,26 +998,36 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
         skq_index_free(ix);
         return fail(-3, "index upload failed");
     }
-    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals, lists)) {
+    // SKQ_CHAIN: 0 no chained tables, 1 chained over whichever probe structure the index takes,
+    // 2 chained over compact tables (the compact probe unless SKQ_PROBE names another)
+    const char* chain_env = std::getenv("SKQ_CHAIN");
+    const int cm = chain_env ? std::atoi(chain_env) : 1;
+    if (cm < 0 || cm > 2) {
+        skq_index_free(ix);
+        return fail(-1, "SKQ_CHAIN: 0, 1 or 2");
+    }
+    const bool chain_ok = seqs && seq_offs && nk <= (uint32_t)skq::NK_FAST && ix->ntx <= (1u << 22) &&
+                          ix->nlist_words < 0x80000000ull;
+    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals, lists, cm == 2 && chain_ok)) {
         skq_index_free(ix);
         return rc2;
     }
     // chained tables (per k slot, ids within 22 bits, transcripts given): the default wherever
     // they fit (SKQ_CHAIN = 0 turns them off; cfg3: k_map1 1.15 against 1.35 ms over the wide
     // entries); a slot whose table does not fit keeps the wide entries alone
-    if (seqs && seq_offs && nk <= (uint32_t)skq::NK_FAST && ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull &&
-        ix->mode == 3) {  // (the entry list behind the chain step gathers wide entries)
-        const char* e = std::getenv("SKQ_CHAIN");
-        const int cm = e ? std::atoi(e) : 1;
-        if (cm == 1)
-            for (uint32_t i = 0; i < nk; ++i)
-                for (uint32_t t = 0; t < ntables; ++t)
-                    if (tables[t].k == ks[i])
-                        if (int rc2 = build_chain(ix, i, dkeys[t], dvals[t], lists, ks[i], seqs, seq_offs, nseq, threshold)) {
-                            skq_index_free(ix);
-                            return rc2;
-                        }
-    }
+    // (the entry list behind the chain step gathers wide or compact entries)
+    if (chain_ok && cm != 0 && (ix->mode == 3 || ix->mode == 5))
+        for (uint32_t i = 0; i < nk; ++i)
+            for (uint32_t t = 0; t < ntables; ++t)
+                if (tables[t].k == ks[i]) {
+                    const bool cmp = ix->mode == 5;
+                    if (int rc2 = build_chain(ix, i, dkeys[t], dvals[t], lists, ks[i], seqs, seq_offs, nseq, threshold,
+                                              cmp ? &ix->cmp_slots_t[t] : nullptr, cmp ? ix->dir_len[i] : 0)) {
+                        skq_index_free(ix);
+                        return rc2;
+                    }
+                }
+    for (auto& v : ix->cmp_slots_t) std::vector<uint32_t>().swap(v);
     *out = ix;
     return 0;
 }

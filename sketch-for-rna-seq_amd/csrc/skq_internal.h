@@ -214,8 +214,9 @@ struct ChainParams {
     int wide;
     const uint32_t* wdir[SKQ_MAX_K];
     uint64_t wdir_len[SKQ_MAX_K];
-    // chained tables (k_map1 TAB = 3, one k slot): a 128-B entry per possible key
-    // (chain_len of them, 8 uint4 each; layout CHN_* below): the key's own record, then records of
+    // chained tables (k_map1 TAB = 3 over wide entries, 4 over compact ones): a
+    // 128-B entry per possible key up to chain_len (TAB 4: per present key, at the key's compact
+    // slot) of 8 uint4 each (layout CHN_* below): the key's own record, then records of
     // keys that follow it along the transcripts (nearest first), each naming the key's WHOLE
     // postings list as a set of the entry's transcripts, so one 128-B request settles a run of a
     // read's retained hashes
@@ -232,7 +233,7 @@ uint64_t session_max_reads(const skq_session* s);
 // host: one sequence's retained hashes at k in position order (repeats kept; ntHash's window
 // rules: windows holding a byte outside ACGTUacgtu skipped) (skq_tables.cpp)
 void sketch_positions(const uint8_t* s, uint64_t len, uint32_t k, uint32_t thr, std::vector<uint32_t>& out);
-// Chained entries (ChainParams::chain), CHAIN_WORDS words per possible key:
+// Chained entries (ChainParams::chain), CHAIN_WORDS words each:
 //   words 0-3         per entry id q (0..7): the records whose list holds it, a 16-bit set in half
 //                     q & 1 of word q >> 1 (a record's count is its key's; an id's is the records')
 //   words 4-11        the entry's transcript ids (up to CHN_TIDS, each once)
@@ -240,9 +241,11 @@ void sketch_positions(const uint8_t* s, uint64_t len, uint32_t k, uint32_t thr, 
 //                     decodes to the key 0x0FFFFFFF no retained hash reaches: keys < CHN_KEY_LIMIT).
 //                     Word 12 CHN_LONG: the key's own list holds more than CHN_TIDS transcripts (the
 //                     entry holds nothing: lookups go to the wide entries); word 12 zero: no such key
-constexpr uint32_t CHAIN_WORDS = 32;  // chained entry: 128 B (words 28-31 unused: 7 of its 8 pieces read)
+//   word 28           the entry's own key ^ CHN_KEY_LIMIT (entries at compact slots: a slot asked for
+//                     a key it does not hold answers "no such key"); words 29-31 unused
+constexpr uint32_t CHAIN_WORDS = 32;  // chained entry: 128 B
 constexpr uint32_t CHN_KEYS = 16, CHN_TIDS = 8;
-constexpr uint32_t CHN_W_SET = 0, CHN_W_TID = 4, CHN_W_KEY = 12;
+constexpr uint32_t CHN_W_SET = 0, CHN_W_TID = 4, CHN_W_KEY = 12, CHN_W_SELF = 28;
 constexpr uint32_t CHN_LONG = 0x80000000u;  // (decodes to 0x8FFFFFFF: neither a hash nor the sort's padding)
 constexpr uint32_t CHN_KEY_LIMIT = 0x0FFFFFFFu;
 // host: ascending sort with threads (skq_tables.cpp)

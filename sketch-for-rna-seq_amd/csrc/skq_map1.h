@@ -79,7 +79,7 @@ struct Map1Static {
 // wide). (Round 3 measured 6 workgroups per CU against 5 with the list packed
 // tighter: no change, profiles/r3_ingest_sweep.log.)
 inline size_t map1_flag_at(int tab, uint32_t hcap) {
-    if (tab == 2) return (size_t)MAP_P * 8;
+    if (tab == 2 || tab == 4) return (size_t)MAP_P * 8;
     return ((size_t)MAP_P * 5 + 15) & ~(size_t)15;
 }
 inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
@@ -128,9 +128,12 @@ template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false, int 
 __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
     static_assert(MW == WG || MW == 64, "a workgroup of 256 threads (4 waves) or of one wave");
     constexpr size_t BC = MW == WG ? MAP1_BC_BYTES : 0;  // (the binning's bucket counters: WG only)
-    constexpr bool CMP = TAB == 2, CHN = TAB == 3;
+    // TAB 4: chained entries at the compact tables' slots (one per present key, not per possible
+    // key: 0.6 GB at cfg3 instead of 27.5 GB), the misses through the compact entries
+    constexpr bool CMP = TAB == 2 || TAB == 4, CHN = TAB == 3 || TAB == 4, CCH = TAB == 4;
     static_assert(PASS || !FINAL, "the final pass is a pass");
     static_assert(!CHN || HCAP <= 32, "hit bits");
+    static_assert(!CCH || SKQ_CHN_COALESCED, "compact chained entries: the coalesced hand-over (word 28)");
     const uint32_t ks = PASS ? p.kslot : 0u;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -467,9 +470,15 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
 #endif
         nraw = (d0 - d) / ROW;  // (> HCAP: more than HCAP retained; exact, d0 - d < 2^32)
     }
+    uint32_t qslot = 0;  // the query's entry (TAB 4: its compact slot, whose entry names its key)
     if constexpr (CHN) {
         cq = s_raw[(HCAP + 1) * MW + tid];  // (the first retained window)
-        has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len[ks];
+        has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len[ks];  // (TAB 4 too: past the last key)
+        qslot = cq;
+        if constexpr (CCH) {  // the bucket's pilot (an L2-resident array), then the slot
+            const uint32_t qh = cmp_key_hash(cq, cp.wseed[ks]);
+            qslot = has_q ? cmp_slot(qh, cp.wpil[ks][cmp_scale(qh, cp.wnb[ks])], cp.wdir_len[ks]) : 0u;
+        }
 #if SKQ_CHN_COALESCED
         // eight lanes read one entry, a 16-B piece each, eight entries per load: a load touches 8
         // lines, not 64 (the texture addresser, busy ~75 % of k_map1's time, works per line), and
@@ -477,7 +486,7 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
         // free here: the hashing loop is done with the staged codes.
         {
             uint32_t* s_q = reinterpret_cast<uint32_t*>(s_wave);
-            s_q[lane] = has_q ? cq : 0u;
+            s_q[lane] = has_q ? qslot : 0u;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -487,7 +496,7 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
         }
 #else
         // words 0-27 of the entry (28-31 unused), one lane per entry
-        const u32x4* ent = reinterpret_cast<const u32x4*>(cp.chain[ks]) + (has_q ? (uint64_t)cq * 8 : 0ull);
+        const u32x4* ent = reinterpret_cast<const u32x4*>(cp.chain[ks]) + (has_q ? (uint64_t)qslot * 8 : 0ull);
 #pragma unroll
         for (int u = 0; u < 7; ++u) ce[u] = ent[u];
 #endif
@@ -612,8 +621,10 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
 #if SKQ_CHN_COALESCED
         // the loads' pieces to their owners, 16 entries (2 loads) a round through the wave's region:
         // piece p of entry e at (e * 9 + p) * 16 (the pad: an owner's reads 144 B apart fall in
-        // distinct banks); the owners of a round read their entry's words 0-27
-        u32x4 cw[7];
+        // distinct banks); the owners of a round read their entry's words 0-27 (TAB 4: 0-31, word 28
+        // naming the slot's key)
+        constexpr int NP = CCH ? 8 : 7;
+        u32x4 cw[NP];
         {
             u32x4* s_tr = reinterpret_cast<u32x4*>(s_wave);
             const uint32_t g = lane >> 3, pc = lane & 7u, el = lane & 15u;
@@ -630,14 +641,17 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if ((lane >> 4) == (uint32_t)rd)
 #pragma unroll
-                    for (int q = 0; q < 7; ++q) cw[q] = s_tr[el * 9 + q];
+                    for (int q = 0; q < NP; ++q) cw[q] = s_tr[el * 9 + q];
             });
         }
 #else
         const u32x4* cw = ce;
 #endif
         uint32_t w[28];
-        const bool inb = has_q && cq < cp.chain_len[ks];  // (else the lane read entry 0 and drops it)
+        // (else the lane read entry 0 and drops it; TAB 4: a query that is no key of the index
+        // lands on another key's slot, or an empty one: nothing of it is used)
+        bool inb = has_q && cq < cp.chain_len[ks];
+        if constexpr (CCH) inb = inb && (cw[7].x ^ CHN_KEY_LIMIT) == cq;
 #pragma unroll
         for (int u = 0; u < 7; ++u) {
             w[4 * u] = inb ? cw[u].x : 0u;

@@ -12,23 +12,27 @@ int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap
     constexpr int MW = MAP_MW;
     const dim3 grid((unsigned)((p0.n + MW - 1) / MW));
     SketchParams p = p0;
-    // (the pass's k slot has chained tables: TAB 3)
-    const int tab = cp.chain[p0.kslot] ? 3 : cp.wide == 3 ? 2 : 0;
+    // (the pass's k slot has chained tables: TAB 3 over wide entries, 4 over compact ones)
+    const int tab = cp.chain[p0.kslot] ? (cp.wide == 3 ? 4 : 3) : cp.wide == 3 ? 2 : 0;
     const size_t lds = map1_layout(p, tab, cap, MW);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    switch (cap * 8 + tab + (final_pass ? 1 : 0) * 4) {
-    case 131: hipLaunchKernelGGL((k_map1<16, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 135: hipLaunchKernelGGL((k_map1<16, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 259: hipLaunchKernelGGL((k_map1<32, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 263: hipLaunchKernelGGL((k_map1<32, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 128: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 132: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 130: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 134: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 256: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 260: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 258: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 262: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    switch (cap * 16 + tab * 2 + (final_pass ? 1 : 0)) {
+    case 256: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 257: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 260: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 261: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 262: hipLaunchKernelGGL((k_map1<16, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 263: hipLaunchKernelGGL((k_map1<16, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 264: hipLaunchKernelGGL((k_map1<16, 4, 4, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 265: hipLaunchKernelGGL((k_map1<16, 4, 4, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 512: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 513: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 516: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 517: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 518: hipLaunchKernelGGL((k_map1<32, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 519: hipLaunchKernelGGL((k_map1<32, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 520: hipLaunchKernelGGL((k_map1<32, 4, 4, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 521: hipLaunchKernelGGL((k_map1<32, 4, 4, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -19,7 +19,7 @@ SPLIT = False  # run_gpu: sketch and chain as two calls instead of skq_map (the 
 CHAINED = False  # build: indexes from sequences get the chained tables (skq_index_create_chained)
 
 
-@pytest.fixture(autouse=True, params=["chain", "compact", "compact-split",
+@pytest.fixture(autouse=True, params=["chain", "chain-compact", "compact", "compact-split",
                                       "wide", "wide-split", "dir", "rank", "bucket"])
 def probe_mode(request, monkeypatch):
     """Every test runs with each index probe structure: compact (minimal-perfect-hash) tables
@@ -27,11 +27,12 @@ def probe_mode(request, monkeypatch):
     (transcript ids past 2^22) probed inside the sketch kernel, and the bucket table probed by k_probe
     (SKQ_DIRECT_MB=0). "-split": the same tables through skq_sketch + skq_chain (no fused map).
     "chain": wide tables plus the chained tables (SKQ_CHAIN=1, one per k slot of indexes built
-    from sequences, up to 4 slots); other indexes run as wide."""
+    from sequences, up to 4 slots); other indexes run as wide. "chain-compact": the chained
+    tables over compact tables (entries at the keys' compact slots, k_map1 TAB 4)."""
     if request.param.startswith("chain"):
-        # chained tables (per k slot, indexes built from sequences) over wide tables
+        # chained tables (per k slot, indexes built from sequences) over wide or compact tables
         monkeypatch.setenv("SKQ_DIRECT_MB", "49152")
-        monkeypatch.setenv("SKQ_PROBE", "wide")
+        monkeypatch.setenv("SKQ_PROBE", "compact" if request.param == "chain-compact" else "wide")
         monkeypatch.setenv("SKQ_CHAIN", "1")
         monkeypatch.setattr(sys.modules[__name__], "CHAINED", True)
     elif request.param == "bucket":

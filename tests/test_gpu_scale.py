@@ -94,35 +94,38 @@ def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
     return cpu, st, slow
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact"])
 def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
-    """chain-slab: the totals through k_bin_sum's per-chunk slab (SKQ_SLAB=1)."""
-    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "1")
+    """chain-slab: the totals through k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: the
+    chained tables at the compact tables' slots (SKQ_CHAIN=2)."""
+    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
     cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode != "map1")
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact"])
 def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     """chain: k_map1 over the chained tables (SKQ_CHAIN=1); chain-slab: and the totals through
-    k_bin_sum's per-chunk slab (SKQ_SLAB=1)."""
-    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "1")
+    k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: over compact tables (SKQ_CHAIN=2)."""
+    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
     cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode != "map1")
     assert (st["chained"] > 2) == (mode != "map1"), st
+    assert (st["probe"] == "compact") == (mode == "chain-compact"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert st["max_list"] >= 10  # GENCODE-scale postings (long lists take the inline overflow)
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact"])
 def test_cfg5_multi_k_200k_transcripts(tx200k, mode, monkeypatch):
-    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB)."""
-    monkeypatch.setenv("SKQ_CHAIN", "1" if mode == "chain" else "0")
-    cpu, st, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501, chained=mode == "chain")
-    assert (st["chained"] > 2) == (mode == "chain"), st
+    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB); chain-compact: the
+    chained entries at the compact slots (SKQ_CHAIN=2, 3 x ~0.6 GB)."""
+    monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
+    cpu, st, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501, chained=mode != "map1")
+    assert (st["chained"] > 2) == (mode != "map1"), st
     assert (cpu["cand_cnt"] > 0).mean() > 0.95
     assert sl[0] > 100  # the k = 21 pass's capacity sends reads to the slow path
 
@@ -134,12 +137,12 @@ def test_full_batch_totals(tx200k, n, seed, ks, monkeypatch):
     shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it) and cfg5's batch (10M,
     multi-k passes, ~37k slow reads whose runs the slow wave writes while it reads other reads'
     packed offsets): per-transcript totals equal the oracle's over the same reads as FASTQ text.
-    Each batch runs twice against one oracle pass: over the wide entries, and over the chained
+    Each batch runs three times against one oracle pass: over the wide entries, over the chained
     tables the bench and the CLI default to (an index given the transcripts' sequences), whose
     marker entries (lists > 8 ids), queries past the table, slow-read hand-off and totals binning
-    are then checked at the full batch too."""
+    are then checked at the full batch too, and over the chained entries at the compact tables'
+    slots (SKQ_CHAIN=2), where a query that is no key lands on another key's slot."""
     L = 150
-    monkeypatch.setenv("SKQ_CHAIN", "1")
     tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
     bases, _, _ = synth.reads(tx200k, n, L, seed=seed, err=0.001)  # bench.py's batch of rank seed - 1000
     cpu = orc.fastq_map(_oracle(tables, ks, tx200k.ntx), synth.fastq_bytes(bases, L), nthreads=NTHREADS,
@@ -147,10 +150,12 @@ def test_full_batch_totals(tx200k, n, seed, ks, monkeypatch):
     assert cpu["n"] == n
     d = skq.DeviceBuffer.from_numpy(bases)
     del bases
-    for chained in (False, True):
+    for chained in (0, 1, 2):
+        monkeypatch.setenv("SKQ_CHAIN", str(max(chained, 1)))
         index = skq.Index(ks, tx200k.ntx, tables, seqs=(tx200k.seqs, tx200k.offs) if chained else None)
         st = index.stats()
-        assert (st["chained"] > 2) == chained, st  # (1 + the mean records per entry; 0: none)
+        assert (st["chained"] > 2) == bool(chained), st  # (1 + the mean records per entry; 0: none)
+        assert (st["probe"] == "compact") == (chained == 2), st
         s = skq.Session(index, n, L)
         s.map(d.ptr, None, n, L, fixed_len=L)
         s.check()

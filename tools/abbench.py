@@ -61,12 +61,20 @@ dev = torch.device("cuda", 0)
 d = torch.from_numpy(bases).to(dev)
 sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 ix, ss = {}, {}
+envb = dict(kv.split("=", 1) for kv in a.env_b.split(",") if kv)
+saved = {k_: os.environ.get(k_) for k_ in envb}
 for v, m in mods.items():
+    for k_, v_ in envb.items():  # (index switches, e.g. SKQ_CHAIN, SKQ_PROBE: read at the build)
+        if v == "B":
+            os.environ[k_] = v_
+        elif saved[k_] is None:
+            os.environ.pop(k_, None)
+        else:
+            os.environ[k_] = saved[k_]
     ix[v] = m.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs))
     ss[v] = m.Session(ix[v], n, L)
     print(v, {"A": a.lib_a, "B": a.lib_b}[v], ix[v].stats(), flush=True)
 res = {v: [] for v in mods}
-envb = dict(kv.split("=", 1) for kv in a.env_b.split(",") if kv)
 for rnd in range(a.rounds + 2):
     for v in (("A", "B") if rnd % 2 == 0 else ("B", "A")):
         s = ss[v]
@@ -74,8 +82,10 @@ for rnd in range(a.rounds + 2):
             for k_, v_ in envb.items():
                 if v == "B":
                     os.environ[k_] = v_
-                else:
+                elif saved[k_] is None:
                     os.environ.pop(k_, None)
+                else:
+                    os.environ[k_] = saved[k_]
         s.enable_timing(True)
         torch.cuda.synchronize()
         t = time.perf_counter()
