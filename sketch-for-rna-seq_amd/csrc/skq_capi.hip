@@ -1394,6 +1394,13 @@ static int map_bins_dev() {
     return v;
 }
 
+// SKQ_MAPK=0: the multi-k map as one k_map1 launch per k slot (round 4) instead of one k_mapk
+// launch (read at every map, so one process can run both)
+static bool mapk_dev() {
+    const char* e = std::getenv("SKQ_MAPK");
+    return !(e && std::atoi(e) == 0);
+}
+
 // SKQ_ABLATE (development phase pricing: k_map1 skips phases, so results are WRONG) is honoured
 // only beside SKQ_DEV=1, and announced once on stderr whenever it is active
 static uint32_t ablate_mask() {
@@ -1607,13 +1614,23 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         // 2..4 k slots: one k_map1 pass per k slot (each with the raw capacity its k needs), their
         // per-k tables in the session's ktab / kcnt; the last pass merges, filters and bins
         const uint32_t nk = s->idx->nk;
-        for (uint32_t i = 0; i < nk && !rc; ++i) {
-            skq::SketchParams pi = sp;
-            pi.kslot = i;
-            const uint32_t ml = d_offs ? max_len : fixed_len;
-            const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(ml, s->max_len), skq::LFAST));
-            rc = skq::launch_map1_pass(pi, cp, std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, pass_sigmas())),
-                                       i + 1 == nk, stream);
+        const uint32_t ml = d_offs ? max_len : fixed_len;
+        const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(ml, s->max_len), skq::LFAST));
+        uint32_t cap[SKQ_MAX_K] = {}, capmax = 0;
+        for (uint32_t i = 0; i < nk; ++i) {
+            cap[i] = std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, pass_sigmas()));
+            capmax = std::max(capmax, cap[i]);
+        }
+        // one launch for every k slot (k_mapk; SKQ_MAPK=0: one per k slot) when they share a table
+        // kind; else a launch per k slot, each with its own capacity
+        rc = mapk_dev() ? skq::launch_mapk(sp, cp, capmax, stream) : -5;
+        if (rc == -5) {
+            rc = 0;
+            for (uint32_t i = 0; i < nk && !rc; ++i) {
+                skq::SketchParams pi = sp;
+                pi.kslot = i;
+                rc = skq::launch_map1_pass(pi, cp, cap[i], i + 1 == nk, stream);
+            }
         }
     }
     if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");

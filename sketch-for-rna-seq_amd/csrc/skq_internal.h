@@ -268,6 +268,9 @@ bool map1_bins_ok();
 // for each k slot (p.kslot; a raw capacity `cap` of 16 or 32 hashes, at most the hashes' layout
 // stride p.hcap); the last (final_pass) merges the per-k tables, filters, orders and bins
 int launch_map1_pass(const SketchParams& p, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream);
+// the same passes in one launch (k_mapk: every workgroup runs the k slots in turn; one capacity for
+// all of them, and every k slot chained or none: -5 otherwise)
+int launch_mapk(const SketchParams& p, const ChainParams& cp, uint32_t cap, void* stream);
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);

@@ -124,26 +124,38 @@ inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap, uint32_t mw =
 // skipped. FINAL (the last k slot's pass): the earlier passes' entries are merged in registers with
 // this pass's table (matched only, when this k slot filters), then filtered, ordered, written and
 // binned as in the one-k map.
-template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false, int MW = WG>
-__global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
+// (the kernel's only static LDS, one instance for every body a kernel inlines: k_mapk runs several)
+template <int HCAP, int MW>
+__device__ __forceinline__ Map1Static<HCAP, MW>& map1_static() {
+    __shared__ __attribute__((aligned(16))) Map1Static<HCAP, MW> s_st;
+    return s_st;
+}
+
+// the work of one k slot ks over the workgroup's reads (k_map1: one launch per k slot; k_mapk: the
+// k slots one after another in one launch)
+// (FINAL: a constant in the k_map1 instantiations, which fold it; k_mapk passes it at run time, so
+// its loop over the k slots holds one copy of the body's code)
+template <int HCAP, int MB, int TAB, bool PASS, int MW>
+__device__ __forceinline__ void map1_body(const SketchParams& p, const ChainParams& cp, const uint32_t ks, const bool FINAL) {
     static_assert(MW == WG || MW == 64, "a workgroup of 256 threads (4 waves) or of one wave");
     constexpr size_t BC = MW == WG ? MAP1_BC_BYTES : 0;  // (the binning's bucket counters: WG only)
     // TAB 4: chained entries at the compact tables' slots (one per present key, not per possible
     // key: 0.6 GB at cfg3 instead of 27.5 GB), the misses through the compact entries
     constexpr bool CMP = TAB == 2 || TAB == 4, CHN = TAB == 3 || TAB == 4, CCH = TAB == 4;
-    static_assert(PASS || !FINAL, "the final pass is a pass");
     static_assert(!CHN || HCAP <= 32, "hit bits");
     static_assert(!CCH || SKQ_CHN_COALESCED, "compact chained entries: the coalesced hand-over (word 28)");
-    const uint32_t ks = PASS ? p.kslot : 0u;
     static_assert(HCAP >= TS && HCAP >= CCAP, "the raw rows hold the count tables and the binned region");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
+    int tid = threadIdx.x;
+    // (opaque to the optimiser: k_mapk's loop over k slots would otherwise hoist every
+    // thread-derived address out of the loop and keep them live across the whole body)
+    asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63, wv = tid >> 6;
     MAP1_STAMP(0);
     const uint32_t wc = p.tile_chunks;  // chunks per wave
     const size_t wave_bytes = p.map_wave_bytes;
     // (static LDS: the raw rows' and the roll terms' addresses fold into the instructions' offsets)
-    __shared__ __attribute__((aligned(16))) Map1Static<HCAP, MW> s_st;
+    Map1Static<HCAP, MW>& s_st = map1_static<HCAP, MW>();
     uint2* s_tab = s_st.tab;
     const uint2* s_seed = s_tab + 16;
     uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem);  // the binning's bucket counters (map1_layout)
@@ -925,7 +937,7 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
                     koff[i] = wave_incl_scan(c, lane) - c;
                 }
         }
-        if constexpr (FINAL) {
+        if (FINAL) {
             // the transcripts over the k slots, in registers: slot s holds tid ut[s] (EMPTY: free)
             // and its 8-bit counts per k slot uc[s]; this pass's table as it lies (its slots), then
             // the earlier passes' entries matched by tid — or, when this k slot does not filter
@@ -1098,6 +1110,38 @@ __global__ __launch_bounds__(MW) void k_map1(SketchParams p, ChainParams cp) {
     if constexpr (MW == WG)
         if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
     MAP1_STAMP(5);
+}
+
+// (SKQ_MAP1_WPE: a development A/B of the waves per SIMD the compiler budgets registers for; TAB 4
+// takes 107-109 VGPRs, 4 waves, where the other kinds fit 5)
+#ifndef SKQ_MAP1_WPE
+#define SKQ_MAP1_WPE 1
+#endif
+template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false, int MW = WG>
+__global__ __launch_bounds__(MW) __attribute__((amdgpu_waves_per_eu(SKQ_MAP1_WPE))) void k_map1(SketchParams p, ChainParams cp) {
+    static_assert(PASS || !FINAL, "the final pass is a pass");
+    map1_body<HCAP, MB, TAB, PASS, MW>(p, cp, PASS ? p.kslot : 0u, FINAL);
+}
+
+// Multi-k map in ONE launch: each workgroup runs the k slots' passes over its own reads one after
+// another (the same work as the k_map1 pass launches, each k slot with the same capacity HCAP and
+// table kind TAB). A pass's per-read results (pflag, status, ktab / kcnt, the staged image of the
+// bases) are read back by the same workgroup's waves in the next pass, through the CU's cache, and
+// the launches' tails are paid once. The barrier between passes: every wave is done with the roll
+// terms and its LDS region before the next pass rewrites them, and the pass's global stores are
+// complete (workgroup-scope release / acquire).
+// (its registers: 128 at 4 waves per SIMD, k_map1's ~100 for 5 plus the loop's; SKQ_MAPK_WPE=5
+// caps them at 96 with ~30 spilled, a development A/B)
+#ifndef SKQ_MAPK_WPE
+#define SKQ_MAPK_WPE 4
+#endif
+template <int HCAP, int MB, int TAB, int MW = WG>
+__global__ __launch_bounds__(MW) __attribute__((amdgpu_waves_per_eu(SKQ_MAPK_WPE))) void k_mapk(SketchParams p, ChainParams cp) {
+#pragma unroll 1
+    for (uint32_t ks = 0; ks < p.nk; ++ks) {
+        if (ks) __syncthreads();
+        map1_body<HCAP, MB, TAB, true, MW>(p, cp, ks, ks + 1 == p.nk);
+    }
 }
 
 }  // namespace skq

@@ -38,4 +38,31 @@ int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// every k slot in one launch (k_mapk): one capacity for all (the largest the k slots need) and
+// one table kind (every k slot chained, or none); -5: the k slots' table kinds differ
+int launch_mapk(const SketchParams& p0, const ChainParams& cp, uint32_t cap, void* stream) {
+    if (p0.n == 0) return 0;
+    if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.nk < 2 || p0.nk > (uint32_t)NK_FAST) return -4;
+    for (uint32_t i = 1; i < p0.nk; ++i)
+        if ((cp.chain[i] != nullptr) != (cp.chain[0] != nullptr)) return -5;
+    constexpr int MW = MAP_MW;
+    const dim3 grid((unsigned)((p0.n + MW - 1) / MW));
+    SketchParams p = p0;
+    const int tab = cp.chain[0] ? (cp.wide == 3 ? 4 : 3) : cp.wide == 3 ? 2 : 0;
+    const size_t lds = map1_layout(p, tab, cap, MW);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (cap * 8 + tab) {
+    case 128: hipLaunchKernelGGL((k_mapk<16, 4, 0, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 130: hipLaunchKernelGGL((k_mapk<16, 4, 2, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 131: hipLaunchKernelGGL((k_mapk<16, 4, 3, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 132: hipLaunchKernelGGL((k_mapk<16, 4, 4, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 256: hipLaunchKernelGGL((k_mapk<32, 4, 0, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 258: hipLaunchKernelGGL((k_mapk<32, 4, 2, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 259: hipLaunchKernelGGL((k_mapk<32, 4, 3, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 260: hipLaunchKernelGGL((k_mapk<32, 4, 4, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 }  // namespace skq

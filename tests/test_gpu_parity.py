@@ -513,10 +513,13 @@ def test_very_long_reads_and_large_postings():
         compare(out, ref, len(reads), 1)
 
 
+@pytest.mark.parametrize("mapk", ["1", "0"])
 @pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
-def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
-    """With wide or compact tables, 2-4 k slots map through the k_map1 passes (no separate count launch);
-    every other probe structure through k_sketch + a count kernel. Both bit-exact."""
+def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len, mapk, monkeypatch):
+    """With wide or compact tables, 2-4 k slots map through the k slots' passes — in one k_mapk
+    launch (SKQ_MAPK=1, the default) or one k_map1 launch each (SKQ_MAPK=0) — with no separate
+    count launch; every other probe structure through k_sketch + a count kernel. All bit-exact."""
+    monkeypatch.setenv("SKQ_MAPK", mapk)
     gi, oi = build(ks, tx=tx300)
     bases, _, _ = synth.reads(tx300, 2000, read_len, seed=77, err=0.002)
     reads = [bases[i * read_len:(i + 1) * read_len].tobytes() for i in range(2000)]
@@ -532,7 +535,7 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     s.check()
     s.enable_timing(False)
     count_launches = s.kernel_time(2)[1]
-    if probe_mode in ("wide", "compact", "chain"):
+    if probe_mode in ("wide", "compact", "chain", "chain-compact"):
         assert count_launches == 0 and s.kernel_time(0)[1] == 1
     else:
         assert count_launches == 1
@@ -545,13 +548,15 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
     np.testing.assert_array_equal(out["totals"][1], ts)
 
 
+@pytest.mark.parametrize("mapk", ["1", "0"])
 @pytest.mark.parametrize("stash", ["1", "0"])
-def test_multi_k_passes_base_image(tx300, probe_mode, monkeypatch, stash):
+def test_multi_k_passes_base_image(tx300, probe_mode, monkeypatch, stash, mapk):
     """The k_map1 passes: the first stores each wave's staged bases (2-bit codes + bad bits) and
     the later passes stage from that image (SKQ_STASH=1, the default) or re-read the bases
     (SKQ_STASH=0). Variable lengths, an unaligned buffer, bad bytes, short and > 256-bp reads and
     several batches through one session (the image grows with the batch): bit-exact both ways."""
     monkeypatch.setenv("SKQ_STASH", stash)
+    monkeypatch.setenv("SKQ_MAPK", mapk)  # (one launch for the k slots, or one per k slot)
     ks = [21, 25, 31]
     gi, oi = build(ks, tx=tx300)
     rng = random.Random(11)

@@ -119,10 +119,12 @@ def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact", "chain-launches"])
 def test_cfg5_multi_k_200k_transcripts(tx200k, mode, monkeypatch):
-    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB); chain-compact: the
-    chained entries at the compact slots (SKQ_CHAIN=2, 3 x ~0.6 GB)."""
+    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB), the passes in one
+    k_mapk launch; chain-compact: the chained entries at the compact slots (SKQ_CHAIN=2, 3 x
+    ~0.6 GB); chain-launches: one k_map1 launch per k slot (SKQ_MAPK=0)."""
+    monkeypatch.setenv("SKQ_MAPK", "0" if mode == "chain-launches" else "1")
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     cpu, st, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501, chained=mode != "map1")
     assert (st["chained"] > 2) == (mode != "map1"), st

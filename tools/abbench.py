@@ -78,7 +78,7 @@ res = {v: [] for v in mods}
 for rnd in range(a.rounds + 2):
     for v in (("A", "B") if rnd % 2 == 0 else ("B", "A")):
         s = ss[v]
-        if rnd == 0:  # (each copy reads its switches at its first map)
+        if True:  # (before every map: some switches are read once, at a copy's first map, others at every map)
             for k_, v_ in envb.items():
                 if v == "B":
                     os.environ[k_] = v_

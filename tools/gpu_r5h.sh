@@ -1,6 +1,6 @@
 #!/bin/bash
-# compact chained tables (TAB 4): parity, then same-process A/B against the chained wide tables;
-# the one-wave workgroup debug and the hashing-loop A/B
+# compact chained tables (TAB 4) and the one-launch multi-k map (k_mapk): parity, then same-process
+# A/Bs; the one-wave workgroup debug and the hashing-loop A/B; cfg2 batch-size sweep
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r5h
@@ -14,11 +14,14 @@ step() {  # name seconds cmd...: stops the script after a crash, abort or time l
     return 0
 }
 PT="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
-step parity 600 $PT tests/test_gpu_parity.py -k "chain-compact"
-step scale 600 $PT tests/test_gpu_scale.py -k "chain-compact"
+step parity 600 $PT tests/test_gpu_parity.py -k "chain-compact or multi_k"
+step scale 900 $PT tests/test_gpu_scale.py -k "chain-compact or cfg5"
+step ab_cfg5_mapk 300 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/libskq.so --config cfg5 --rounds 12 --env-b SKQ_MAPK=0
+step ab_cfg5_tab4 400 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/libskq.so --config cfg5 --rounds 12 --env-b SKQ_CHAIN=2
 step ab_cfg3 300 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/libskq.so --rounds 20 --env-b SKQ_CHAIN=2
 step ab_cfg2 300 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/libskq.so --config cfg2 --rounds 20 --env-b SKQ_CHAIN=2
+step ab_cfg5_wpe5 300 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/ab/wpe5/libskq.so --config cfg5 --rounds 12
+step ab_cfg3_tab4_wpe5 300 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/ab/wpe5/libskq.so --rounds 20 --chain 2
+step nsweep2 300 python3 tools/nsweep.py --config cfg2
 SKQ_LIB=$PWD/sketch-for-rna-seq_amd/lib/ab/wg64/libskq.so step dbg 200 python3 tools/dbg_wg64.py
 step ab_hash 300 python3 tools/abbench.py sketch-for-rna-seq_amd/lib/ab/oldhash/libskq.so --rounds 30
-step nsweep2 300 python3 tools/nsweep.py --config cfg2
-step stamps2 300 python3 tools/kbench.py --ntx 10000 --reads 1000000 --len 100 --probes wide/chain --rounds 3 --stamps
