@@ -1394,11 +1394,13 @@ static int map_bins_dev() {
     return v;
 }
 
-// SKQ_MAPK=0: the multi-k map as one k_map1 launch per k slot (round 4) instead of one k_mapk
-// launch (read at every map, so one process can run both)
+// SKQ_MAPK=1: the multi-k map as one k_mapk launch (every workgroup runs the k slots in turn)
+// instead of one k_map1 launch per k slot: 1.4 % slower at cfg5 (its loop holds 128 VGPRs, 4
+// waves per SIMD against the passes' 5; profiles/r5_mapk_ab.log), so not the default. Read at
+// every map, so one process can run both.
 static bool mapk_dev() {
     const char* e = std::getenv("SKQ_MAPK");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) == 1;
 }
 
 // SKQ_ABLATE (development phase pricing: k_map1 skips phases, so results are WRONG) is honoured
@@ -1621,8 +1623,8 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
             cap[i] = std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, pass_sigmas()));
             capmax = std::max(capmax, cap[i]);
         }
-        // one launch for every k slot (k_mapk; SKQ_MAPK=0: one per k slot) when they share a table
-        // kind; else a launch per k slot, each with its own capacity
+        // a launch per k slot, each with its own capacity (or, SKQ_MAPK=1, one k_mapk launch for
+        // them all when they share a table kind)
         rc = mapk_dev() ? skq::launch_mapk(sp, cp, capmax, stream) : -5;
         if (rc == -5) {
             rc = 0;

@@ -348,6 +348,8 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         // integer forms issue at half rate).
         const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)s_raw;
         constexpr uint32_t ROW = (uint32_t)MW * 4u;
+        constexpr uint32_t ROW_SH = MW == 256 ? 21u : 23u;  // (2^31 >> ROW_SH == ROW)
+        static_assert((0x80000000u >> ROW_SH) == ROW, "row stride");
         const uint32_t d0 = (uint32_t)tid * 4u + (uint32_t)(HCAP + 1) * ROW;
         uint32_t d = d0 - (hlo <= T ? ROW : 0u);
 #if SKQ_HASH_PAIR
@@ -408,7 +410,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                 hlo = h;
                 yprev = e[j].y;
                 *(__attribute__((address_space(3))) uint32_t*)(size_t)(rbase + d) = h;
-                uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - h, h, 0x80000000u, 0x02) >> 21
+                uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - h, h, 0x80000000u, 0x02) >> ROW_SH
                                                       : (h <= T ? ROW : 0u);
                 if (!decltype(full)::value) adv &= (uint32_t)((int)(j - (int)jn) >> 31);  // (windows past the read)
                 d -= adv;
@@ -465,7 +467,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                 roll33b(hlo, hhi, e[j]);
                 *(__attribute__((address_space(3))) uint32_t*)(size_t)(rbase + d) = hlo;
                 // (small: ~((T - h) | h) & 2^31 as one bitop3, then the shift down to ROW)
-                uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - hlo, hlo, 0x80000000u, 0x02) >> 21
+                uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - hlo, hlo, 0x80000000u, 0x02) >> ROW_SH
                                                       : (hlo <= T ? ROW : 0u);
                 if (!decltype(full)::value) adv &= (uint32_t)((int)(j - (int)jn) >> 31);  // (windows past the read)
                 d = __builtin_elementwise_sub_sat(d, adv);

@@ -120,7 +120,7 @@ def totals_from(ref, n, ntx):
 def test_probe_mode_is_selected(tx300, probe_mode):
     gi, _ = build([21, 31], tx=tx300)
     st = gi.stats()
-    base = {"chain": "wide"}.get(probe_mode, probe_mode.split("-")[0])
+    base = {"chain": "wide", "chain-compact": "compact"}.get(probe_mode, probe_mode.split("-")[0])
     assert st["probe"] == base
     assert st["device_bytes"] > 0
     assert (st["chained"] > 1) == probe_mode.startswith("chain")  # (one chained table per k slot)
@@ -516,8 +516,8 @@ def test_very_long_reads_and_large_postings():
 @pytest.mark.parametrize("mapk", ["1", "0"])
 @pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
 def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len, mapk, monkeypatch):
-    """With wide or compact tables, 2-4 k slots map through the k slots' passes — in one k_mapk
-    launch (SKQ_MAPK=1, the default) or one k_map1 launch each (SKQ_MAPK=0) — with no separate
+    """With wide or compact tables, 2-4 k slots map through the k slots' passes — one k_map1
+    launch each (the default) or one k_mapk launch for all (SKQ_MAPK=1) — with no separate
     count launch; every other probe structure through k_sketch + a count kernel. All bit-exact."""
     monkeypatch.setenv("SKQ_MAPK", mapk)
     gi, oi = build(ks, tx=tx300)

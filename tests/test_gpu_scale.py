@@ -119,12 +119,12 @@ def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact", "chain-launches"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact", "chain-mapk"])
 def test_cfg5_multi_k_200k_transcripts(tx200k, mode, monkeypatch):
-    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB), the passes in one
-    k_mapk launch; chain-compact: the chained entries at the compact slots (SKQ_CHAIN=2, 3 x
-    ~0.6 GB); chain-launches: one k_map1 launch per k slot (SKQ_MAPK=0)."""
-    monkeypatch.setenv("SKQ_MAPK", "0" if mode == "chain-launches" else "1")
+    """chain: every k slot's pass over its own chained tables (3 x 27.5 GB), one k_map1 launch
+    each; chain-compact: the chained entries at the compact slots (SKQ_CHAIN=2, 3 x ~0.6 GB);
+    chain-mapk: the passes in one k_mapk launch (SKQ_MAPK=1)."""
+    monkeypatch.setenv("SKQ_MAPK", "1" if mode == "chain-mapk" else "0")
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     cpu, st, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501, chained=mode != "map1")
     assert (st["chained"] > 2) == (mode != "map1"), st
