@@ -1333,6 +1333,8 @@ static int ensure_side(skq_session* s) {
 // (small batches: the extra stream hand-offs cost more than the overlap gains; with the grouped
 // k_bin_sum for few buckets, 1M reads run 5 % faster forked, 10M reads too)
 static bool totals_fork(const skq::ChainParams& p, int accumulate) {
+    const char* e = std::getenv("SKQ_TOTALS_FORK");  // (0: on the launch stream; development A/B)
+    if (e && std::atoi(e) == 0) return false;
     return accumulate && p.slow_totals && p.n >= (1u << 19);
 }
 
@@ -1387,11 +1389,8 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
 // SKQ_MAP_BINS=1 (development A/B): k_map1 bins its candidates in its own epilogue (round 4)
 // instead of k_bin_packed after it
 static int map_bins_dev() {
-    static const int v = [] {
-        const char* e = std::getenv("SKQ_MAP_BINS");
-        return e && std::atoi(e) == 1 ? 1 : 0;
-    }();
-    return v;
+    const char* e = std::getenv("SKQ_MAP_BINS");
+    return e && std::atoi(e) == 1 ? 1 : 0;
 }
 
 // SKQ_MAPK=1: the multi-k map as one k_mapk launch (every workgroup runs the k slots in turn)
