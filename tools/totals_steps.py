@@ -22,13 +22,15 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--ntx", type=int, default=200_000)
 ap.add_argument("--reads", type=int, default=10_000_000)
 ap.add_argument("--len", type=int, default=150)
+ap.add_argument("--ks", default="31")
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--variants", default="", help="K=V[+K=V],... env sets run in turn (interleaved rounds)")
 ap.add_argument("--rounds", type=int, default=3)
 a = ap.parse_args()
 tx = synth.transcriptome(a.ntx, seed=1)
-tables = skq.build_tables(tx.seqs, tx.offs, [31], nthreads=16)
-ix = skq.Index([31], tx.ntx, tables, seqs=(tx.seqs, tx.offs))
+ks = [int(x) for x in a.ks.split(",")]
+tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
+ix = skq.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs))
 bases, _, _ = synth.reads(tx, a.reads, a.len, seed=1000, err=0.001)
 d = torch.from_numpy(bases).to("cuda:0")
 sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
