@@ -1008,13 +1008,36 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
     }
     const bool chain_ok = seqs && seq_offs && nk <= (uint32_t)skq::NK_FAST && ix->ntx <= (1u << 22) &&
                           ix->nlist_words < 0x80000000ull;
-    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals, lists, cm == 2 && chain_ok)) {
+    // the index sized by the device: wide entries + chained tables per possible key where both fit
+    // (the fastest), else compact entries + chained tables per present key (cfg3: 0.77 GB against
+    // 34.4 GB, k_map1 19 % slower, and 20 % faster than the wide entries alone)
+    bool prefer_compact = cm == 2 && chain_ok;
+    if (cm == 1 && chain_ok && !std::getenv("SKQ_PROBE")) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            uint64_t wide = 0, budget = 49152ull << 20, cbudget = 65536ull << 20;
+            if (const char* e = std::getenv("SKQ_DIRECT_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
+            if (const char* e = std::getenv("SKQ_CHAIN_MB")) cbudget = std::strtoull(e, nullptr, 10) << 20;
+            for (uint32_t t = 0; t < ntables; ++t) wide += dkeys[t].empty() ? 0 : ((uint64_t)dkeys[t].back() + 1) * 32;
+            bool fits = wide <= budget && wide <= fr / 2;  // (build_direct's rule for the wide entries)
+            uint64_t f = fr > wide ? fr - wide : 0;
+            for (uint32_t i = 0; i < nk && fits; ++i)  // (build_chain's rule, slot by slot)
+                for (uint32_t t = 0; t < ntables; ++t)
+                    if (tables[t].k == ks[i] && !dkeys[t].empty()) {
+                        const uint64_t c = ((uint64_t)dkeys[t].back() + 1) * 128;
+                        fits = f >= (32ull << 30) && c <= (f - (32ull << 30)) / 2 && c <= cbudget;
+                        f -= fits ? c : 0;
+                    }
+            prefer_compact = !fits;
+        }
+    }
+    if (int rc2 = build_direct(ix, ntables, tables, dkeys, dvals, lists, prefer_compact)) {
         skq_index_free(ix);
         return rc2;
     }
-    // chained tables (per k slot, ids within 22 bits, transcripts given): the default wherever
-    // they fit (SKQ_CHAIN = 0 turns them off; cfg3: k_map1 1.15 against 1.35 ms over the wide
-    // entries); a slot whose table does not fit keeps the wide entries alone
+    // chained tables (per k slot, ids within 22 bits, transcripts given): the default (SKQ_CHAIN = 0
+    // turns them off; cfg3: k_map1 0.91 against 1.35 ms over the wide entries alone);
+    // a slot whose table does not fit after all keeps the probe entries alone
     // (the entry list behind the chain step gathers wide or compact entries)
     if (chain_ok && cm != 0 && (ix->mode == 3 || ix->mode == 5))
         for (uint32_t i = 0; i < nk; ++i)

@@ -94,15 +94,24 @@ def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
     return cpu, st, slow
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact", "chain-tight"])
 def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
     """chain-slab: the totals through k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: the
-    chained tables at the compact tables' slots (SKQ_CHAIN=2)."""
+    chained tables at the compact tables' slots (SKQ_CHAIN=2); chain-tight: a device budget the
+    chained tables per possible key do not fit (SKQ_CHAIN_MB=2048), so the index sizes itself to
+    compact entries + chained tables per present key."""
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
+    if mode == "chain-tight":
+        monkeypatch.setenv("SKQ_CHAIN_MB", "2048")
     cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode != "map1")
     assert (cpu["cand_cnt"] > 0).mean() > 0.9
     assert st["probe"] in ("compact", "wide", "hash")
+    if mode != "map1":
+        assert st["chained"] > 2, st
+        assert (st["probe"] == "compact") == (mode in ("chain-compact", "chain-tight")), st
+        if st["probe"] == "compact":
+            assert st["device_bytes"] < 2e9, st
 
 
 @pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact"])
