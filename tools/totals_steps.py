@@ -34,9 +34,14 @@ ix = skq.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs))
 bases, _, _ = synth.reads(tx, a.reads, a.len, seed=1000, err=0.001)
 d = torch.from_numpy(bases).to("cuda:0")
 sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-s = skq.Session(ix, a.reads, a.len)
 variants = [dict(kv.split("=", 1) for kv in v.split("+") if kv) for v in a.variants.split(",")] if a.variants else [{}]
 keys = sorted({k for v in variants for k in v})
+sessions = []
+for v in variants:  # (a session per variant: some switches, e.g. SKQ_BIN_BITS, are read at its creation)
+    for k in keys:
+        os.environ.pop(k, None)
+    os.environ.update(v)
+    sessions.append(skq.Session(ix, a.reads, a.len))
 res = {i: [] for i in range(len(variants))}
 ref = None
 for rnd in range(a.rounds + 1):
@@ -44,6 +49,7 @@ for rnd in range(a.rounds + 1):
         for k in keys:
             os.environ.pop(k, None)
         os.environ.update(v)
+        s = sessions[i]
         s.reset_totals(sp)
         for _ in range(2):
             s.map(d.data_ptr(), None, a.reads, a.len, fixed_len=a.len, stream=sp, accumulate=True)
