@@ -1159,6 +1159,9 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     s->cand_cnt_b[0] = s->cand_cnt;
     s->cand_tid_b[0] = s->cand_tid;
     // totals buckets: at most WG buckets of at most 2^14 ids (the LDS histogram), else direct
+    // (2^12-id buckets for large transcript sets, 2^13 for small ones: cfg3 1.071 against 1.094 ms
+    // per step with 1024 k_bin_sum workgroups, cfg2 the same either way; profiles/r5_totals_sweep.log)
+    s->bin_bits = ix->ntx > (1u << 16) ? 12u : 13u;
     if (const char* e = std::getenv("SKQ_BIN_BITS")) s->bin_bits = (uint32_t)std::max(8, std::min(14, std::atoi(e)));  // (A/B)
     while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
     s->bin_nb = s->bin_bits <= 14 ? (uint32_t)(((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits) : 0u;

@@ -3073,9 +3073,10 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
         if (hipGetLastError() != hipSuccess) return -2;
     }
     if (nb == 0) return 0;
-    // about two workgroups per CU in flight: chunks * nb ~ 512 (SKQ_BIN_WGS, read at every launch:
-    // other counts, development A/B; at most 512 with the slab, which is sized for that many)
-    uint32_t wgs = 512;
+    // chunks * nb ~ 512 workgroups, 1024 for many buckets (their bins are 32 KiB: four workgroups
+    // per CU) (SKQ_BIN_WGS, read at every launch: other counts, development A/B; at most 512 with
+    // the slab, which is sized for that many)
+    uint32_t wgs = nb >= 16 && !p.tx_slab ? 1024 : 512;
     if (const char* e = std::getenv("SKQ_BIN_WGS")) wgs = (uint32_t)std::max(1, std::min(p.tx_slab ? 512 : 8192, std::atoi(e)));
     const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nW, wgs / nb));
     const uint32_t chunk = (nW + chunks - 1) / chunks;
