@@ -48,6 +48,8 @@ def _args(argv=None):
     ap.add_argument("--chunk-mb", type=int, default=64, help="end to end: FASTQ chunk (MiB)")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the FASTQ-file -> EM leg reported beside the kernel path")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="development A/B: no per-kernel HIP events in the timed steps (the roofline then has no launch time)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="N = 1, default config: skip the cfg2 and cfg5 legs reported under `configs`")
     ap.add_argument("--dist-backend", default="nccl",
@@ -375,7 +377,7 @@ def measure(cname, cfg, args, rank, world, dev, gpu, sample, totals_dev=True):
     sess.check(sp)
     for kind in range(4):
         sess.kernel_time(kind)
-    sess.enable_timing(True)
+    sess.enable_timing(not args.no_kernel_timing)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
