@@ -135,6 +135,7 @@ struct skq_session {
     // [0] the arrays above, [1] allocated on first use; cand_cnt / cand_tid point at the current pair
     uint32_t* cand_cnt_b[2] = {};
     uint32_t* cand_tid_b[2] = {};
+    uint32_t* cand_wtot_b[2] = {};  // per wave of 64 reads: its packed candidate words (k_bin_packed)
     uint32_t* cand_ext = nullptr;
     uint64_t cand_ext_cap = 0;
     uint64_t* scratch = nullptr;
@@ -1148,6 +1149,7 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
         (rc = dev_alloc(&s->ovf4, s->ovf_cap)) || (rc = dev_alloc(&s->cand_cnt, max_reads)) ||
         (rc = dev_alloc(&s->pflag, max_reads)) ||
         (rc = dev_alloc(&s->cand_tid, max_reads * skq::CCAP)) ||
+        (rc = dev_alloc(&s->cand_wtot_b[0], (max_reads + 63) / 64)) ||
         (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
         (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
         (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
@@ -1223,6 +1225,8 @@ int skq_session_free(skq_session* s) {
     dev_free(s->cand_score);
     dev_free(s->cand_cnt_b[1]);
     dev_free(s->cand_tid_b[1]);
+    dev_free(s->cand_wtot_b[0]);
+    dev_free(s->cand_wtot_b[1]);
     dev_free(s->cand_ext);
     dev_free(s->scratch);
     for (int b = 0; b < 2; ++b) {
@@ -1620,9 +1624,11 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     const bool side_bins = totals_fork(cp, accumulate) && cp.cpack && !cp.map_bins;
     if (side_bins && s->bin_par == 1) {
         if (!s->cand_tid_b[1]) {
-            if (dev_alloc(&s->cand_tid_b[1], s->max_reads * skq::CCAP) || dev_alloc(&s->cand_cnt_b[1], s->max_reads)) {
+            if (dev_alloc(&s->cand_tid_b[1], s->max_reads * skq::CCAP) || dev_alloc(&s->cand_cnt_b[1], s->max_reads) ||
+                dev_alloc(&s->cand_wtot_b[1], (s->max_reads + 63) / 64)) {
                 dev_free(s->cand_tid_b[1]);
                 dev_free(s->cand_cnt_b[1]);
+                dev_free(s->cand_wtot_b[1]);
                 (void)hipGetLastError();
             }
         }
@@ -1632,6 +1638,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         if (int rc = wait_totals(s, st)) return rc;
     s->cand_cnt = cp.cand_cnt = s->cand_cnt_b[par];
     s->cand_tid = cp.cand_tid = s->cand_tid_b[par];
+    cp.cand_wtot = s->cand_wtot_b[par];
     hipEvent_t t0{};
     record(s, 0, &t0, st);
     int rc = 0;

@@ -159,6 +159,7 @@ struct ChainParams {
     DevTable tabs[SKQ_MAX_K];
     uint32_t* cand_cnt;
     uint32_t* cand_tid;
+    uint32_t* cand_wtot;  // (fused map, packed) per wave of 64 reads: its packed candidate words (k_bin_packed)
     uint32_t* cand_score;
     uint32_t* cand_ext;
     uint64_t cand_ext_cap;     // pairs

@@ -2694,23 +2694,34 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
     __shared__ uint32_t s_bc[WG + 1];
     __shared__ __attribute__((aligned(16))) uint32_t s_reg[WG * CCAP];
     const uint32_t t = threadIdx.x, w = blockIdx.x, lane = t & 63;
-    const uint64_t r = (uint64_t)w * WG + t;
     s_bc[t] = 0;
     if (t == 0) s_bc[WG] = 0;
-    const uint32_t c = r < p.n ? p.cand_cnt[r] : 0u;
-    const uint32_t nc = (c & CAND_EXT) ? 0u : min(c, (uint32_t)CCAP);
-    const uint32_t incl = wave_incl_scan(nc, lane);
-    const uint32_t* src = p.cand_tid + (r - lane) * CCAP + (incl - nc);
-    uint32_t key[CCAP];
+    // each wave takes one map wave's region: its packed words [0, tot) (ChainParams::cand_wtot, the
+    // map's own count of them) read coalesced, 16 B per lane per round of 256 words. A full wave's
+    // first round is loaded beside its count, not after it (the region is allocated whatever its
+    // fill; the words past tot are masked), so the kernel waits on one memory round trip, where the
+    // per-read counts, their scan and then each lane's own run took two and touched a line per lane
+    const uint64_t W = (uint64_t)w * (WG / 64) + (t >> 6), r0 = W * 64;  // (the map wave)
+    const uint32_t tot = r0 < p.n ? p.cand_wtot[W] : 0u;  // (wave-uniform)
+    const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + r0 * CCAP) + lane;
+    const uint32_t lim = r0 + 64 <= p.n ? 256u : tot;  // (a partial last wave: only what it holds)
+    constexpr int R = 64 * CCAP / 256;  // rounds of a full region
+    uint4 x[R];
 #pragma unroll
-    for (int d = 0; d < CCAP; ++d) {
-        if (!__any((uint32_t)d < nc)) break;  // (uniform: the wave's longest list)
-        key[d] = (uint32_t)d < nc ? src[d] : 0u;
+    for (int q = 0; q < R; ++q) {
+        const uint32_t e = q * 256 + lane * 4;
+        const bool ld = q == 0 ? e < lim : e < tot;
+        x[q] = ld ? src[q * 64] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    const uint32_t mask = (1u << bits) - 1u;
 #pragma unroll
-    for (int d = 0; d < CCAP; ++d)
-        if ((uint32_t)d < nc) atomicAdd(&s_bc[(key[d] & 0x3FFFFFu) >> bits], 1u);
+    for (int q = 0; q < R; ++q) {
+        const uint32_t xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (q * 256 + lane * 4 + i < tot) atomicAdd(&s_bc[(xs[i] & 0x3FFFFFu) >> bits], 1u);
+    }
     __syncthreads();
     if (t < 64) {  // one wave scans the (<= 256) bucket counts, 4 per lane
         uint32_t c4[4], sum = 0;
@@ -2735,11 +2746,15 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
     }
     __syncthreads();
 #pragma unroll
-    for (int d = 0; d < CCAP; ++d) {
-        if ((uint32_t)d >= nc) continue;
-        const uint32_t tid = key[d] & 0x3FFFFFu, score = key[d] >> 22;
-        const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
-        s_reg[pos] = (tid & ((1u << bits) - 1u)) | (score << bits);
+    for (int q = 0; q < R; ++q) {
+        const uint32_t xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (q * 256 + lane * 4 + i >= tot) continue;
+            const uint32_t tid = xs[i] & 0x3FFFFFu, score = xs[i] >> 22;
+            const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
+            s_reg[pos] = (tid & mask) | (score << bits);
+        }
     }
     __syncthreads();
     const uint32_t total = s_bc[nb - 1];
@@ -2776,44 +2791,56 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
     for (uint32_t i = t; i < bs; i += WG) s_bins[i] = 0;
     __syncthreads();
     const uint32_t w0 = blockIdx.x * chunk, w1 = min(nW, w0 + chunk);
-    // one lane per region (the header loads of WG regions are coalesced); a segment holds ~32
+    // one lane per region (the header loads of WG regions are coalesced); a segment holds ~16-32
     // entries, read as 16-B words (a lane's load is one line-request for 4 entries, not 1: the
-    // texture addresser works per lane-request), 4 in flight, and the next region's header is
-    // read ahead (two workgroups per CU, 64 KiB of bins each)
+    // texture addresser works per lane-request), U in flight per segment, TWO regions' segments
+    // in flight together and the next pair's headers read ahead (the walk is a chain of dependent
+    // round trips: two segments per round halve it)
     constexpr int U = 4;
     uint32_t w = w0 + t;
-    uint32_t s0 = 0, s1 = 0;
-    if (w < w1) {
-        s0 = hdr[(uint64_t)b * nW + w];
-        s1 = hdr[(uint64_t)(b + 1) * nW + w];
-    }
-    while (w < w1) {
-        const uint32_t* reg = region + (uint64_t)w * rstride;
-        const uint32_t wn = w + WG;
-        uint32_t n0 = 0, n1 = 0;
-        if (wn < w1) {
-            n0 = hdr[(uint64_t)b * nW + wn];
-            n1 = hdr[(uint64_t)(b + 1) * nW + wn];
+    auto head = [&](uint32_t x, uint32_t& a, uint32_t& e) {
+        a = e = 0;
+        if (x < w1) {
+            a = hdr[(uint64_t)b * nW + x];
+            e = hdr[(uint64_t)(b + 1) * nW + x];
         }
-        const uint4* reg4 = reinterpret_cast<const uint4*>(reg);  // (regions are 16-B aligned)
-        for (uint32_t q = s0 & ~3u; q < s1; q += 4 * U) {
-            uint4 x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = reg4[min(q / 4 + u, (s1 - 1) / 4)];
+    };
+    uint32_t sa0, sa1, sb0, sb1;
+    head(w, sa0, sa1);
+    head(w + WG, sb0, sb1);
+    const uint32_t msk = bs - 1u;
+    while (w < w1) {
+        const uint4* ra = reinterpret_cast<const uint4*>(region + (uint64_t)w * rstride);  // (16-B aligned)
+        const uint4* rb = reinterpret_cast<const uint4*>(region + (uint64_t)(w + WG) * rstride);
+        uint32_t na0, na1, nb0, nb1;
+        head(w + 2 * WG, na0, na1);
+        head(w + 3 * WG, nb0, nb1);
+        for (uint32_t k = 0;; k += 4 * U) {
+            const uint32_t qa = (sa0 & ~3u) + k, qb = (sb0 & ~3u) + k;
+            const bool ma = qa < sa1, mb = qb < sb1;
+            if (!ma && !mb) break;
+            uint4 xa[U], xb[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+                xa[u] = ma ? ra[min(qa / 4 + u, (sa1 - 1) / 4)] : make_uint4(0, 0, 0, 0);
+                xb[u] = mb ? rb[min(qb / 4 + u, (sb1 - 1) / 4)] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t ya[4] = {xa[u].x, xa[u].y, xa[u].z, xa[u].w};
+                const uint32_t yb[4] = {xb[u].x, xb[u].y, xb[u].z, xb[u].w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const uint32_t j = q + 4 * u + i;
-                    if (j >= s0 && j < s1)
-                        atomicAdd(&s_bins[xs[i] & (bs - 1u)], (1ull << 40) | (unsigned long long)(xs[i] >> bits));
+                    const uint32_t ja = qa + 4 * u + i, jb = qb + 4 * u + i;
+                    if (ma && ja >= sa0 && ja < sa1)
+                        atomicAdd(&s_bins[ya[i] & msk], (1ull << 40) | (unsigned long long)(ya[i] >> bits));
+                    if (mb && jb >= sb0 && jb < sb1)
+                        atomicAdd(&s_bins[yb[i] & msk], (1ull << 40) | (unsigned long long)(yb[i] >> bits));
                 }
             }
         }
-        w = wn;
-        s0 = n0;
-        s1 = n1;
+        w += 2 * WG;
+        sa0 = na0, sa1 = na1, sb0 = nb0, sb1 = nb1;
     }
     __syncthreads();
     bins_out(s_bins, bs, b, nb, ntx, tx_acc, slab);

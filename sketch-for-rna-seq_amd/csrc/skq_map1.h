@@ -1052,6 +1052,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
             }
             if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
                 const uint32_t incl = wave_incl_scan(nc, lane);
+                if (lane == 63 && cp.cand_wtot && nr) cp.cand_wtot[r0 >> 6] = incl;  // (k_bin_packed)
                 wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64),
                                     reinterpret_cast<uint32_t*>(s_wave), lane, [&](int d) { return (uint32_t)d < nc; },
                                     [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
@@ -1100,6 +1101,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         }
         if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
             const uint32_t incl = wave_incl_scan(nc, lane);
+            if (lane == 63 && cp.cand_wtot && nr) cp.cand_wtot[r0 >> 6] = incl;  // (k_bin_packed)
             // (the wave's region: the entry list and the per-read flags are dead)
             wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64), reinterpret_cast<uint32_t*>(s_wave),
                                 lane, [&](int d) { return (uint32_t)d < nc; },
