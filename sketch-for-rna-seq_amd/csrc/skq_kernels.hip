@@ -2689,10 +2689,17 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
 // alternate by batch parity, so that map writes the other pair). A read the slow paths took has
 // no share of its wave's region (its count word is 0 or, once they have run, a CAND_EXT mark) and
 // adds its totals itself.
+// CAPW: the staged region's capacity in words. The default, 1,280 (a workgroup's 256 reads carry
+// ~800 candidates at cfg3), keeps the kernel's LDS at ~6 KB, which fits beside five k_map1
+// workgroups (~156 KB of a CU's 160), so on the side stream it runs next to the next batch's map
+// instead of waiting for a map workgroup's LDS; a workgroup with more candidates adds them all
+// directly (64-bit atomics into the running totals) and leaves its region empty.
+template <uint32_t CAPW>
 __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW,
                                                    uint32_t* hdr, uint32_t* region) {
     __shared__ uint32_t s_bc[WG + 1];
-    __shared__ __attribute__((aligned(16))) uint32_t s_reg[WG * CCAP];
+    __shared__ uint32_t s_tot;
+    __shared__ __attribute__((aligned(16))) uint32_t s_reg[CAPW];
     const uint32_t t = threadIdx.x, w = blockIdx.x, lane = t & 63;
     s_bc[t] = 0;
     if (t == 0) s_bc[WG] = 0;
@@ -2732,19 +2739,25 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
             sum += c4[u];
         }
         const uint32_t bi = wave_incl_scan(sum, t);
+        const uint32_t all = __shfl(bi, 63, 64);
+        const bool fits = all <= CAPW;
         uint32_t run = bi - sum;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t b = 4 * t + u;
             if (b < nb) {
-                hdr[(uint64_t)b * nW + w] = run;
+                hdr[(uint64_t)b * nW + w] = fits ? run : 0u;
                 s_bc[b] = run;
             }
             run += c4[u];
         }
-        if (t == 63) hdr[(uint64_t)nb * nW + w] = bi;
+        if (t == 63) {
+            hdr[(uint64_t)nb * nW + w] = fits ? bi : 0u;
+            s_tot = bi;
+        }
     }
     __syncthreads();
+    const bool fits = s_tot <= CAPW;  // (uniform)
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const uint32_t xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
@@ -2752,15 +2765,20 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
         for (int i = 0; i < 4; ++i) {
             if (q * 256 + lane * 4 + i >= tot) continue;
             const uint32_t tid = xs[i] & 0x3FFFFFu, score = xs[i] >> 22;
-            const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
-            s_reg[pos] = (tid & mask) | (score << bits);
+            if (fits) {
+                const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
+                s_reg[pos] = (tid & mask) | (score << bits);
+            } else {  // (more candidates than the staging holds: straight into the totals)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid]), 1ull);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
+            }
         }
     }
+    if (!fits) return;  // (uniform)
     __syncthreads();
-    const uint32_t total = s_bc[nb - 1];
     uint4* reg = reinterpret_cast<uint4*>(region + (uint64_t)w * (WG * CCAP));
     const uint4* sr = reinterpret_cast<const uint4*>(s_reg);
-    for (uint32_t q = t; q < (total + 3) / 4; q += WG) reg[q] = sr[q];
+    for (uint32_t q = t; q < (s_tot + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
 // the workgroup's bins out: to its slab slot with plain coalesced stores (k_fold_slab sums the
@@ -3082,8 +3100,17 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     const uint32_t* region = p.bin_region;
     if (nb > (uint32_t)WG) return -1;
     if (!binned) {
-        if (p.cpack && nb)  // (the fused map's packed candidates)
-            hipLaunchKernelGGL(k_bin_packed, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+        if (p.cpack && nb) {  // (the fused map's packed candidates; SKQ_BINP_CAP: 1 the full staging
+            // (development A/B), 2 a 64-word one, so nearly every workgroup takes the direct adds (tests))
+            const char* e = std::getenv("SKQ_BINP_CAP");
+            const int cap = e ? std::atoi(e) : 0;
+            if (cap == 1)
+                hipLaunchKernelGGL(k_bin_packed<WG * CCAP>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+            else if (cap == 2)
+                hipLaunchKernelGGL(k_bin_packed<64>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+            else
+                hipLaunchKernelGGL(k_bin_packed<1280>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+        }
         else
             hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
         if (hipGetLastError() != hipSuccess) return -2;

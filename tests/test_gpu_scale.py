@@ -114,10 +114,13 @@ def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
             assert st["device_bytes"] < 2e9, st
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact", "chain-binp-direct"])
 def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     """chain: k_map1 over the chained tables (SKQ_CHAIN=1); chain-slab: and the totals through
-    k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: over compact tables (SKQ_CHAIN=2)."""
+    k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: over compact tables (SKQ_CHAIN=2);
+    chain-binp-direct: k_bin_packed with a 64-word staging (SKQ_BINP_CAP=2), so its workgroups add
+    their candidates straight into the totals."""
+    monkeypatch.setenv("SKQ_BINP_CAP", "2" if mode == "chain-binp-direct" else "0")
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
     cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode != "map1")
