@@ -2689,11 +2689,10 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
 // alternate by batch parity, so that map writes the other pair). A read the slow paths took has
 // no share of its wave's region (its count word is 0 or, once they have run, a CAND_EXT mark) and
 // adds its totals itself.
-// CAPW: the staged region's capacity in words. The default, 1,280 (a workgroup's 256 reads carry
-// ~800 candidates at cfg3), keeps the kernel's LDS at ~6 KB, which fits beside five k_map1
-// workgroups (~156 KB of a CU's 160), so on the side stream it runs next to the next batch's map
-// instead of waiting for a map workgroup's LDS; a workgroup with more candidates adds them all
-// directly (64-bit atomics into the running totals) and leaves its region empty.
+// CAPW: the staged region's capacity in words: WG * CCAP (every candidate a workgroup can have),
+// or less — a workgroup with more candidates than that adds them all directly (64-bit atomics into
+// the running totals) and leaves its region empty. (1,280 words, ~6 KB of LDS, would fit beside
+// five k_map1 workgroups on a CU: measured no faster, launch_bin.)
 template <uint32_t CAPW>
 __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW,
                                                    uint32_t* hdr, uint32_t* region) {
@@ -3100,16 +3099,18 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     const uint32_t* region = p.bin_region;
     if (nb > (uint32_t)WG) return -1;
     if (!binned) {
-        if (p.cpack && nb) {  // (the fused map's packed candidates; SKQ_BINP_CAP: 1 the full staging
-            // (development A/B), 2 a 64-word one, so nearly every workgroup takes the direct adds (tests))
+        if (p.cpack && nb) {  // (the fused map's packed candidates; SKQ_BINP_CAP: 3 a 1,280-word staging
+            // (development A/B: beside five map workgroups; 1.078 against 1.074 ms per cfg3 step, so
+            // not kept, profiles/r5_totals_kernels_ab.log), 2 a 64-word one, so nearly every
+            // workgroup takes the direct adds (tests))
             const char* e = std::getenv("SKQ_BINP_CAP");
             const int cap = e ? std::atoi(e) : 0;
-            if (cap == 1)
-                hipLaunchKernelGGL(k_bin_packed<WG * CCAP>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+            if (cap == 3)
+                hipLaunchKernelGGL(k_bin_packed<1280>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
             else if (cap == 2)
                 hipLaunchKernelGGL(k_bin_packed<64>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
             else
-                hipLaunchKernelGGL(k_bin_packed<1280>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+                hipLaunchKernelGGL(k_bin_packed<WG * CCAP>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
         }
         else
             hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
