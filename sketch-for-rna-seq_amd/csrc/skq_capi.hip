@@ -1612,7 +1612,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     // candidates packed too, unless the totals would be binned from the padded rows (k_bin)
     s->cand_packed = s->hash_packed && (!accumulate || cp.slow_totals);
     cp.cpack = s->cand_packed ? 1u : 0u;
-    cp.map_bins = map_bins_dev() && skq::map1_bins_ok();
+    cp.map_bins = map_bins_dev() && (s->idx->nk == 1 ? skq::map1_bins_ok() : skq::pass_bins_ok());
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));

@@ -265,6 +265,8 @@ int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid = 2048
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
 // whether k_map1 runs four-wave workgroups, which can bin in their epilogue (map_bins)
 bool map1_bins_ok();
+// (the same for the multi-k passes, skq_map1_pass.hip)
+bool pass_bins_ok();
 // fused sketch + chain for 2..4 k slots (wide or compact tables) by passes: k_map1 in pass mode
 // for each k slot (p.kslot; a raw capacity `cap` of 16 or 32 hashes, at most the hashes' layout
 // stride p.hcap); the last (final_pass) merges the per-k tables, filters, orders and bins

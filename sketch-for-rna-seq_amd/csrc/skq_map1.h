@@ -22,6 +22,13 @@ constexpr uint32_t MAP_P = 512;
 #define SKQ_MAP_WG 256
 #endif
 constexpr int MAP_MW = SKQ_MAP_WG;
+// threads per workgroup of the multi-k passes (k_map1 PASS, k_mapk): one wave, whose LDS is
+// released when it ends (cfg5 4.6 % faster than four-wave workgroups; one k: 3.8 % slower,
+// profiles/r5_wg64_ab.log)
+#ifndef SKQ_PASS_WG
+#define SKQ_PASS_WG 64
+#endif
+constexpr int PASS_MW = SKQ_PASS_WG;
 constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 // A wave's packed output (lane-ordered runs: this lane's words from its exclusive offset `off`
 // of the wave's `tot`, word j present when has(j), valued val(j)) to 16-B aligned g through the

@@ -6,10 +6,12 @@
 
 namespace skq {
 
+bool pass_bins_ok() { return PASS_MW == WG; }
+
 int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
     if (p0.n == 0) return 0;
     if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.kslot >= SKQ_MAX_K) return -4;
-    constexpr int MW = MAP_MW;
+    constexpr int MW = PASS_MW;
     const dim3 grid((unsigned)((p0.n + MW - 1) / MW));
     SketchParams p = p0;
     // (the pass's k slot has chained tables: TAB 3 over wide entries, 4 over compact ones)
@@ -45,7 +47,7 @@ int launch_mapk(const SketchParams& p0, const ChainParams& cp, uint32_t cap, voi
     if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.nk < 2 || p0.nk > (uint32_t)NK_FAST) return -4;
     for (uint32_t i = 1; i < p0.nk; ++i)
         if ((cp.chain[i] != nullptr) != (cp.chain[0] != nullptr)) return -5;
-    constexpr int MW = MAP_MW;
+    constexpr int MW = PASS_MW;
     const dim3 grid((unsigned)((p0.n + MW - 1) / MW));
     SketchParams p = p0;
     const int tab = cp.chain[0] ? (cp.wide == 3 ? 4 : 3) : cp.wide == 3 ? 2 : 0;
