@@ -144,7 +144,7 @@ __device__ __forceinline__ Map1Static<HCAP, MW>& map1_static() {
 // its loop over the k slots holds one copy of the body's code)
 template <int HCAP, int MB, int TAB, bool PASS, int MW>
 __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainParams& cp, const uint32_t ks, const bool FINAL) {
-    static_assert(MW == WG || MW == 64, "a workgroup of 256 threads (4 waves) or of one wave");
+    static_assert(MW == WG || MW == 64 || MW == 128, "a workgroup of 256 threads (4 waves), of two or of one");
     constexpr size_t BC = MW == WG ? MAP1_BC_BYTES : 0;  // (the binning's bucket counters: WG only)
     // TAB 4: chained entries at the compact tables' slots (one per present key, not per possible
     // key: 0.6 GB at cfg3 instead of 27.5 GB), the misses through the compact entries
@@ -355,7 +355,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         // integer forms issue at half rate).
         const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)s_raw;
         constexpr uint32_t ROW = (uint32_t)MW * 4u;
-        constexpr uint32_t ROW_SH = MW == 256 ? 21u : 23u;  // (2^31 >> ROW_SH == ROW)
+        constexpr uint32_t ROW_SH = MW == 256 ? 21u : MW == 128 ? 22u : 23u;  // (2^31 >> ROW_SH == ROW)
         static_assert((0x80000000u >> ROW_SH) == ROW, "row stride");
         const uint32_t d0 = (uint32_t)tid * 4u + (uint32_t)(HCAP + 1) * ROW;
         uint32_t d = d0 - (hlo <= T ? ROW : 0u);
