@@ -51,8 +51,8 @@ launches = []
 acc = collections.Counter()
 npass = 0
 for d in sorted(disp):
-    if grid[d] != full:
-        continue  # (the parity sample and other sizes)
+    if not a.reads <= grid[d] < a.reads + 256:
+        continue  # (the parity sample and other sizes; workgroups of 64 or 256 threads)
     is_pass, is_final = targs(name[d])
     if not is_pass:
         launches.append(dict(disp[d]))  # one k slot: this dispatch is the launch
