@@ -791,7 +791,9 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
         if (!known) return fail(-1, std::string("SKQ_PROBE: unknown probe kind ") + force);
         if (!std::strcmp(force, "bucket")) return 0;
     } else {
-        force = prefer_compact ? "compact" : nullptr;  // (SKQ_CHAIN=2)
+        // (SKQ_CHAIN=2, or the sizing rule of index_create_impl: a compact index whose placement
+        // fails falls back to the other kinds, as an unforced one does)
+        force = prefer_compact ? "compact" : nullptr;
     }
     if (force && !std::strcmp(force, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
     uint64_t need = 0, len[SKQ_MAX_K] = {};
@@ -812,7 +814,7 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
         cmp_need += (uint64_t)std::ceil((double)dkeys[t].size() / 0.95) * 32 + 64 + (dkeys[t].size() + 4) / 5 * 2;
     if (ids_ok && (forced("compact") || (!force && cmp_need <= budget && cmp_need <= fr / 2))) {
         const int rc = build_compact(ix, ntables, tables, dkeys, dvals, lists);
-        if (rc == 0 || forced("compact")) return rc;
+        if (rc == 0 || (forced("compact") && !prefer_compact)) return rc;  // (SKQ_PROBE=compact: its error)
         for (auto& d : ix->d_wdir_t) dev_free(d);  // (placement or allocation failed: another kind)
         for (auto& d : ix->d_wpil_t) dev_free(d);
         for (auto& w : ix->wdir) w = nullptr;
