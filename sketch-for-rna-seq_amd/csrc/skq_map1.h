@@ -313,12 +313,6 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     u32x4 ce[CHN ? (SKQ_CHN_COALESCED ? 8 : 7) : 1];
     uint32_t nraw = 0;  // retained windows (position order) in the raw rows
-    // (TAB 4) the query's bucket pilot, requested inside the hashing loop once the read's first
-    // retained window is known (after about half its blocks), so that the pilot's latency overlaps
-    // the rest of the loop instead of standing between the loop and the entry's request; a read
-    // with no retained window by then has no query (its hashes take the entry list)
-    uint32_t pil_e = 0;
-    bool has_e = false;
     if (hashing) {
         const uint32_t T = p.threshold;
         const uint32_t L = (uint32_t)len;
@@ -431,18 +425,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         };
         uint32_t w0 = 1, bi = 0;
         if (T < 0x80000000u) {  // (uniform)
-            const uint32_t eb = CCH ? max(1u, (nw - 1) / 32) : 0u;  // (blocks before the query's pilot)
-            for (; w0 + 16 <= nw && !(cp.ablate & 32u); w0 += 16, ++bi) {
-                block(bi, 16u, std::true_type{}, std::true_type{});
-                if constexpr (CCH) {
-                    if (bi + 1 == eb) {
-                        has_e = d != d0;
-                        const uint32_t qe = s_raw[(HCAP + 1) * MW + tid];
-                        const uint32_t qhe = cmp_key_hash(qe, cp.wseed[ks]);
-                        pil_e = cp.wpil[ks][cmp_scale(qhe, cp.wnb[ks])];
-                    }
-                }
-            }
+            for (; w0 + 16 <= nw && !(cp.ablate & 32u); w0 += 16, ++bi) block(bi, 16u, std::true_type{}, std::true_type{});
             if (w0 < nw && !(cp.ablate & 32u)) block(bi, nw - w0, std::false_type{}, std::true_type{});
         } else {
             for (; w0 + 16 <= nw; w0 += 16, ++bi) block(bi, 16u, std::true_type{}, std::false_type{});
@@ -513,14 +496,9 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         cq = s_raw[(HCAP + 1) * MW + tid];  // (the first retained window)
         has_q = hashing && nraw && nraw <= HCAP && cq < cp.chain_len[ks];  // (TAB 4 too: past the last key)
         qslot = cq;
-        if constexpr (CCH) {  // the slot from the pilot requested in the hashing loop
-#if SKQ_HASH_PAIR
-            has_q = has_q && has_e;
-            qslot = has_q ? cmp_slot(cmp_key_hash(cq, cp.wseed[ks]), pil_e, cp.wdir_len[ks]) : 0u;
-#else
+        if constexpr (CCH) {  // the bucket's pilot (an L2-resident array), then the slot
             const uint32_t qh = cmp_key_hash(cq, cp.wseed[ks]);
             qslot = has_q ? cmp_slot(qh, cp.wpil[ks][cmp_scale(qh, cp.wnb[ks])], cp.wdir_len[ks]) : 0u;
-#endif
         }
 #if SKQ_CHN_COALESCED
         // eight lanes read one entry, a 16-B piece each, eight entries per load: a load touches 8
@@ -543,8 +521,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
 #pragma unroll
         for (int u = 0; u < 7; ++u) ce[u] = ent[u];
 #endif
-        // (a query past the table: no such key; TAB 4: a read with no query from the loop has none)
-        has_q = hashing && nraw && nraw <= HCAP && (!(CCH && SKQ_HASH_PAIR) || has_e);
+        has_q = hashing && nraw && nraw <= HCAP;  // (a query past the table: no such key)
     }
     if (hashing) {
         if (nraw > HCAP) {
