@@ -83,7 +83,7 @@ struct Map1Static {
 };
 // the per-read overflow flags' place in the wave's region: after the list — hashes, then owning
 // lanes (u8; compact tables: u32 slot | lane << 26) (tab: 0 wide, 2 compact, 3 chained over
-// wide). (Round 3 measured 6 workgroups per CU against 5 with the list packed
+// wide, 4 chained over compact). (Round 3 measured 6 workgroups per CU against 5 with the list packed
 // tighter: no change, profiles/r3_ingest_sweep.log.)
 inline size_t map1_flag_at(int tab, uint32_t hcap) {
     if (tab == 2 || tab == 4) return (size_t)MAP_P * 8;
@@ -123,7 +123,8 @@ inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap, uint32_t mw =
             cp.stamps[((uint64_t)blockIdx.x * (MW / 64) + wv) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// TAB: 0 = wide tables, 2 = compact tables, 3 = chained tables over wide ones. PASS: one k slot (p.kslot) of a
+// TAB: 0 = wide tables, 2 = compact tables, 3 = chained tables over wide ones, 4 = chained tables at the
+// compact tables' slots (over compact ones). PASS: one k slot (p.kslot) of a
 // multi-k map: the entries of the read's count table at that k that meet that k's need go out to
 // cp.ktab / cp.kcnt with the need (a transcript short of one k slot's need fails the multi-k
 // filter whatever the other k slots hold), with no candidates or binning; a read any pass lists
