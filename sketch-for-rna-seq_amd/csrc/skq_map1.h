@@ -954,27 +954,43 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
             // (need 0), placed in a free slot (src/sparse_chaining.cpp:55-73)
             const bool merge = hashing && !slow && !listed;
             if (merge) {
-                uint32_t ut[TS], uc[TS], mxf = 0;
+                // this pass's table (in LDS, the lane's own column): its need, and which slots meet it
+                uint32_t mxf = 0, thisok = 0;
+                {
+                    uint32_t ev[TS];
 #pragma unroll
-                for (int sl = 0; sl < TS; ++sl) {
-                    const uint32_t ev = colbase[sl * MW + ((lane + sl) & 63u)];
-                    ut[sl] = ev != EMPTY ? ev >> 8 : EMPTY;
-                    uc[sl] = ev != EMPTY ? (ev & 0xFFu) << (8 * ks) : 0u;
-                    mxf = max(mxf, ev != EMPTY ? ev & 0xFFu : 0u);
+                    for (int sl = 0; sl < TS; ++sl) {
+                        ev[sl] = colbase[sl * MW + ((lane + sl) & 63u)];
+                        mxf = max(mxf, ev[sl] != EMPTY ? ev[sl] & 0xFFu : 0u);
+                    }
+                    const uint32_t nf = need_of(mxf);
+#pragma unroll
+                    for (int sl = 0; sl < TS; ++sl)
+                        thisok |= ev[sl] != EMPTY && (ev[sl] & 0xFFu) >= nf ? 1u << sl : 0u;
                 }
                 const uint32_t needf = need_of(mxf);
                 const bool inter = needf > 0;  // only this k slot's transcripts can pass
+                if (!inter) thisok = 0xFFFFu;  // (this k slot does not filter: any slot, also one filled below)
                 bool full = false;
                 // the earlier passes' entry counts and needs, then their entries 8 per k slot at a
                 // time, all of a batch's loads in flight together
                 const uint8_t* kneed = cp.kcnt + (uint64_t)p.nk * cp.n;
-                uint32_t mk[NK_FAST - 1], nd[NK_FAST - 1];
+                uint32_t mk[NK_FAST - 1], nd[NK_FAST - 1], nfilt = 0;
 #pragma unroll
                 for (int i = 0; i < NK_FAST - 1; ++i) {
                     mk[i] = (uint32_t)i < ks ? cp.kcnt[(uint64_t)i * cp.n + r] : 0u;
                     nd[i] = (uint32_t)i < ks ? kneed[(uint64_t)i * cp.n + r] : 0u;
+                    nfilt += nd[i] > 0 ? 1u : 0u;
                 }
-                for (uint32_t j0 = 0; j0 < (uint32_t)TS; j0 += 8) {
+                // each earlier entry (its pass's count, meeting that pass's need) found in this
+                // pass's table by its own probe sequence (home slot, then on) and added into the
+                // entry there: the count field gathers the counts over the k slots (<= 4 x 32), bits
+                // 30-31 count the filtering k slots that hold the transcript (ids < 2^22: free bits).
+                // Where this k slot does not filter (need 0) a transcript it lacks takes the first
+                // free slot on its probe path (src/sparse_chaining.cpp:55-73). The lane's column is
+                // its own: plain loads and stores. (Round 4 compared every entry with all 16 slots in
+                // registers: 8.8 % of cfg5's map time, profiles/r5_merge_ab.log.)
+                for (uint32_t j0 = 0; j0 < ((cp.ablate & 64u) ? 0u : (uint32_t)TS); j0 += 8) {  // (64: pricing)
                     bool more = false;
 #pragma unroll
                     for (int i = 0; i < NK_FAST - 1; ++i) more |= j0 < mk[i];
@@ -994,25 +1010,23 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                     for (int u = 0; u < 8; ++u) {
                         const uint32_t e = eb[i][u];
                         if (e == EMPTY) continue;
-                        const uint32_t x = e >> 8, inc = (e & 0xFFu) << (8 * i);
-                        bool found = false;
-#pragma unroll
-                        for (int sl = 0; sl < TS; ++sl) {
-                            const bool h = ut[sl] == x;
-                            uc[sl] += h ? inc : 0u;
-                            found |= h;
-                        }
-                        if (!found && !inter) {
-                            bool placed = false;
-#pragma unroll
-                            for (int sl = 0; sl < TS; ++sl) {
-                                const bool f = !placed && ut[sl] == EMPTY;
-                                ut[sl] = f ? x : ut[sl];
-                                uc[sl] = f ? inc : uc[sl];
-                                placed |= f;
+                        const uint32_t x = e >> 8, add = (e & 0xFFu) + (nd[i] > 0 ? 1u << 30 : 0u);
+                        uint32_t sl = Counter<1, WG>::slot_of(x);
+                        bool done = false;
+#pragma unroll 1
+                        for (int z = 0; z < TS && !done; ++z) {
+                            uint32_t* a = colbase + sl * MW + ((lane + sl) & 63u);
+                            const uint32_t v = *a;
+                            if (v == EMPTY) {
+                                if (!inter) *a = (x << 8) + add;
+                                done = true;
+                            } else if (((v >> 8) & TID_MASK) == x) {
+                                *a = v + add;
+                                done = true;
                             }
-                            full |= !placed;
+                            sl = (sl + 1) & (TS - 1);
                         }
+                        full |= !done && !inter;
                     }
                 }
                 if (full) {  // more than TS transcripts over the k slots
@@ -1020,25 +1034,18 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                     p.pflag[r] = 1;
                     cp.cand_cnt[r] = 0;
                 } else {
-                    // filter at every k slot (src/sparse_chaining.cpp:76-101), as Counter::finish: the
-                    // earlier k slots' needs as their passes found them, this one's from its table
-                    // (counts <= 32 here, so a need of 255 passes nothing)
-                    uint32_t need4 = min(needf, 255u) << (8 * ks);
+                    // filter at every k slot (src/sparse_chaining.cpp:76-101), as Counter::finish: this
+                    // one's need from its table (thisok), the earlier ones' as their passes applied them
+                    // (their entries met them: a transcript passes where every filtering earlier k
+                    // slot holds it); score = the counts' sum (src/sparse_chaining.cpp:100). (Counts
+                    // <= 32 here, so a need past 255 passes nothing.)
                     const bool nonef = needf > 255u;
 #pragma unroll
-                    for (int i = 0; i < NK_FAST - 1; ++i) need4 |= nd[i] << (8 * i);
-#pragma unroll
                     for (int sl = 0; sl < TS; ++sl) {
-                        bool ok = ut[sl] != EMPTY;
-                        uint32_t score = 0;
-#pragma unroll
-                        for (int i = 0; i < NK_FAST; ++i) {
-                            const uint32_t ci = (uc[sl] >> (8 * i)) & 0xFFu;
-                            ok &= ci >= ((need4 >> (8 * i)) & 0xFFu) && !nonef;
-                            score += ci;
-                        }
+                        const uint32_t v = colbase[sl * MW + ((lane + sl) & 63u)];
+                        const bool ok = v != EMPTY && ((thisok >> sl) & 1u) && (v >> 30) == nfilt && !nonef;
                         // score desc, tid asc (src/sparse_chaining.cpp:108-109, ties normalised)
-                        key[sl] = ok ? ((1023u - score) << 22) | ut[sl] : ~0u;
+                        key[sl] = ok ? ((1023u - (v & 0xFFu)) << 22) | ((v >> 8) & TID_MASK) : ~0u;
                     }
                     bitonic_sort<TS>(key);
                     uint32_t* ct = cp.cand_tid + r;
