@@ -989,7 +989,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                 // Where this k slot does not filter (need 0) a transcript it lacks takes the first
                 // free slot on its probe path (src/sparse_chaining.cpp:55-73). The lane's column is
                 // its own: plain loads and stores. (Round 4 compared every entry with all 16 slots in
-                // registers: 8.8 % of cfg5's map time, profiles/r5_merge_ab.log.)
+                // registers: the same time within 0.3 %, 18 KB more code; profiles/r5_merge_ab.log.)
                 for (uint32_t j0 = 0; j0 < ((cp.ablate & 64u) ? 0u : (uint32_t)TS); j0 += 8) {  // (64: pricing)
                     bool more = false;
 #pragma unroll
