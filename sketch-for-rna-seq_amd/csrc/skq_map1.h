@@ -937,41 +937,15 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                                 reinterpret_cast<uint32_t*>(s_wave), lane, [&](int sl) { return kev[sl] != EMPTY; },
                                 [&](int sl) { return kev[sl]; });
         }
-        // (last pass, packed) where each earlier pass's entries of this read start in its region;
-        // the wave's regions themselves, when they fit the wave's LDS region (cfg5: ~200 words per
-        // k slot of the ~700), copied there with 16-B coalesced loads (a few lines per k slot, where
-        // each lane's own run touched a line per lane and load), the entries then read from LDS
-        uint32_t koff[NK_FAST - 1] = {}, kst[NK_FAST - 1] = {};
-        bool kstaged = false;
-        const uint32_t* s_k = reinterpret_cast<const uint32_t*>(s_wave);
+        // (last pass, packed) where each earlier pass's entries of this read start in its region
+        uint32_t koff[NK_FAST - 1] = {};
         if (FINAL && cp.hpack) {  // (uniform)
-            uint32_t tot[NK_FAST - 1] = {}, base = 0;
 #pragma unroll
             for (int i = 0; i < NK_FAST - 1; ++i)
                 if ((uint32_t)i < ks) {
                     const uint32_t c = live ? cp.kcnt[(uint64_t)i * cp.n + r] : 0u;
-                    const uint32_t incl = wave_incl_scan(c, lane);
-                    koff[i] = incl - c;
-                    tot[i] = __shfl(incl, 63, 64);
-                    kst[i] = base;
-                    base += (tot[i] + 3) & ~3u;
+                    koff[i] = wave_incl_scan(c, lane) - c;
                 }
-            kstaged = base <= p.map_wave_bytes / 4;  // (uniform)
-            if (kstaged) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint4* s_k4 = reinterpret_cast<uint4*>(s_wave);
-#pragma unroll
-                for (int i = 0; i < NK_FAST - 1; ++i)
-                    if ((uint32_t)i < ks) {
-                        const uint4* src = reinterpret_cast<const uint4*>(cp.ktab + (uint64_t)i * TS * cp.n + r0 * TS);
-                        for (uint32_t q = lane; q < (tot[i] + 3) / 4; q += 64) s_k4[kst[i] / 4 + q] = src[q];
-                    }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
         }
         if (FINAL) {
             // the transcripts over the k slots, in registers: slot s holds tid ut[s] (EMPTY: free)
@@ -1027,9 +1001,8 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
 #pragma unroll
                         for (int u = 0; u < 8; ++u)
                             eb[i][u] = j0 + u < mk[i]
-                                           ? (kstaged ? s_k[kst[i] + koff[i] + j0 + u]
-                                              : cp.hpack ? cp.ktab[(uint64_t)i * TS * cp.n + (r - lane) * TS + koff[i] + j0 + u]
-                                                         : cp.ktab[((uint64_t)i * TS + j0 + u) * cp.n + r])
+                                           ? (cp.hpack ? cp.ktab[(uint64_t)i * TS * cp.n + (r - lane) * TS + koff[i] + j0 + u]
+                                                       : cp.ktab[((uint64_t)i * TS + j0 + u) * cp.n + r])
                                            : EMPTY;
 #pragma unroll
                     for (int i = 0; i < NK_FAST - 1; ++i)
