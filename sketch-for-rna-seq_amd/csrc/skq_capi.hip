@@ -1374,11 +1374,20 @@ static bool totals_fork(const skq::ChainParams& p, int accumulate) {
 // else launch_bin writes them (k_bin, or k_bin_packed over the fused map's packed candidates)
 static int binned(const skq::ChainParams& p) { return p.slow_totals && (!p.cpack || p.map_bins) ? 1 : 0; }
 
+// SKQ_GENERAL_SLOW=0 (development A/B): the general paths behind k_slow_wave as two launches
+// (k_sketch_slow over ovf3, then k_chain_slow over ovf4) instead of k_general_slow
+static bool general_slow_dev() {
+    const char* e = std::getenv("SKQ_GENERAL_SLOW");
+    return !(e && std::atoi(e) == 0);
+}
+
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
                       hipStream_t st) {
     const bool fork = totals_fork(p, accumulate);
     hipEvent_t t0{};
-    if (fork) {
+    // the side stream's totals, handed off right after the map (SKQ_FORK_LATE A/B, round 5: after
+    // the slow paths instead was 1 % slower at cfg3, 3 % at cfg2; profiles/r5_tail_ab.log)
+    auto fork_totals = [&]() -> int {
         if (int rc = ensure_side(s)) return rc;
         HIP_TRY(hipEventRecord(s->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
@@ -1389,7 +1398,10 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         record_stop(s, 3, t0, s->side);
         HIP_TRY(hipEventRecord(s->ev_join[s->bin_par], s->side));
         s->join_rec[s->bin_par] = true;
-    }
+        return 0;
+    };
+    if (fork)
+        if (int rc = fork_totals()) return rc;
     if (sp && (p.wide == 1 || p.wide == 3) && p.nk <= (uint32_t)skq::NK_FAST) {
         // the fused map's slow reads: the wave path first, the general paths for what it leaves
         if (int rc = skq::launch_slow_wave(*sp, p, s->ovf3, s->ovf4, st))
@@ -1400,8 +1412,12 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         skq::ChainParams p2 = p;
         p2.ovf2 = s->ovf4;
         p2.ovf_word = skq::C_OVF4;
-        if (skq::launch_sketch_slow(sp2, st, 256)) return fail(-3, "sketch slow-path launch failed");
-        if (skq::launch_chain_slow(p2, st, 256)) return fail(-3, "chain slow-path launch failed");
+        if (general_slow_dev()) {  // one launch for both general paths
+            if (skq::launch_general_slow(sp2, p2, st, 256)) return fail(-3, "general slow-path launch failed");
+        } else {
+            if (skq::launch_sketch_slow(sp2, st, 256)) return fail(-3, "sketch slow-path launch failed");
+            if (skq::launch_chain_slow(p2, st, 256)) return fail(-3, "chain slow-path launch failed");
+        }
     } else {
         if (sp && skq::launch_sketch_slow(*sp, st)) return fail(-3, "sketch slow-path launch failed");
         if (skq::launch_chain_slow(p, st)) return fail(-3, "chain slow-path launch failed");

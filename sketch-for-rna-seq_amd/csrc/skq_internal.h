@@ -277,6 +277,9 @@ int launch_mapk(const SketchParams& p, const ChainParams& cp, uint32_t cap, void
 int launch_probe(const ChainParams& p, void* stream);  // k_probe
 int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
+// k_sketch_slow then k_chain_slow per read in one launch, over the chain list p.ovf2 (the fused
+// map's tail behind k_slow_wave: the reads still flagged ST_SLOW1 are re-sketched first)
+int launch_general_slow(const SketchParams& sp, const ChainParams& p, void* stream, unsigned grid = 256);
 // the wave slow path behind k_map1 and its passes (wide or compact tables, <= 4 k slots; -4 otherwise):
 // the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
 int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);

@@ -588,17 +588,25 @@ __device__ __forceinline__ uint32_t packed_share(const uint32_t* hash_cnt, const
 constexpr uint32_t SLOW_CAP = 4096;
 
 #if SKQ_PART == 0
-__global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
-    __shared__ uint32_t s_buf[SLOW_CAP];
-    __shared__ uint32_t s_scan[WG];
-    __shared__ uint32_t s_cnt, s_bad;
-    __shared__ unsigned long long s_at;
+// the workgroup's LDS for one read of k_sketch_slow (also k_general_slow's)
+struct SketchSlowLds {
+    uint32_t buf[SLOW_CAP];
+    uint32_t scan[WG];
+    uint32_t cnt, bad;
+    unsigned long long at;
+};
+
+// one listed read, by the whole workgroup (uniform r)
+__device__ __forceinline__ void sketch_slow_read(const SketchParams& p, uint64_t r, SketchSlowLds& L) {
+    uint32_t* s_buf = L.buf;
+    uint32_t* s_scan = L.scan;
+    uint32_t& s_cnt = L.cnt;
+    uint32_t& s_bad = L.bad;
+    unsigned long long& s_at = L.at;
     const uint32_t t = threadIdx.x;
-    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
     unsigned long long* bump = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_H);
     const uint64_t* seed = p.rolltab + p.nk * 16;
-    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
-        const uint64_t r = p.ovf1[j];
+    {
         uint64_t start, len;
         read_extent(p.offs, p.fixed_len, r, start, len);
         const uint8_t* s = p.reads + start;
@@ -726,6 +734,12 @@ __global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
         if (t == 0) p.status[r] = st;
         __syncthreads();
     }
+}
+
+__global__ __launch_bounds__(WG) void k_sketch_slow(SketchParams p) {
+    __shared__ SketchSlowLds L;
+    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
+    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) sketch_slow_read(p, p.ovf1[j], L);
 }
 #endif  // SKQ_PART == 0
 
@@ -2022,17 +2036,25 @@ __global__ __launch_bounds__(WG) void k_countw(ChainParams p) {
 // Slow chain path: one workgroup per listed read. (tid << 8 | k slot) words are gathered into
 // LDS (global scratch beyond SLOW_CAP), sorted, and counted per transcript run.
 #if SKQ_PART == 0
-__global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
-    __shared__ uint64_t s_ent[SLOW_CAP];
-    __shared__ uint32_t s_max[SKQ_MAX_K];
-    __shared__ uint32_t s_cnt, s_nc;
-    __shared__ unsigned long long s_at;
+// the workgroup's LDS for one read of k_chain_slow (also k_general_slow's)
+struct ChainSlowLds {
+    uint64_t ent[SLOW_CAP];
+    uint32_t max[SKQ_MAX_K];
+    uint32_t cnt, nc;
+    unsigned long long at;
+};
+
+// one listed read, by the whole workgroup (uniform r)
+__device__ __forceinline__ void chain_slow_read(const ChainParams& p, uint64_t r, ChainSlowLds& L) {
+    uint64_t* s_ent = L.ent;
+    uint32_t* s_max = L.max;
+    uint32_t& s_cnt = L.cnt;
+    uint32_t& s_nc = L.nc;
+    unsigned long long& s_at = L.at;
     const uint32_t t = threadIdx.x;
-    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
     unsigned long long* bump_s = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_S);
     unsigned long long* bump_c = reinterpret_cast<unsigned long long*>(p.ctrl + C_BUMP_C);
-    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
-        const uint64_t r = p.ovf2[j];
+    {
         __syncthreads();
         // pass 1: postings count P
         if (t == 0) s_cnt = 0;
@@ -2072,7 +2094,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
         __syncthreads();
         if (s_at == ~0ull) {
             if (t == 0) p.cand_cnt[r] = 0;
-            continue;
+            return;
         }
         uint64_t* ent = in_lds ? s_ent : p.scratch + s_at;
         // pass 2: gather
@@ -2161,7 +2183,7 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
             __syncthreads();
             if (s_at == ~0ull) {
                 if (t == 0) p.cand_cnt[r] = 0;
-                continue;
+                return;
             }
             ct = p.cand_ext + 2 * (s_at + hd);
             cs = ct + 1;
@@ -2178,6 +2200,29 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
             }
         }
         if (t == 0) p.cand_cnt[r] = p.cpack ? (CAND_EXT | (uint32_t)s_at) : nc;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
+    __shared__ ChainSlowLds L;
+    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
+    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) chain_slow_read(p, p.ovf2[j], L);
+}
+
+// The general slow paths behind k_slow_wave in one launch: each read on its chain list (ovf4),
+// re-sketched first when k_slow_wave left its sketch too (status still ST_SLOW1: the reads on
+// ovf3, a subset of ovf4), then chained, by one workgroup. Per read this is k_sketch_slow's then
+// k_chain_slow's work in their order; a read's chain reads only its own sets, and the packed
+// offsets of its wave's other reads come from shares that a concurrent re-sketch keeps
+// (hash_list<true>). Saves the second launch of the batch's tail.
+__global__ __launch_bounds__(WG) void k_general_slow(SketchParams sp, ChainParams p) {
+    __shared__ SketchSlowLds LS;
+    __shared__ ChainSlowLds LC;
+    const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
+    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
+        const uint64_t r = p.ovf2[j];
+        if (sp.status[r] & ST_SLOW1) sketch_slow_read(sp, r, LS);  // (uniform)
+        chain_slow_read(p, r, LC);
     }
 }
 
@@ -3036,6 +3081,12 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid) {
     if (p.n == 0) return 0;
     hipLaunchKernelGGL(k_chain_slow, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_general_slow(const SketchParams& sp, const ChainParams& p, void* stream, unsigned grid) {
+    if (p.n == 0) return 0;
+    hipLaunchKernelGGL(k_general_slow, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), sp, p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
