@@ -2216,13 +2216,19 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
 // offsets of its wave's other reads come from shares that a concurrent re-sketch keeps
 // (hash_list<true>). Saves the second launch of the batch's tail.
 __global__ __launch_bounds__(WG) void k_general_slow(SketchParams sp, ChainParams p) {
-    __shared__ SketchSlowLds LS;
-    __shared__ ChainSlowLds LC;
+    // one LDS region for both steps (each ends / starts at a barrier): a workgroup needs no more
+    // than k_chain_slow's, so the launch's workgroups still fit beside the side stream's (with
+    // both regions apart, 50 KB each, it waited for k_bin_packed's workgroups: 71 µs at cfg3)
+    __shared__ union {
+        SketchSlowLds s;
+        ChainSlowLds c;
+    } L;
     const uint32_t cnt = min(p.ctrl[p.ovf_word], p.ovf_cap);
     for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
         const uint64_t r = p.ovf2[j];
-        if (sp.status[r] & ST_SLOW1) sketch_slow_read(sp, r, LS);  // (uniform)
-        chain_slow_read(p, r, LC);
+        if (sp.status[r] & ST_SLOW1) sketch_slow_read(sp, r, L.s);  // (uniform)
+        chain_slow_read(p, r, L.c);
+        __syncthreads();  // (the chain's last LDS reads before the next read's sketch writes)
     }
 }
 
