@@ -52,6 +52,17 @@ $(ABDIR)/libskq.so: $(AB_KOBJS) $(filter-out $(OUT)/obj/skq_kernels.o $(OUT)/obj
 ab: $(ABDIR)/libskq.so
 .PHONY: ab
 
+# the debug build of the map's LDS slot counter (skq_map1.h lds_slot_next: clamped instead of
+# wrapped below LDS address 0), loaded by tests/test_debug_lds_gpu.py through SKQ_LIB
+DBG := $(OUT)/ab/debug_lds
+$(DBG)/%.o: $(CSRC)/%.hip $(CSRC)/skq_kernels.hip $(CSRC)/skq_map1.h $(CSRC)/skq_internal.h include/skq.h
+	@mkdir -p $(DBG)
+	$(HIPCC) $(HIPFLAGS) -DSKQ_DEBUG_LDS=1 -c $< -o $@
+$(DBG)/libskq.so: $(DBG)/skq_map1.o $(DBG)/skq_map1_pass.o $(filter-out $(OUT)/obj/skq_map1.o $(OUT)/obj/skq_map1_pass.o,$(LIB_OBJS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $^
+debuglds: $(DBG)/libskq.so
+.PHONY: debuglds
+
 # the command line (index / quant), src/main.cpp's interface
 # (several GPUs: HIP streams and RCCL from the host program; the HIP headers want the platform named)
 $(OUT)/skq: $(CSRC)/skq_cli.cpp $(OUT)/libskq.so include/skq.h include/skq_host.h
@@ -62,6 +73,6 @@ $(OUT)/skq: $(CSRC)/skq_cli.cpp $(OUT)/libskq.so include/skq.h include/skq_host.
 $(OUT)/skq_dropin_check: tests/dropin_check.cpp $(OUT)/libskq.so $(wildcard include/dropin/*.h)
 	$(HOST_CXX) -O2 -std=c++17 -Wall -Iinclude/dropin $< -o $@ -L$(OUT) -lskq -Wl,-rpath,'$$ORIGIN'
 
-all: lib oracle ref $(OUT)/skq $(OUT)/skq_dropin_check
+all: lib oracle ref debuglds $(OUT)/skq $(OUT)/skq_dropin_check
 .PHONY: lib all
 .DEFAULT_GOAL := all

@@ -502,30 +502,40 @@ def measure(cname, cfg, args, rank, world, dev, gpu, sample, totals_dev=True):
         va = per_launch / (avg[kname] * 1e-3)
         valu = {"instructions_per_read": vk["valu_per_read"], "per_wave": vk["valu_per_read"] * 64,
                 "per_launch": per_launch, "achieved": va, "peak": VALU_PEAK, "unit": "wave64 VALU instructions/s",
-                "frac": va / VALU_PEAK, "salu_per_read": vk.get("salu_per_read"),
+                "issue_frac": va / VALU_PEAK, "salu_per_read": vk.get("salu_per_read"),
+                "issue_note": ("an issue-COUNT fraction: instructions over the full-rate issue peak (2 cycles per "
+                               "wave64 instruction); three-operand forms issue at about half that rate "
+                               "(profiles/r4_valu_rate.log), and the counters give no VALU-busy cycles on this "
+                               "stack (SQ_ACTIVE_INST_VALU equals the instruction count; DESIGN.md section 5)"),
                 "source": "%s (%s)" % (vf, vj.get("measured", "builder's PMC passes")),
                 "peak_source": "MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction issues over 2 "
                                "cycles, 2.4 GHz -> 1.229e12 wave-instructions/s"}
     hbm_frac = achieved / HBM_PEAK_GBS
-    bound = "valu" if valu is not None and valu["frac"] > hbm_frac else "hbm"
     requests = None
-    if map1:  # random index requests per launch against the measured gather ceiling
-        rps = n * h / (avg[kname] * 1e-3) / 1e9
-        requests = {"random_per_read": h, "achieved": rps, "ceiling": GATHER_CEIL_GPS, "unit": "G/s",
-                    "frac": rps / GATHER_CEIL_GPS,
-                    "ceiling_source": "tools/micro/gather_bench: random pair-cooperative 32-B gathers, 8 GiB table"}
-        if chained:
-            requests["note"] = ("chained tables: random_per_read counts the hashes looked up; one 128-B chained "
-                                "entry per read (read by eight lanes together) settles most of them and the rest "
-                                "gather 32-B wide entries, so the memory-side requests are all_per_read; the bound "
-                                "is the VALU and the CUs' per-line address work, not this rate (DESIGN.md section 5)")
-        if traffic is not None:  # every memory-side request of the launch, from the calibrated PMC passes
-            kt_ = tr["kernels"][kname]
-            per = kt_["fetch_size_bytes_per_read"] / 64.0 + kt_["write_bytes_per_read"] / 64.0
-            requests.update(all_per_read=per, all_achieved=n * per / (avg[kname] * 1e-3) / 1e9,
-                            all_note="read + write requests per read from %s (FETCH_SIZE and WRITE_SIZE tally 64 B "
-                                     "per request); random-gather rates measured: 46-49 G/s from HBM, 54-56 G/s "
-                                     "from the Infinity Cache (DESIGN.md §5)" % tf)
+    if map1 and traffic is not None:  # every memory-side request of the launch, from the calibrated PMC passes
+        kt_ = tr["kernels"][kname]
+        per = kt_["fetch_size_bytes_per_read"] / 64.0 + kt_["write_bytes_per_read"] / 64.0
+        ra = n * per / (avg[kname] * 1e-3) / 1e9
+        requests = {"per_read": per, "achieved": ra, "ceiling": GATHER_CEIL_GPS, "unit": "G requests/s",
+                    "frac": ra / GATHER_CEIL_GPS, "hashes_per_read": h,
+                    "note": "memory-side read + write requests per read from %s (FETCH_SIZE and WRITE_SIZE "
+                            "tally 64 B per request) over the launch time, against the measured random-gather "
+                            "ceiling (tools/micro/gather_bench: 46-49 G/s from HBM, 54-56 G/s from the Infinity "
+                            "Cache; DESIGN.md section 5)" % tf}
+    # the bound: the resource nearest its ceiling, or "latency" when none is above 0.7 (then the
+    # kernel waits on dependencies and instruction issue of ~4.5 resident waves per SIMD: the counter
+    # file named in bound_evidence)
+    fr = {"hbm": hbm_frac}
+    if valu is not None:
+        fr["valu_issue"] = valu["issue_frac"]
+    if requests is not None:
+        fr["requests"] = requests["frac"]
+    top = max(fr, key=fr.get)
+    bound = top if fr[top] >= 0.7 else "latency"
+    bj, bf = load_profile_json("r6_pmc_bound_%s.json" % tname)
+    bound_ev = None
+    if bj is not None and bj.get("kernel") == kname:
+        bound_ev = dict(bj.get("derived", {}), source=bf, measured=bj.get("measured"))
     value = n * world * args.steps / elapsed
     line = {
         "value": value, "ms_per_step": elapsed / args.steps * 1e3,
@@ -533,8 +543,10 @@ def measure(cname, cfg, args, rank, world, dev, gpu, sample, totals_dev=True):
         "roofline": {"bound": bound, "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": hbm_frac, "traffic": traffic,
                      "bound_note": ("achieved / peak / frac are the HBM roofline on SURVEY.md 8(d)'s algorithmic "
-                                    "bytes; valu is the same launch against the VALU issue peak; bound names the "
-                                    "larger fraction"),
+                                    "bytes; valu (issue count) and requests (memory-side requests) are the same "
+                                    "launch against their ceilings; bound names the largest fraction, or latency "
+                                    "when none reaches 0.7"),
+                     "fractions": fr, "bound_evidence": bound_ev,
                      "algorithmic_bytes": n * b_basis, "avg_launch_ms": avg[kname],
                      "bytes_basis": ("SURVEY.md 8(d): L + 8h + 4P + 4h + 8C per read" if b_basis == b_path
                                      else "kernel input/output bytes"),

@@ -687,3 +687,88 @@ int orc_fastq_map(const orc_index* ix, const char* fq, uint64_t len, uint32_t th
     free(rec);
     return rc;
 }
+
+/* ---- per-read digests (tests: per-read parity at full batch sizes) ------------------------ */
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+static uint64_t dg_item(uint64_t tag, uint64_t j, uint64_t v) { return mix64((tag << 56) ^ (j << 32) ^ v); }
+
+typedef struct {
+    const orc_index* ix;
+    const uint8_t* bases;
+    uint32_t L, threshold;
+    double fraction;
+    uint64_t r0, r1;
+    uint64_t* digest;
+    uint64_t* tx_acc; /* (reads << 40 | score) per transcript, this thread's reads */
+    int rc;
+} dg_job;
+
+static void* dg_worker(void* arg) {
+    dg_job* j = (dg_job*)arg;
+    const orc_index* ix = j->ix;
+    uint32_t* scratch = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)j->L + 1) * ix->nk + 4);
+    uint32_t* hs = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)j->L + 1) * ix->nk + 4);
+    uint32_t* ct = (uint32_t*)malloc(sizeof(uint32_t) * (ix->ntx + 1));
+    uint32_t* cs = (uint32_t*)malloc(sizeof(uint32_t) * (ix->ntx + 1));
+    uint32_t hc[64];
+    for (uint64_t r = j->r0; r < j->r1 && j->rc == 0; ++r) {
+        uint8_t st;
+        uint32_t nc;
+        j->rc = map_one(ix, j->bases + r * j->L, j->L, j->threshold, j->fraction, &st, hc, hs, j->L + 1, &nc, ct, cs,
+                        ix->ntx + 1, scratch);
+        uint64_t d = dg_item(0xA5, 0, st);
+        for (unsigned i = 0; i < ix->nk; ++i)
+            for (uint32_t q = 0; q < hc[i]; ++q) d += dg_item(i + 1, q, hs[(size_t)i * (j->L + 1) + q]);
+        for (uint32_t q = 0; q < nc; ++q) {
+            d += dg_item(0xC0, q, ct[q]) + dg_item(0xD0, q, cs[q]);
+            if (j->tx_acc) j->tx_acc[ct[q]] += (1ull << 40) | cs[q];
+        }
+        j->digest[r] = d;
+    }
+    free(scratch);
+    free(hs);
+    free(ct);
+    free(cs);
+    return NULL;
+}
+
+int orc_map_digest(const orc_index* ix, const uint8_t* bases, uint32_t L, uint64_t n, uint32_t threshold,
+                   double fraction, int nthreads, uint64_t* digest, uint64_t* tx_reads, uint64_t* tx_score) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    dg_job jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; ++t) {
+        dg_job* j = &jobs[t];
+        memset(j, 0, sizeof(*j));
+        j->ix = ix; j->bases = bases; j->L = L; j->threshold = threshold; j->fraction = fraction;
+        j->r0 = n * t / nthreads; j->r1 = n * (t + 1) / nthreads;
+        j->digest = digest;
+        j->tx_acc = tx_reads ? (uint64_t*)calloc(ix->ntx + 1, sizeof(uint64_t)) : NULL;
+        pthread_create(&th[t], NULL, dg_worker, j);
+    }
+    int rc = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = -1;
+    }
+    if (tx_reads) {
+        memset(tx_reads, 0, sizeof(uint64_t) * ix->ntx);
+        memset(tx_score, 0, sizeof(uint64_t) * ix->ntx);
+        for (int t = 0; t < nthreads; ++t) {
+            for (uint32_t x = 0; x < ix->ntx; ++x) {
+                tx_reads[x] += jobs[t].tx_acc[x] >> 40;
+                tx_score[x] += jobs[t].tx_acc[x] & ((1ull << 40) - 1);
+            }
+            free(jobs[t].tx_acc);
+        }
+    }
+    return rc;
+}

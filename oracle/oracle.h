@@ -119,6 +119,19 @@ int orc_fastq_map(const orc_index* idx, const char* fq, uint64_t len, uint32_t t
                   uint32_t* hashes, uint32_t hcap, uint32_t* cand_cnt, uint32_t* cand_tid, uint32_t* cand_score,
                   uint32_t ccap, uint8_t* kept, uint64_t* tx_reads, uint64_t* tx_score);
 
+/* Per-read digests of a batch of fixed-length reads (bases[r*L .. (r+1)*L)), for per-read parity
+ * at full batch sizes where keeping every record's outputs would not fit: for read r,
+ *   digest[r] = item(0xA5, 0, status) + SUM_{k slot i, j < hash_cnt} item(i + 1, j, hash_j)
+ *             + SUM_{j < cand_cnt} (item(0xC0, j, tid_j) + item(0xD0, j, score_j))   (mod 2^64),
+ *   item(tag, j, v) = splitmix64-finaliser((tag << 56) ^ (j << 32) ^ v),
+ * hashes ascending per k slot, candidates by score desc then tid asc (orc_map_batch's outputs).
+ * So two results agree iff (with overwhelming probability) every read's status, retained-hash sets
+ * and candidate list agree, read by read. tx_reads / tx_score (optional): the per-transcript totals.
+ * nthreads over contiguous read ranges. Returns 0, -1 on a failure. (tests/digest.py restates the
+ * digest over an skq export.) */
+int orc_map_digest(const orc_index* idx, const uint8_t* bases, uint32_t L, uint64_t n, uint32_t threshold,
+                   double fraction, int nthreads, uint64_t* digest, uint64_t* tx_reads, uint64_t* tx_score);
+
 /* EM over the reads' candidate lists (src/isoform_assignment.cpp:9-65): pi starts uniform over
  * the ntx transcripts; E-step per read in order, posterior = pi*score * (1/denominator) when the
  * denominator exceeds 1e-10; M-step pi = (posterior_sum + 0.01f/R) + 0.01f (float pseudocount,

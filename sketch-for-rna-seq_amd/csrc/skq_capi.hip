@@ -103,70 +103,76 @@ struct TimedLaunch {
     hipEvent_t start, stop;
 };
 
-struct skq_session {
-    skq_index* idx = nullptr;
-    uint64_t max_reads = 0;
-    uint32_t max_len = 0;
-    uint32_t hcap = 0;         // stride of the current results
-    uint32_t hcap_alloc = 0;   // stride the hashes buffer was sized for
-    uint64_t n_reads = 0;      // reads in the current results
-    bool have_sketch = false;
-    bool probed = false;       // the last skq_sketch also filled lofs/pflag (fused probe)
-    bool have_chain = false;   // candidates belong to the current batch
-    bool hash_packed = false;  // hashes in the per-wave packed layout (single-k fused map)
-    bool cand_packed = false;  // candidates likewise
+// A frame: every per-batch array a map and its tail (the slow paths, the totals binning) read or
+// write. A fused map whose tail runs on the session's side stream takes the other frame from the
+// previous batch's (skq_session::f and alt swap), so the next batch's map on the launch stream
+// writes one frame while the previous batch's tail on the side stream still reads and writes the
+// other: the launch stream then runs the maps back to back (the batch tail).
+struct Frame {
     uint8_t* status = nullptr;
     uint32_t* hash_cnt = nullptr;
     uint32_t* hashes = nullptr;
     uint32_t* lofs = nullptr;    // list offsets per probe (k_probe -> k_count), shaped like hashes
     uint8_t* pflag = nullptr;
     uint32_t* hash_ext = nullptr;
-    uint64_t hash_ext_cap = 0;
     uint32_t* ovf1 = nullptr;
     uint32_t* ovf2 = nullptr;
     uint32_t* ovf3 = nullptr;  // second-level lists behind k_slow_wave
     uint32_t* ovf4 = nullptr;
-    uint32_t ovf_cap = 0;
     uint32_t* cand_cnt = nullptr;
     uint32_t* cand_tid = nullptr;
     uint32_t* cand_score = nullptr;
-    // the fused map's packed candidates, by batch parity when the totals run on the side stream
-    // (k_bin_packed there reads one batch's pair while the next batch's map writes the other):
-    // [0] the arrays above, [1] allocated on first use; cand_cnt / cand_tid point at the current pair
-    uint32_t* cand_cnt_b[2] = {};
-    uint32_t* cand_tid_b[2] = {};
-    uint32_t* cand_wtot_b[2] = {};  // per wave of 64 reads: its packed candidate words (k_bin_packed)
+    uint32_t* cand_wtot = nullptr;  // per wave of 64 reads: its packed candidate words (k_bin_packed)
     uint32_t* cand_ext = nullptr;
-    uint64_t cand_ext_cap = 0;
     uint64_t* scratch = nullptr;
-    uint64_t scratch_cap = 0;
-    // per-transcript totals by buckets of 2^bin_bits ids (k_bin / k_bin_sum); bin_nb = 0: direct
-    uint32_t bin_bits = 13, bin_nb = 0;
-    // double-buffered by batch parity: a batch's k_bin_sum (side stream) reads its bins while
-    // the next batch's map kernel writes the other set
-    uint32_t* bin_hdr[2] = {};
-    uint32_t* bin_region[2] = {};
-    uint32_t bin_par = 0;
-    uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
-    uint64_t* tx_slab = nullptr;  // k_bin_sum's per-workgroup bins (ChainParams::tx_slab), 512 << bin_bits
+    uint32_t* ctrl = nullptr;
     uint32_t* ktab = nullptr;    // multi-k map by passes: per-k count tables (allocated on first use)
     uint8_t* kcnt = nullptr;
     uint32_t* stash = nullptr;   // multi-k map by passes: the first pass's staged bases (SketchParams::stash)
     uint64_t stash_words = 0;
+    uint32_t hcap_alloc = 0;     // stride the hashes buffer was sized for
+};
+
+struct skq_session {
+    skq_index* idx = nullptr;
+    uint64_t max_reads = 0;
+    uint32_t max_len = 0;
+    uint32_t hcap = 0;         // stride of the current results
+    uint64_t n_reads = 0;      // reads in the current results
+    bool have_sketch = false;
+    bool probed = false;       // the last skq_sketch also filled lofs/pflag (fused probe)
+    bool have_chain = false;   // candidates belong to the current batch
+    bool hash_packed = false;  // hashes in the per-wave packed layout (single-k fused map)
+    bool cand_packed = false;  // candidates likewise
+    Frame f;                   // the current batch's frame (its results)
+    Frame alt;                 // the other frame (allocated with the first batch whose tail runs on the side stream)
+    int fid = 0;               // which of the two frames f is (events below are per frame)
+    uint64_t hash_ext_cap = 0;
+    uint32_t ovf_cap = 0;
+    uint64_t cand_ext_cap = 0;
+    uint64_t scratch_cap = 0;
+    // per-transcript totals by buckets of 2^bin_bits ids (k_bin / k_bin_sum); bin_nb = 0: direct.
+    // One set: every kernel that bins runs after the previous batch's k_bin_sum (the side stream
+    // runs the tails in order; the launch stream waits for it before binning itself)
+    uint32_t bin_bits = 13, bin_nb = 0;
+    uint32_t* bin_hdr = nullptr;
+    uint32_t* bin_region = nullptr;
+    uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
-    uint32_t* ctrl = nullptr;
     // explicit-sketch chaining (skq_chain_sketches) keeps its inputs' layout for export
     const uint32_t* x_hashes = nullptr;
     const uint64_t* x_offs = nullptr;
     bool timing = false;
     std::vector<TimedLaunch> timed;
     uint64_t* stamps = nullptr;  // development: k_map1 phase clocks (skq_session_set_stamps)
-    // side stream for the totals (k_bin_sum runs beside the slow paths), created on first use
+    // the side stream (batch tails), created on first use; per frame x, ev_done[x] follows the last
+    // side-stream work on frame x (its tail, then the reset of its control words once the next
+    // batch has taken the other frame: zeroed[x])
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork{}, ev_join[2]{};  // ev_join[b]: k_bin_sum of the last batch of parity b
-    bool join_rec[2] = {false, false};
-
+    hipEvent_t ev_fork{}, ev_done[2]{};
+    bool done_rec[2] = {false, false};
+    bool zeroed[2] = {false, false};
 };
 
 int skq::session_device(const skq_session* s) { return s->idx->device; }
@@ -182,22 +188,11 @@ int dev_alloc(T** p, uint64_t count) {
     return 0;
 }
 
-// the gather tables (wide and chained entries, GBs read at random): physically contiguous when
-// SKQ_CONTIG=1 (development A/B: contiguous memory lets the page tables use their largest
-// fragments, so a translation covers more of the table), else hipMalloc
+// the gather tables (wide and chained entries, GBs read at random): plain hipMalloc (physically
+// contiguous memory, hipDeviceMallocContiguous, measured the same in round 4: DESIGN.md §5)
 template <typename T>
 int dev_alloc_table(T** p, uint64_t count) {
-    static const bool contig = [] {
-        const char* e = std::getenv("SKQ_CONTIG");
-        return e && std::atoi(e) == 1;
-    }();
-    *p = nullptr;
-    if (count == 0) count = 1;
-    if (contig && hipExtMallocWithFlags(reinterpret_cast<void**>(p), count * sizeof(T), hipDeviceMallocContiguous) == hipSuccess)
-        return 0;
-    (void)hipGetLastError();
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
-    return 0;
+    return dev_alloc(p, count);
 }
 
 template <typename T>
@@ -224,18 +219,30 @@ uint32_t pick_hcap(uint32_t max_len, uint32_t mink, uint32_t threshold, double s
     return 64;
 }
 
-// the multi-k passes' raw capacity: the mean retained windows of the pass's k plus this many
-// standard deviations (reads beyond it take k_slow_wave); SKQ_PASS_SIGMAS overrides (A/B)
-// the multi-k passes stage from the first pass's image of the bases; SKQ_STASH=0 re-reads the
-// bases in every pass (A/B; read per batch, so the parity tests run both)
+// Development switches (A/B builds of the shipped library's choices, and the parity tests that pin
+// both sides of them) are read only beside SKQ_DEV=1; without it the library reads SKQ_PROBE,
+// SKQ_CHAIN, SKQ_CHAIN_MB, SKQ_DIRECT_MB (the index's kinds and budgets), SKQ_DEVICE (the drop-in's
+// device) and SKQ_INGEST_TRACE, and nothing else.
+static const char* dev_env(const char* name) {
+    static const bool dev = [] {
+        const char* e = std::getenv("SKQ_DEV");
+        return e && std::atoi(e) == 1;
+    }();
+    return dev ? std::getenv(name) : nullptr;
+}
+
+// the multi-k passes stage from the first pass's image of the bases; SKQ_STASH=0 (development)
+// re-reads the bases in every pass (read per batch, so the parity tests run both)
 static bool use_stash() {
-    const char* e = std::getenv("SKQ_STASH");
+    const char* e = dev_env("SKQ_STASH");
     return !e || std::atoi(e) != 0;
 }
 
+// the multi-k passes' raw capacity: the mean retained windows of the pass's k plus this many
+// standard deviations (reads beyond it take k_slow_wave); SKQ_PASS_SIGMAS (development) overrides
 double pass_sigmas() {
     static const double v = [] {
-        const char* e = std::getenv("SKQ_PASS_SIGMAS");
+        const char* e = dev_env("SKQ_PASS_SIGMAS");
         return e ? std::atof(e) : 3.0;
     }();
     return v;
@@ -256,13 +263,13 @@ void record_stop(skq_session* s, int kind, hipEvent_t start, hipStream_t st) {
 }
 
 int ensure_hashes(skq_session* s, uint32_t hcap) {
-    if (s->hcap_alloc >= hcap) return 0;
+    if (s->f.hcap_alloc >= hcap) return 0;
     (void)hipDeviceSynchronize();
-    dev_free(s->hashes);
-    dev_free(s->lofs);
-    if (dev_alloc(&s->hashes, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
-    if (dev_alloc(&s->lofs, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
-    s->hcap_alloc = hcap;
+    dev_free(s->f.hashes);
+    dev_free(s->f.lofs);
+    if (dev_alloc(&s->f.hashes, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
+    if (dev_alloc(&s->f.lofs, s->max_reads * s->idx->nk * (uint64_t)hcap)) return -3;
+    s->f.hcap_alloc = hcap;
     return 0;
 }
 
@@ -541,14 +548,18 @@ struct ChainHost {
     double seconds = 0;  // host build time
     uint64_t triples = 0;  // (key, successor, hop) candidates sorted (host peak: 12 B each + ent)
 };
+// (keyed on what the callers have in common: the caller's table arrays and transcript sequences,
+// not the per-call host image derived from them, whose address differs in every call)
 struct ChainKey {
     const void* seqs;
     const void* offs;
-    const void* lists;
+    const void* tkeys;
+    const void* toffs;
+    const void* ttids;
     uint64_t nseq, k, thr, m, last, nlists;
     bool operator==(const ChainKey& o) const {
-        return seqs == o.seqs && offs == o.offs && lists == o.lists && nseq == o.nseq && k == o.k && thr == o.thr &&
-               m == o.m && last == o.last && nlists == o.nlists;
+        return seqs == o.seqs && offs == o.offs && tkeys == o.tkeys && toffs == o.toffs && ttids == o.ttids &&
+               nseq == o.nseq && k == o.k && thr == o.thr && m == o.m && last == o.last && nlists == o.nlists;
     }
 };
 struct ChainShare {
@@ -670,9 +681,10 @@ static void chain_note(uint32_t k, const char* why, uint64_t need, uint64_t fr) 
 
 // slots: the keys' compact slots (chained entries over compact tables, nslots of them), or null
 // (one entry per possible key up to the largest)
-int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
-                const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs, const uint64_t* offs,
-                uint32_t nseq, uint32_t threshold, const std::vector<uint32_t>* slots, uint64_t nslots) {
+int build_chain(skq_index* ix, uint32_t slot, const skq_kmer_table& src, const std::vector<uint32_t>& keys,
+                const std::vector<uint32_t>& vals, const std::vector<uint32_t>& lists, uint32_t k, const uint8_t* seqs,
+                const uint64_t* offs, uint32_t nseq, uint32_t threshold, const std::vector<uint32_t>* slots,
+                uint64_t nslots) {
     const uint64_t m = keys.size();
     if (m == 0 || keys.back() >= skq::CHN_KEY_LIMIT) return 0;  // (records hold key ^ CHN_KEY_LIMIT)
     if (slots && slots->size() != m) return fail(-3, "chained table: compact slots missing");
@@ -689,7 +701,7 @@ int build_chain(skq_index* ix, uint32_t slot, const std::vector<uint32_t>& keys,
         return 0;
     }
     // the host entries: shared with the other devices building the same tables at the same time
-    const ChainKey key{seqs, offs, &lists, nseq, k, threshold, m, len, lists.size()};
+    const ChainKey key{seqs, offs, src.keys, src.offs, src.tids, nseq, k, threshold, m, len, lists.size()};
     std::shared_future<std::shared_ptr<const ChainHost>> fut;
     std::promise<std::shared_ptr<const ChainHost>> prom;
     bool builder = false;
@@ -854,6 +866,31 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
 }
 
 }  // namespace
+
+// The side stream runs batch tails (a fused map's slow paths and totals; a large two-kernel batch's
+// totals) in batch order. wait_side: a launch-stream point after every side-stream piece of work so
+// far (every reader of the running totals, and every batch that does not take the other frame).
+static int wait_side(skq_session* s, hipStream_t st) {
+    for (int b = 0; b < 2; ++b)
+        if (s->side && s->done_rec[b]) HIP_TRY(hipStreamWaitEvent(st, s->ev_done[b], 0));
+    return 0;
+}
+
+// the host waits for the side stream's work on the current frame (its results) and the totals
+static int sync_side(skq_session* s) {
+    for (int b = 0; b < 2; ++b)
+        if (s->side && s->done_rec[b]) HIP_TRY(hipEventSynchronize(s->ev_done[b]));
+    return 0;
+}
+
+static int ensure_side(skq_session* s) {
+    if (s->side) return 0;
+    HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_done[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_done[1], hipEventDisableTiming));
+    return 0;
+}
 
 extern "C" {
 
@@ -1047,7 +1084,7 @@ static int index_create_impl(int device, uint32_t ntx, uint32_t nk, const uint32
             for (uint32_t t = 0; t < ntables; ++t)
                 if (tables[t].k == ks[i]) {
                     const bool cmp = ix->mode == 5;
-                    if (int rc2 = build_chain(ix, i, dkeys[t], dvals[t], lists, ks[i], seqs, seq_offs, nseq, threshold,
+                    if (int rc2 = build_chain(ix, i, tables[t], dkeys[t], dvals[t], lists, ks[i], seqs, seq_offs, nseq, threshold,
                                               cmp ? &ix->cmp_slots_t[t] : nullptr, cmp ? ix->dir_len[i] : 0)) {
                         skq_index_free(ix);
                         return rc2;
@@ -1097,8 +1134,9 @@ int skq_index_stats(const skq_index* ix, uint64_t* device_bytes, uint64_t* npost
 int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chain_slow) {
     if (!s) return fail(-1, "null session");
     DeviceGuard g(s->idx->device);
+    if (int rc = sync_side(s)) return rc;
     uint32_t c[skq::C_WORDS];
-    HIP_TRY(hipMemcpy(c, s->ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c, s->f.ctrl, sizeof(c), hipMemcpyDeviceToHost));
     if (sketch_slow) *sketch_slow = c[skq::C_OVF1];
     if (chain_slow) *chain_slow = c[skq::C_OVF2];
     return 0;
@@ -1107,8 +1145,9 @@ int skq_session_slow_reads(skq_session* s, uint32_t* sketch_slow, uint32_t* chai
 int skq_session_slow_counts(skq_session* s, uint32_t* counts) {
     if (!s || !counts) return fail(-1, "null argument");
     DeviceGuard g(s->idx->device);
+    if (int rc = sync_side(s)) return rc;
     uint32_t c[skq::C_WORDS];
-    HIP_TRY(hipMemcpy(c, s->ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c, s->f.ctrl, sizeof(c), hipMemcpyDeviceToHost));
     counts[0] = c[skq::C_OVF1];
     counts[1] = c[skq::C_OVF2];
     counts[2] = c[skq::C_OVF3];
@@ -1124,6 +1163,49 @@ int skq_index_chain_build(const skq_index* ix, double* host_seconds, uint64_t* h
     if (host_seconds) *host_seconds = ix->chain_build_s;
     if (host_peak_bytes) *host_peak_bytes = ix->chain_host_bytes;
     return 0;
+}
+
+// one frame's buffers for the session's sizes (the hashes and lofs: ensure_hashes)
+static int frame_alloc(skq_session* s, Frame& fr, uint32_t hcap) {
+    const uint64_t R = s->max_reads;
+    const uint32_t nk = s->idx->nk;
+    int rc = 0;
+    if ((rc = dev_alloc(&fr.status, R)) || (rc = dev_alloc(&fr.hash_cnt, R * nk)) ||
+        (rc = dev_alloc(&fr.hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&fr.ovf1, s->ovf_cap)) ||
+        (rc = dev_alloc(&fr.ovf2, s->ovf_cap)) || (rc = dev_alloc(&fr.ovf3, s->ovf_cap)) ||
+        (rc = dev_alloc(&fr.ovf4, s->ovf_cap)) || (rc = dev_alloc(&fr.cand_cnt, R)) || (rc = dev_alloc(&fr.pflag, R)) ||
+        (rc = dev_alloc(&fr.cand_tid, R * skq::CCAP)) || (rc = dev_alloc(&fr.cand_wtot, (R + 63) / 64)) ||
+        (rc = dev_alloc(&fr.cand_score, R * skq::CCAP)) || (rc = dev_alloc(&fr.cand_ext, 2 * s->cand_ext_cap)) ||
+        (rc = dev_alloc(&fr.scratch, s->scratch_cap)) || (rc = dev_alloc(&fr.ctrl, skq::C_WORDS)))
+        return rc;
+    if (hipMemset(fr.ctrl, 0, skq::C_WORDS * 4) != hipSuccess) return fail(-3, "memset failed");
+    if (dev_alloc(&fr.hashes, R * nk * (uint64_t)hcap) || dev_alloc(&fr.lofs, R * nk * (uint64_t)hcap)) return -3;
+    fr.hcap_alloc = hcap;
+    return 0;
+}
+
+static void frame_free(Frame& fr) {
+    dev_free(fr.status);
+    dev_free(fr.hash_cnt);
+    dev_free(fr.hashes);
+    dev_free(fr.lofs);
+    dev_free(fr.pflag);
+    dev_free(fr.hash_ext);
+    dev_free(fr.ovf1);
+    dev_free(fr.ovf2);
+    dev_free(fr.ovf3);
+    dev_free(fr.ovf4);
+    dev_free(fr.cand_cnt);
+    dev_free(fr.cand_tid);
+    dev_free(fr.cand_score);
+    dev_free(fr.cand_wtot);
+    dev_free(fr.cand_ext);
+    dev_free(fr.scratch);
+    dev_free(fr.ctrl);
+    dev_free(fr.ktab);
+    dev_free(fr.kcnt);
+    dev_free(fr.stash);
+    fr = Frame{};
 }
 
 int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_session** out) {
@@ -1145,49 +1227,28 @@ int skq_session_create(skq_index* ix, uint64_t max_reads, uint32_t max_len, skq_
     s->scratch_cap = 1ull << 24;
     const uint32_t hcap0 = pick_hcap(Lc, ix->mink, skq_threshold((double)0.05f));
     int rc = 0;
-    if ((rc = dev_alloc(&s->status, max_reads)) || (rc = dev_alloc(&s->hash_cnt, max_reads * ix->nk)) ||
-        (rc = dev_alloc(&s->hash_ext, s->hash_ext_cap)) || (rc = dev_alloc(&s->ovf1, s->ovf_cap)) ||
-        (rc = dev_alloc(&s->ovf2, s->ovf_cap)) || (rc = dev_alloc(&s->ovf3, s->ovf_cap)) ||
-        (rc = dev_alloc(&s->ovf4, s->ovf_cap)) || (rc = dev_alloc(&s->cand_cnt, max_reads)) ||
-        (rc = dev_alloc(&s->pflag, max_reads)) ||
-        (rc = dev_alloc(&s->cand_tid, max_reads * skq::CCAP)) ||
-        (rc = dev_alloc(&s->cand_wtot_b[0], (max_reads + 63) / 64)) ||
-        (rc = dev_alloc(&s->cand_score, max_reads * skq::CCAP)) ||
-        (rc = dev_alloc(&s->cand_ext, 2 * s->cand_ext_cap)) || (rc = dev_alloc(&s->scratch, s->scratch_cap)) ||
-        (rc = dev_alloc(&s->tx_reads, ix->ntx)) || (rc = dev_alloc(&s->tx_score, ix->ntx)) ||
-        (rc = dev_alloc(&s->tx_acc, ix->ntx)) ||
-        (rc = dev_alloc(&s->ctrl, skq::C_WORDS)) || (rc = ensure_hashes(s, hcap0))) {
+    if ((rc = frame_alloc(s, s->f, hcap0)) || (rc = dev_alloc(&s->tx_reads, ix->ntx)) ||
+        (rc = dev_alloc(&s->tx_score, ix->ntx)) || (rc = dev_alloc(&s->tx_acc, ix->ntx))) {
         skq_session_free(s);
         return rc;
     }
-    s->cand_cnt_b[0] = s->cand_cnt;
-    s->cand_tid_b[0] = s->cand_tid;
     // totals buckets: at most WG buckets of at most 2^14 ids (the LDS histogram), else direct
     // (2^12-id buckets for large transcript sets, 2^13 for small ones: cfg3 1.071 against 1.094 ms
     // per step with 1024 k_bin_sum workgroups, cfg2 the same either way; profiles/r5_totals_sweep.log)
     s->bin_bits = ix->ntx > (1u << 16) ? 12u : 13u;
-    if (const char* e = std::getenv("SKQ_BIN_BITS")) s->bin_bits = (uint32_t)std::max(8, std::min(14, std::atoi(e)));  // (A/B)
+    if (const char* e = dev_env("SKQ_BIN_BITS")) s->bin_bits = (uint32_t)std::max(8, std::min(14, std::atoi(e)));
     while (((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits > (uint64_t)skq::WG) ++s->bin_bits;
     s->bin_nb = s->bin_bits <= 14 ? (uint32_t)(((uint64_t)ix->ntx + (1ull << s->bin_bits) - 1) >> s->bin_bits) : 0u;
     const uint64_t nW = (max_reads + skq::WG - 1) / skq::WG;
     const uint64_t rwords = nW * skq::WG * skq::CCAP;
-    for (int b = 0; b < 2 && s->bin_nb; ++b)
-        if ((rc = dev_alloc(&s->bin_hdr[b], (uint64_t)(s->bin_nb + 1) * nW)) ||
-            (rc = dev_alloc(&s->bin_region[b], rwords))) {
-            skq_session_free(s);
-            return rc;
-        }
-    // (k_bin_sum's grid holds at most 512 (chunk, bucket) workgroups: 32 MiB at 2^13 ids a bucket;
-    // SKQ_SLAB=1: through the slab, else the bins go to tx_acc by atomics; development A/B)
-    const char* sl = std::getenv("SKQ_SLAB");
-    if (s->bin_nb && (sl && std::atoi(sl) == 1) && (rc = dev_alloc(&s->tx_slab, 512ull << s->bin_bits))) {
+    if (s->bin_nb && ((rc = dev_alloc(&s->bin_hdr, (uint64_t)(s->bin_nb + 1) * nW)) ||
+                      (rc = dev_alloc(&s->bin_region, rwords)))) {
         skq_session_free(s);
         return rc;
     }
     if (hipMemset(s->tx_reads, 0, ix->ntx * 8ull) != hipSuccess ||
         hipMemset(s->tx_acc, 0, ix->ntx * 8ull) != hipSuccess ||
-        hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess ||
-        hipMemset(s->ctrl, 0, skq::C_WORDS * 4) != hipSuccess) {
+        hipMemset(s->tx_score, 0, ix->ntx * 8ull) != hipSuccess) {
         skq_session_free(s);
         return fail(-3, "memset failed");
     }
@@ -1206,46 +1267,20 @@ int skq_session_free(skq_session* s) {
         (void)hipStreamSynchronize(s->side);
         (void)hipStreamDestroy(s->side);
         (void)hipEventDestroy(s->ev_fork);
-        (void)hipEventDestroy(s->ev_join[0]);
-        (void)hipEventDestroy(s->ev_join[1]);
-
+        (void)hipEventDestroy(s->ev_done[0]);
+        (void)hipEventDestroy(s->ev_done[1]);
     }
-    dev_free(s->status);
-    dev_free(s->hash_cnt);
-    dev_free(s->hashes);
-    dev_free(s->lofs);
-    dev_free(s->pflag);
-    dev_free(s->hash_ext);
-    dev_free(s->ovf1);
-    dev_free(s->ovf2);
-    dev_free(s->ovf3);
-    dev_free(s->ovf4);
-    if (s->cand_cnt_b[0]) s->cand_cnt = s->cand_cnt_b[0];  // (the current pair may be the second)
-    if (s->cand_tid_b[0]) s->cand_tid = s->cand_tid_b[0];
-    dev_free(s->cand_cnt);
-    dev_free(s->cand_tid);
-    dev_free(s->cand_score);
-    dev_free(s->cand_cnt_b[1]);
-    dev_free(s->cand_tid_b[1]);
-    dev_free(s->cand_wtot_b[0]);
-    dev_free(s->cand_wtot_b[1]);
-    dev_free(s->cand_ext);
-    dev_free(s->scratch);
-    for (int b = 0; b < 2; ++b) {
-        dev_free(s->bin_hdr[b]);
-        dev_free(s->bin_region[b]);
-    }
+    frame_free(s->f);
+    frame_free(s->alt);
+    dev_free(s->bin_hdr);
+    dev_free(s->bin_region);
     dev_free(s->tx_acc);
-    dev_free(s->tx_slab);
-    dev_free(s->ktab);
-    dev_free(s->kcnt);
-    dev_free(s->stash);
     dev_free(s->tx_reads);
     dev_free(s->tx_score);
-    dev_free(s->ctrl);
     delete s;
     return 0;
 }
+
 
 // prep: fill *prep and the session's batch state without launching (the fused map launches)
 static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
@@ -1274,13 +1309,13 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     p.hcap = hcap;
     p.ovf_cap = s->ovf_cap;
     p.rolltab = ix->d_rolltab;
-    p.status = s->status;
-    p.hash_cnt = s->hash_cnt;
-    p.hashes = s->hashes;
-    p.hash_ext = s->hash_ext;
+    p.status = s->f.status;
+    p.hash_cnt = s->f.hash_cnt;
+    p.hashes = s->f.hashes;
+    p.hash_ext = s->f.hash_ext;
     p.hash_ext_cap = s->hash_ext_cap - (uint64_t)skq::SW_GRID * skq::SW_HCH;  // (the rest: k_slow_wave's stretches)
-    p.ctrl = s->ctrl;
-    p.ovf1 = s->ovf1;
+    p.ctrl = s->f.ctrl;
+    p.ovf1 = s->f.ovf1;
     p.ovf_word = skq::C_OVF1;
     p.fuse = ix->mode;
     for (uint32_t i = 0; i < ix->nk; ++i) {
@@ -1289,13 +1324,15 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
         p.rank[i] = ix->rank[i];
         p.rovf[i] = ix->rovf[i];
     }
-    p.lofs = s->lofs;
-    p.pflag = s->pflag;
+    p.lofs = s->f.lofs;
+    p.pflag = s->f.pflag;
     p.nthash = nthash;
     if (prep) {
         *prep = p;
     } else {
-        HIP_TRY(hipMemsetAsync(s->ctrl, 0, 8 * 4, st));
+        if (int rc = wait_side(s, st)) return rc;  // (the frame's previous tail, the totals' bins)
+        s->zeroed[s->fid] = false;
+        HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, 8 * 4, st));
         hipEvent_t t0{};
         record(s, 0, &t0, st);
         if (skq::launch_sketch(p, stream)) return fail(-3, "sketch launch failed");
@@ -1323,130 +1360,76 @@ int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_off
     return sketch_impl(s, d_seqs, d_offs, fixed_len, n_seqs, max_len, threshold, 1, stream);
 }
 
-// Totals on the side stream: a batch's k_bin_sum may still run when the next batch starts. The
-// kernel that next bins into the same buffer (two batches on) waits for it; every reader of the
-// running totals waits for both.
-static int wait_bins(skq_session* s, hipStream_t st) {
-    if (s->side && s->join_rec[s->bin_par]) HIP_TRY(hipStreamWaitEvent(st, s->ev_join[s->bin_par], 0));
-    return 0;
-}
-
-static int wait_totals(skq_session* s, hipStream_t st) {
-    for (int b = 0; b < 2; ++b)
-        if (s->side && s->join_rec[b]) HIP_TRY(hipStreamWaitEvent(st, s->ev_join[b], 0));
-    return 0;
-}
-
-// The tail of a chain: the slow paths and the per-transcript totals. When the count kernel binned
-// the fast reads' candidates, k_bin_sum only reads those bins and adds into the running totals
-// with atomics (commuting with the slow paths' direct adds). For batches of 512k+ reads it runs on
-// the session's side stream and nothing on the launch stream waits for it: it overlaps the slow
-// paths and the next batch's map kernel, which bins into the other buffer (wait_bins).
-// the side stream (totals binning) and its events
-static int ensure_side(skq_session* s) {
-    if (s->side) return 0;
-    // (SKQ_SIDE_PRIO=1: the side stream at the lowest priority, so the next batch's map is
-    // dispatched ahead of the totals; development A/B)
-    const char* pe = std::getenv("SKQ_SIDE_PRIO");
-    if (pe && std::atoi(pe) == 1) {
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        std::fprintf(stderr, "[skq] side stream priority %d (range %d..%d)\n", lo, lo, hi);
-        HIP_TRY(hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo));
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-    }
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_join[0], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_join[1], hipEventDisableTiming));
-    return 0;
-}
-
-// (small batches: the extra stream hand-offs cost more than the overlap gains; with the grouped
-// k_bin_sum for few buckets, 1M reads run 5 % faster forked, 10M reads too)
-static bool totals_fork(const skq::ChainParams& p, int accumulate) {
-    const char* e = std::getenv("SKQ_TOTALS_FORK");  // (0: on the launch stream; development A/B)
-    if (e && std::atoi(e) == 0) return false;
-    return accumulate && p.slow_totals && p.n >= (1u << 19);
-}
-
-// bins already written for this batch (the count kernels' epilogue, or k_map1's with map_bins);
-// else launch_bin writes them (k_bin, or k_bin_packed over the fused map's packed candidates)
-static int binned(const skq::ChainParams& p) { return p.slow_totals && (!p.cpack || p.map_bins) ? 1 : 0; }
-
-// SKQ_GENERAL_SLOW=0 (development A/B): the general paths behind k_slow_wave as two launches
-// (k_sketch_slow over ovf3, then k_chain_slow over ovf4) instead of k_general_slow
-static bool general_slow_dev() {
-    const char* e = std::getenv("SKQ_GENERAL_SLOW");
-    return !(e && std::atoi(e) == 0);
-}
+// The tail of a batch: the slow paths, then the per-transcript totals (k_bin_packed over the fused
+// map's packed candidates, or k_bin_sum over the bins the count kernel wrote, then k_fold_totals:
+// atomics into the running totals, commuting with the slow paths' direct adds).
+// side = true (a fused map that took the other frame): the whole tail runs on the side stream,
+// beside the next batch's map on the launch stream (the batch tail); ev_done of the
+// frame follows it. Else the slow paths run on the launch stream and the totals, for batches of
+// 512k+ reads, on the side stream (the launch stream waits for them before it bins again).
+// bins already written for this batch (the count kernels' epilogue); else launch_bin writes them
+// (k_bin, or k_bin_packed over the fused map's packed candidates)
+static int binned(const skq::ChainParams& p) { return p.slow_totals && !p.cpack ? 1 : 0; }
 
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
-                      hipStream_t st) {
-    const bool fork = totals_fork(p, accumulate);
+                      hipStream_t st, bool side) {
     hipEvent_t t0{};
-    // the side stream's totals, handed off right after the map (SKQ_FORK_LATE A/B, round 5: after
-    // the slow paths instead was 1 % slower at cfg3, 3 % at cfg2; profiles/r5_tail_ab.log)
-    auto fork_totals = [&]() -> int {
+    const bool totals = accumulate != 0;
+    const bool fork = side || (totals && p.slow_totals && p.n >= (1u << 19));
+    hipStream_t tq = st;  // the stream of the totals
+    if (fork) {
         if (int rc = ensure_side(s)) return rc;
         HIP_TRY(hipEventRecord(s->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
-        record(s, 3, &t0, s->side);
-        if (skq::launch_bin(p, binned(p), s->side) ||
-            skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, s->side))
+        tq = s->side;
+    }
+    hipStream_t sq = side ? s->side : st;  // the stream of the slow paths
+    if (!fork && totals)
+        if (int rc = wait_side(s, st)) return rc;  // (tx_acc and the bins: an earlier batch's totals may run)
+    auto do_totals = [&]() -> int {
+        if (!totals) return 0;
+        record(s, 3, &t0, tq);
+        if (skq::launch_bin(p, binned(p), tq) ||
+            skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, tq))
             return fail(-3, "totals launch failed");
-        record_stop(s, 3, t0, s->side);
-        HIP_TRY(hipEventRecord(s->ev_join[s->bin_par], s->side));
-        s->join_rec[s->bin_par] = true;
+        record_stop(s, 3, t0, tq);
         return 0;
     };
-    if (fork)
-        if (int rc = fork_totals()) return rc;
+    // (with the count kernel's bins, a two-kernel batch's totals go first: its slow paths add their
+    // own reads' totals directly; else k_bin reads every read's final list, the slow ones' too)
+    const bool totals_first = !side && p.slow_totals;
+    if (totals_first)
+        if (int rc = do_totals()) return rc;
     if (sp && (p.wide == 1 || p.wide == 3) && p.nk <= (uint32_t)skq::NK_FAST) {
-        // the fused map's slow reads: the wave path first, the general paths for what it leaves
-        if (int rc = skq::launch_slow_wave(*sp, p, s->ovf3, s->ovf4, st))
+        // the fused map's slow reads: the wave path first, then k_general_slow for what it leaves
+        if (int rc = skq::launch_slow_wave(*sp, p, s->f.ovf3, s->f.ovf4, sq))
             return fail(-3, rc == -4 ? "slow path: unsupported tables" : "slow-path launch failed");
         skq::SketchParams sp2 = *sp;
-        sp2.ovf1 = s->ovf3;
+        sp2.ovf1 = s->f.ovf3;
         sp2.ovf_word = skq::C_OVF3;
         skq::ChainParams p2 = p;
-        p2.ovf2 = s->ovf4;
+        p2.ovf2 = s->f.ovf4;
         p2.ovf_word = skq::C_OVF4;
-        if (general_slow_dev()) {  // one launch for both general paths
-            if (skq::launch_general_slow(sp2, p2, st, 256)) return fail(-3, "general slow-path launch failed");
-        } else {
-            if (skq::launch_sketch_slow(sp2, st, 256)) return fail(-3, "sketch slow-path launch failed");
-            if (skq::launch_chain_slow(p2, st, 256)) return fail(-3, "chain slow-path launch failed");
-        }
+        if (skq::launch_general_slow(sp2, p2, sq, 256)) return fail(-3, "general slow-path launch failed");
     } else {
-        if (sp && skq::launch_sketch_slow(*sp, st)) return fail(-3, "sketch slow-path launch failed");
-        if (skq::launch_chain_slow(p, st)) return fail(-3, "chain slow-path launch failed");
+        if (sp && skq::launch_sketch_slow(*sp, sq)) return fail(-3, "sketch slow-path launch failed");
+        if (skq::launch_chain_slow(p, sq)) return fail(-3, "chain slow-path launch failed");
     }
-    if (accumulate && !fork) {
-        if (int rc = wait_totals(s, st)) return rc;  // (tx_acc: an earlier batch's fold may be pending)
-        record(s, 3, &t0, st);
-        if (skq::launch_bin(p, binned(p), st) ||
-            skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, st))
-            return fail(-3, "totals launch failed");
-        record_stop(s, 3, t0, st);
+    if (!totals_first)
+        if (int rc = do_totals()) return rc;
+    if (fork) {
+        HIP_TRY(hipEventRecord(s->ev_done[s->fid], s->side));
+        s->done_rec[s->fid] = true;
     }
-    if (accumulate && p.bin_nb) s->bin_par ^= 1;  // this batch's bins were written
     return 0;
 }
 
-// SKQ_MAP_BINS=1 (development A/B): k_map1 bins its candidates in its own epilogue (round 4)
-// instead of k_bin_packed after it
-static int map_bins_dev() {
-    const char* e = std::getenv("SKQ_MAP_BINS");
-    return e && std::atoi(e) == 1 ? 1 : 0;
-}
-
-// SKQ_MAPK=1: the multi-k map as one k_mapk launch (every workgroup runs the k slots in turn)
-// instead of one k_map1 launch per k slot: 1.4 % slower at cfg5 (its loop holds 128 VGPRs, 4
-// waves per SIMD against the passes' 5; profiles/r5_mapk_ab.log), so not the default. Read at
-// every map, so one process can run both.
+// SKQ_MAPK=1 (development): the multi-k map as one k_mapk launch (every workgroup runs the k slots
+// in turn) instead of one k_map1 launch per k slot: 1.4 % slower at cfg5 (its loop holds 128
+// VGPRs, 4 waves per SIMD against the passes' 5; profiles/r5_mapk_ab.log), so not the default.
+// Read at every map, so one process can run both.
 static bool mapk_dev() {
-    const char* e = std::getenv("SKQ_MAPK");
+    const char* e = dev_env("SKQ_MAPK");
     return e && std::atoi(e) == 1;
 }
 
@@ -1475,11 +1458,8 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const skq_index* ix = s->idx;
-    if (!prep && s->cand_tid_b[0]) {  // (two-kernel path: the first candidate pair, once no side-stream reader has it)
-        if (int rc = wait_totals(s, st)) return rc;
-        s->cand_cnt = s->cand_cnt_b[0];
-        s->cand_tid = s->cand_tid_b[0];
-    }
+    if (!prep)  // (two-kernel path: the current frame, once no side-stream work has it)
+        if (int rc = wait_side(s, st)) return rc;
     skq::ChainParams p{};
     p.n = n;
     p.nk = ix->nk;
@@ -1490,33 +1470,32 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.status = status;
     p.hash_cnt = hash_cnt;
     p.hashes = hashes;
-    p.hpack = hashes == s->hashes && s->hash_packed ? 1u : 0u;
-    p.hash_ext = s->hash_ext;
+    p.hpack = hashes == s->f.hashes && s->hash_packed ? 1u : 0u;
+    p.hash_ext = s->f.hash_ext;
     p.hash_offs = hash_offs;
     p.present = present;
     p.buckets = ix->d_buckets;
     p.lists = ix->d_lists;
     for (uint32_t i = 0; i < ix->nk; ++i) p.tabs[i] = ix->tabs[i];
-    p.cand_cnt = s->cand_cnt;
-    p.cand_tid = s->cand_tid;
-    p.cand_score = s->cand_score;
-    p.cand_ext = s->cand_ext;
+    p.cand_cnt = s->f.cand_cnt;
+    p.cand_tid = s->f.cand_tid;
+    p.cand_score = s->f.cand_score;
+    p.cand_ext = s->f.cand_ext;
     p.cand_ext_cap = s->cand_ext_cap - (uint64_t)skq::SW_GRID * skq::SW_CCH;  // (the rest: k_slow_wave's stretches)
-    p.scratch = s->scratch;
+    p.scratch = s->f.scratch;
     p.scratch_cap = s->scratch_cap;
     p.tx_acc = s->tx_acc;
-    p.tx_slab = s->tx_slab;
-    p.ktab = s->ktab;
-    p.kcnt = s->kcnt;
+    p.ktab = s->f.ktab;
+    p.kcnt = s->f.kcnt;
     p.tx_reads = s->tx_reads;
     p.tx_score = s->tx_score;
-    p.ctrl = s->ctrl;
-    p.ovf2 = s->ovf2;
+    p.ctrl = s->f.ctrl;
+    p.ovf2 = s->f.ovf2;
     p.ovf_word = skq::C_OVF2;
-    p.lofs = s->lofs;
-    p.pflag = s->pflag;
+    p.lofs = s->f.lofs;
+    p.pflag = s->f.pflag;
     // lofs stride: the sketch's hcap when it probed (fused), else k_probe's own capacity
-    p.lcap = probed ? hcap : std::min<uint32_t>(s->hcap_alloc, skq::HFAST);
+    p.lcap = probed ? hcap : std::min<uint32_t>(s->f.hcap_alloc, skq::HFAST);
     // wide tables: the count kernel reads the sketch's hashes and gathers the entries itself
     p.wide = !probed ? 0 : ix->mode == 3 ? 1 : ix->mode == 5 ? 3 : 0;
     if (p.wide) {
@@ -1538,16 +1517,16 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     p.ntx = ix->ntx;
     p.bin_bits = s->bin_bits;
     p.bin_nb = s->bin_nb;
-    p.bin_hdr = s->bin_hdr[s->bin_par];
-    p.bin_region = s->bin_region[s->bin_par];
+    p.bin_hdr = s->bin_hdr;
+    p.bin_region = s->bin_region;
     p.slow_totals = accumulate && skq::count_bins(p);
     if (prep) {
         *prep = p;
         return 0;
     }
     s->cand_packed = false;  // (the chain kernels write the padded rows)
-    HIP_TRY(hipMemsetAsync(s->ctrl + 8, 0, 8 * 4, st));
-    if (int rc = wait_bins(s, st)) return rc;
+    s->zeroed[s->fid] = false;
+    HIP_TRY(hipMemsetAsync(s->f.ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
     if (!probed) {
         record(s, 1, &t0, st);
@@ -1557,7 +1536,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     record(s, 2, &t0, st);
     if (skq::launch_count(p, stream)) return fail(-3, "count launch failed");
     record_stop(s, 2, t0, st);
-    if (int rc = chain_tail(s, nullptr, p, accumulate, st)) return rc;
+    if (int rc = chain_tail(s, nullptr, p, accumulate, st, false)) return rc;
     s->have_chain = true;
     return 0;
 }
@@ -1565,7 +1544,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
 int skq_chain(skq_session* s, double fraction, int accumulate, void* stream) {
     if (!s) return fail(-1, "null session");
     if (!s->have_sketch) return fail(-1, "no sketch to chain: call skq_sketch first");
-    return chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap,
+    return chain_impl(s, s->n_reads, s->f.status, s->f.hash_cnt, s->f.hashes, nullptr, nullptr, s->hcap,
                       fraction, accumulate, s->probed, stream);
 }
 
@@ -1586,38 +1565,73 @@ static bool map_fusable(const skq_session* s, const uint64_t* d_offs, uint32_t f
 static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_offs, uint32_t fixed_len,
                      uint64_t n_reads, uint32_t max_len, uint32_t threshold, double fraction, int accumulate,
                      void* stream) {
+    DeviceGuard g(s->idx->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const skq_index* ix = s->idx;
+    // the candidates packed (skq.h), unless the totals would be binned from the padded rows (k_bin);
+    // then, for batches of 512k+ reads, the tail on the side stream in the other frame
+    const bool slow_totals = accumulate && ix->ntx <= (1u << 22) && ix->nk <= (uint32_t)skq::NK_FAST && s->bin_nb > 0;
+    const bool cpack = !accumulate || slow_totals;
+    bool side = cpack && n_reads >= (1u << 19);
+    if (side) {
+        if (int rc = ensure_side(s)) return rc;
+        if (!s->alt.ctrl && frame_alloc(s, s->alt, s->f.hcap_alloc)) {  // (no room: the tail stays on the launch stream)
+            frame_free(s->alt);
+            (void)hipGetLastError();
+            side = false;
+        }
+    }
+    if (side) {
+        // this batch takes the other frame; the previous batch's frame is no longer the results, so
+        // its control words are reset on the side stream behind its tail (anything the caller ran on
+        // those results before this call is ahead of ev_fork on the launch stream)
+        std::swap(s->f, s->alt);
+        s->fid ^= 1;
+        const int o = s->fid ^ 1;
+        HIP_TRY(hipEventRecord(s->ev_fork, st));
+        HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+        HIP_TRY(hipMemsetAsync(s->alt.ctrl, 0, skq::C_WORDS * 4, s->side));
+        HIP_TRY(hipEventRecord(s->ev_done[o], s->side));
+        s->done_rec[o] = true;
+        s->zeroed[o] = true;
+        // this frame's last tail (two batches back) and its reset
+        if (s->done_rec[s->fid]) HIP_TRY(hipStreamWaitEvent(st, s->ev_done[s->fid], 0));
+        if (!s->zeroed[s->fid]) HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
+    } else {
+        if (int rc = wait_side(s, st)) return rc;
+        HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
+    }
+    s->zeroed[s->fid] = false;
     skq::SketchParams sp{};
     skq::ChainParams cp{};
-    if (s->idx->nk > 1 && (!s->ktab || !s->kcnt)) {  // the per-k tables of the multi-k passes
-        DeviceGuard g(s->idx->device);
-        dev_free(s->ktab);  // (both or neither: a failed pair is retried whole)
-        dev_free(s->kcnt);
-        int rc = dev_alloc(&s->ktab, (uint64_t)s->idx->nk * skq::DCAP * s->max_reads);
-        if (!rc) rc = dev_alloc(&s->kcnt, 2ull * s->idx->nk * s->max_reads);  // counts, needs
+    if (ix->nk > 1 && (!s->f.ktab || !s->f.kcnt)) {  // the per-k tables of the multi-k passes
+        dev_free(s->f.ktab);  // (both or neither: a failed pair is retried whole)
+        dev_free(s->f.kcnt);
+        int rc = dev_alloc(&s->f.ktab, (uint64_t)ix->nk * skq::DCAP * s->max_reads);
+        if (!rc) rc = dev_alloc(&s->f.kcnt, 2ull * ix->nk * s->max_reads);  // counts, needs
         if (rc) {
-            dev_free(s->ktab);
-            dev_free(s->kcnt);
+            dev_free(s->f.ktab);
+            dev_free(s->f.kcnt);
             return rc;
         }
     }
     if (int rc = sketch_impl(s, d_reads, d_offs, fixed_len, n_reads, max_len, threshold, 0, stream, &sp)) return rc;
-    if (s->idx->nk > 1 && use_stash()) {  // the first pass's image of the bases, for the later passes
+    if (ix->nk > 1 && use_stash()) {  // the first pass's image of the bases, for the later passes
         const uint64_t words = ((n_reads + 63) / 64) * (uint64_t)skq::stash_stride(sp.tile_chunks);
-        if (words > s->stash_words) {
-            DeviceGuard g(s->idx->device);
-            dev_free(s->stash);
-            s->stash_words = 0;
-            if (int rc = dev_alloc(&s->stash, words)) return rc;
-            s->stash_words = words;
+        if (words > s->f.stash_words) {
+            dev_free(s->f.stash);
+            s->f.stash_words = 0;
+            if (int rc = dev_alloc(&s->f.stash, words)) return rc;
+            s->f.stash_words = words;
         }
-        sp.stash = s->stash;
+        sp.stash = s->f.stash;
         sp.stash_stride = skq::stash_stride(sp.tile_chunks);
     }
     // the hashes (and the multi-k passes' per-k tables) in the per-wave packed layout (whole
     // lines written; skq.h)
     s->hash_packed = true;
-    sp.hpack = s->hash_packed ? 1u : 0u;
-    if (int rc = chain_impl(s, s->n_reads, s->status, s->hash_cnt, s->hashes, nullptr, nullptr, s->hcap, fraction,
+    sp.hpack = 1u;
+    if (int rc = chain_impl(s, s->n_reads, s->f.status, s->f.hash_cnt, s->f.hashes, nullptr, nullptr, s->hcap, fraction,
                             accumulate, true, stream, &cp))
         return rc;
     // (chained records decode unused slots as the key 0x0FFFFFFF: reads sketched at a
@@ -1627,50 +1641,24 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
             cp.chain[i] = nullptr;
             cp.chain_len[i] = 0;
         }
-    // candidates packed too, unless the totals would be binned from the padded rows (k_bin)
-    s->cand_packed = s->hash_packed && (!accumulate || cp.slow_totals);
-    cp.cpack = s->cand_packed ? 1u : 0u;
-    cp.map_bins = map_bins_dev() && (s->idx->nk == 1 ? skq::map1_bins_ok() : skq::pass_bins_ok());
-    DeviceGuard g(s->idx->device);
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    HIP_TRY(hipMemsetAsync(s->ctrl, 0, 16 * 4, st));
-    if (int rc = wait_bins(s, st)) return rc;
-    // the candidate pair: this batch's parity when k_bin_packed will read it on the side stream
-    // (wait_bins above has waited for the batch two back, the last reader of that pair); else the
-    // first pair, once every side-stream reader is done
-    uint32_t par = 0;
-    const bool side_bins = totals_fork(cp, accumulate) && cp.cpack && !cp.map_bins;
-    if (side_bins && s->bin_par == 1) {
-        if (!s->cand_tid_b[1]) {
-            if (dev_alloc(&s->cand_tid_b[1], s->max_reads * skq::CCAP) || dev_alloc(&s->cand_cnt_b[1], s->max_reads) ||
-                dev_alloc(&s->cand_wtot_b[1], (s->max_reads + 63) / 64)) {
-                dev_free(s->cand_tid_b[1]);
-                dev_free(s->cand_cnt_b[1]);
-                dev_free(s->cand_wtot_b[1]);
-                (void)hipGetLastError();
-            }
-        }
-        if (s->cand_tid_b[1]) par = 1;
-    }
-    if (!side_bins || par != s->bin_par)
-        if (int rc = wait_totals(s, st)) return rc;
-    s->cand_cnt = cp.cand_cnt = s->cand_cnt_b[par];
-    s->cand_tid = cp.cand_tid = s->cand_tid_b[par];
-    cp.cand_wtot = s->cand_wtot_b[par];
+    if ((cp.slow_totals != 0) != slow_totals) return fail(-3, "internal: totals binning mismatch");
+    s->cand_packed = cpack;
+    cp.cpack = cpack ? 1u : 0u;
+    cp.cand_wtot = s->f.cand_wtot;
     hipEvent_t t0{};
     record(s, 0, &t0, st);
     int rc = 0;
-    if (s->idx->nk == 1) {
+    if (ix->nk == 1) {
         rc = skq::launch_map1(sp, cp, stream);
     } else {
         // 2..4 k slots: one k_map1 pass per k slot (each with the raw capacity its k needs), their
-        // per-k tables in the session's ktab / kcnt; the last pass merges, filters and bins
-        const uint32_t nk = s->idx->nk;
+        // per-k tables in the frame's ktab / kcnt; the last pass merges, filters and emits
+        const uint32_t nk = ix->nk;
         const uint32_t ml = d_offs ? max_len : fixed_len;
         const uint32_t Lc = std::max<uint32_t>(1, std::min<uint32_t>(std::min(ml, s->max_len), skq::LFAST));
         uint32_t cap[SKQ_MAX_K] = {}, capmax = 0;
         for (uint32_t i = 0; i < nk; ++i) {
-            cap[i] = std::min(s->hcap, pick_hcap(Lc, s->idx->ks[i], threshold, pass_sigmas()));
+            cap[i] = std::min(s->hcap, pick_hcap(Lc, ix->ks[i], threshold, pass_sigmas()));
             capmax = std::max(capmax, cap[i]);
         }
         // a launch per k slot, each with its own capacity (or, SKQ_MAPK=1, one k_mapk launch for
@@ -1687,7 +1675,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     }
     if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
     record_stop(s, 0, t0, st);
-    if (int rc = chain_tail(s, &sp, cp, accumulate, st)) return rc;
+    if (int rc = chain_tail(s, &sp, cp, accumulate, st, side)) return rc;
     s->have_chain = true;
     // the fused kernels filled no probe offsets (lofs): a later skq_chain on these sketches
     // probes them itself (k_probe, then the count kernel over the packed sets)
@@ -1718,34 +1706,34 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
     s->x_offs = d_hash_offs;
     // every external sketch counts as sketched: the session's status array, set to SKQ_READ_OK,
     // stands in (the count kernels read a status for every read)
+    if (int rc = wait_side(s, reinterpret_cast<hipStream_t>(stream))) return rc;  // (the frame may be a tail's)
     if (n_reads)
-        HIP_TRY(hipMemsetAsync(s->status, SKQ_READ_OK, n_reads, reinterpret_cast<hipStream_t>(stream)));
-    return chain_impl(s, n_reads, s->status, d_hash_cnt, d_hashes, d_hash_offs, d_present, 0, fraction,
+        HIP_TRY(hipMemsetAsync(s->f.status, SKQ_READ_OK, n_reads, reinterpret_cast<hipStream_t>(stream)));
+    return chain_impl(s, n_reads, s->f.status, d_hash_cnt, d_hashes, d_hash_offs, d_present, 0, fraction,
                       accumulate, false, stream);
 }
 
 int skq_session_results(skq_session* s, skq_results* o) {
     if (!s || !o) return fail(-1, "null argument");
-    {  // the totals of forked batches (chain_tail) may still run on the side stream
+    {  // the batch's tail and the totals may still run on the side stream
         DeviceGuard g(s->idx->device);
-        for (int b = 0; b < 2; ++b)
-            if (s->side && s->join_rec[b]) HIP_TRY(hipEventSynchronize(s->ev_join[b]));
+        if (int rc = sync_side(s)) return rc;
     }
     o->n_reads = s->n_reads;
     o->nk = s->idx->nk;
     o->hcap = s->hcap;
     o->ccap = skq::CCAP;
     o->ntx = s->idx->ntx;
-    o->status = s->status;
-    o->hash_cnt = s->hash_cnt;
-    o->hashes = s->hashes;
-    o->hash_ext = s->hash_ext;
+    o->status = s->f.status;
+    o->hash_cnt = s->f.hash_cnt;
+    o->hashes = s->f.hashes;
+    o->hash_ext = s->f.hash_ext;
     o->hash_layout = s->hash_packed ? 1u : 0u;
     o->cand_layout = s->cand_packed ? 1u : 0u;
-    o->cand_cnt = s->cand_cnt;
-    o->cand_tid = s->cand_tid;
-    o->cand_score = s->cand_score;
-    o->cand_ext = s->cand_ext;
+    o->cand_cnt = s->f.cand_cnt;
+    o->cand_tid = s->f.cand_tid;
+    o->cand_score = s->f.cand_score;
+    o->cand_ext = s->f.cand_ext;
     o->tx_reads = s->tx_reads;
     o->tx_score = s->tx_score;
     return 0;
@@ -1756,7 +1744,8 @@ int skq_session_check(skq_session* s, void* stream) {
     DeviceGuard g(s->idx->device);
     uint32_t c[skq::C_WORDS];
     HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
-    HIP_TRY(hipMemcpy(c, s->ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    if (int rc = sync_side(s)) return rc;
+    HIP_TRY(hipMemcpy(c, s->f.ctrl, sizeof(c), hipMemcpyDeviceToHost));
     const uint32_t err = c[skq::C_ERR1] | c[skq::C_ERR2];
     if (err) {
         char buf[160];
@@ -1773,7 +1762,7 @@ int skq_session_reset_totals(skq_session* s, void* stream) {
     if (!s) return fail(-1, "null session");
     DeviceGuard g(s->idx->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (int rc = wait_totals(s, st)) return rc;
+    if (int rc = wait_side(s, st)) return rc;
     HIP_TRY(hipMemsetAsync(s->tx_reads, 0, s->idx->ntx * 8ull, st));
     HIP_TRY(hipMemsetAsync(s->tx_acc, 0, s->idx->ntx * 8ull, st));
     HIP_TRY(hipMemsetAsync(s->tx_score, 0, s->idx->ntx * 8ull, st));
@@ -1791,11 +1780,11 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     std::vector<uint32_t> hc, cc(n);
     std::vector<uint8_t> st(n);
     if (n) {
-        if (s->have_chain) HIP_TRY(hipMemcpy(cc.data(), s->cand_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
+        if (s->have_chain) HIP_TRY(hipMemcpy(cc.data(), s->f.cand_cnt, cc.size() * 4, hipMemcpyDeviceToHost));
         if (s->have_sketch) {
             hc.resize(n * nk);  // [i][r]
-            HIP_TRY(hipMemcpy(hc.data(), s->hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
-            HIP_TRY(hipMemcpy(st.data(), s->status, n, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(hc.data(), s->f.hash_cnt, hc.size() * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(st.data(), s->f.status, n, hipMemcpyDeviceToHost));
         }
     }
     std::vector<uint32_t> cx;  // packed candidates: the read's cand_ext run (pair offset) or ~0u
@@ -1804,7 +1793,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
         for (uint64_t r = 0; r < n; ++r)
             if (cc[r] & skq::CAND_EXT) {
                 cx[r] = cc[r] & ~skq::CAND_EXT;
-                HIP_TRY(hipMemcpy(&cc[r], s->cand_ext + 2ull * cx[r], 4, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(&cc[r], s->f.cand_ext + 2ull * cx[r], 4, hipMemcpyDeviceToHost));
             }
     }
     // packed layout: per (k slot, read) the hash_ext run ([count, region share, hashes...]) or ~0u,
@@ -1817,7 +1806,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
             if (hc[e] & skq::HASH_EXT) {
                 xo[e] = (uint32_t)skq::run_at(hc[e]);
                 sh[e] = skq::run_share(hc[e]);
-                HIP_TRY(hipMemcpy(&hc[e], s->hash_ext + xo[e], 4, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(&hc[e], s->f.hash_ext + xo[e], 4, hipMemcpyDeviceToHost));
             }
     }
     uint64_t th = 0, tc = 0;
@@ -1831,7 +1820,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
         if (s->have_sketch) {
             const uint32_t hcap = s->hcap;
             std::vector<uint32_t> pad((uint64_t)nk * hcap * n);  // padded: [i][j][r]; packed: per wave
-            if (n) HIP_TRY(hipMemcpy(pad.data(), s->hashes, pad.size() * 4, hipMemcpyDeviceToHost));
+            if (n) HIP_TRY(hipMemcpy(pad.data(), s->f.hashes, pad.size() * 4, hipMemcpyDeviceToHost));
             uint64_t at = 0;
             if (s->hash_packed) {  // per k slot, sets in lane order per wave; runs in hash_ext
                 std::vector<uint64_t> woff(nk, 0);
@@ -1842,7 +1831,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
                         const uint32_t c = hc[e];
                         if (xo[e] != ~0u) {
                             if (hashes && c)
-                                HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + xo[e] + 2, c * 4ull, hipMemcpyDeviceToHost));
+                                HIP_TRY(hipMemcpy(hashes + at, s->f.hash_ext + xo[e] + 2, c * 4ull, hipMemcpyDeviceToHost));
                         } else if (hashes) {
                             std::copy_n(pad.data() + (uint64_t)i * hcap * n + (r & ~63ull) * hcap + woff[i], c,
                                         hashes + at);
@@ -1862,7 +1851,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
                             if (c <= hcap) {
                                 for (uint32_t j = 0; j < c; ++j) hashes[at + j] = pad[((uint64_t)i * hcap + j) * n + r];
                             } else {
-                                HIP_TRY(hipMemcpy(hashes + at, s->hash_ext + pad[(uint64_t)i * hcap * n + r], c * 4ull,
+                                HIP_TRY(hipMemcpy(hashes + at, s->f.hash_ext + pad[(uint64_t)i * hcap * n + r], c * 4ull,
                                                   hipMemcpyDeviceToHost));
                             }
                         }
@@ -1877,8 +1866,8 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
     if (cand_offs || cand_tid || cand_score) {
         std::vector<uint32_t> t((uint64_t)skq::CCAP * n), sc((uint64_t)skq::CCAP * n);  // [j][r]
         if (n && s->have_chain) {
-            HIP_TRY(hipMemcpy(t.data(), s->cand_tid, t.size() * 4, hipMemcpyDeviceToHost));
-            HIP_TRY(hipMemcpy(sc.data(), s->cand_score, sc.size() * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(t.data(), s->f.cand_tid, t.size() * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(sc.data(), s->f.cand_score, sc.size() * 4, hipMemcpyDeviceToHost));
         }
         uint64_t at = 0, woff = 0;
         std::vector<uint32_t> ext;
@@ -1890,7 +1879,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
                 if (cx[r] != ~0u) {
                     ext.resize(2ull * c);
                     if (c)
-                        HIP_TRY(hipMemcpy(ext.data(), s->cand_ext + 2ull * (cx[r] + 1), ext.size() * 4,
+                        HIP_TRY(hipMemcpy(ext.data(), s->f.cand_ext + 2ull * (cx[r] + 1), ext.size() * 4,
                                           hipMemcpyDeviceToHost));
                     for (uint32_t j = 0; j < c; ++j) {
                         if (cand_tid) cand_tid[at + j] = ext[2 * j];
@@ -1911,7 +1900,7 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
                 }
             } else {
                 ext.resize(2ull * c);
-                HIP_TRY(hipMemcpy(ext.data(), s->cand_ext + 2ull * t[r], ext.size() * 4, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(ext.data(), s->f.cand_ext + 2ull * t[r], ext.size() * 4, hipMemcpyDeviceToHost));
                 for (uint32_t j = 0; j < c; ++j) {
                     if (cand_tid) cand_tid[at + j] = ext[2 * j];
                     if (cand_score) cand_score[at + j] = ext[2 * j + 1];
@@ -1930,7 +1919,7 @@ int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, i
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const size_t bytes = s->idx->ntx * 8ull;
     const hipMemcpyKind kind = to_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    if (int rc = wait_totals(s, st)) return rc;
+    if (int rc = wait_side(s, st)) return rc;
     if (tx_reads) HIP_TRY(hipMemcpyAsync(tx_reads, s->tx_reads, bytes, kind, st));
     if (tx_score) HIP_TRY(hipMemcpyAsync(tx_score, s->tx_score, bytes, kind, st));
     if (!to_device) HIP_TRY(hipStreamSynchronize(st));

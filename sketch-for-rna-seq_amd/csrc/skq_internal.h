@@ -166,10 +166,6 @@ struct ChainParams {
     uint64_t* scratch;
     uint64_t scratch_cap;      // u64 words
     uint64_t* tx_acc;          // per batch: (reads << 40) | score (k_bin_sum), folded by k_fold_totals
-    // (null: k_bin_sum adds its bins to tx_acc with atomics) per k_bin_sum workgroup (chunk, bucket)
-    // its whole bucket of bins, plain stores, (chunk * nb + bucket) << bin_bits; k_fold_slab sums
-    // the chunks into tx_acc
-    uint64_t* tx_slab;
     uint64_t* tx_reads;
     uint64_t* tx_score;
     uint32_t* ctrl;
@@ -186,9 +182,6 @@ struct ChainParams {
     uint32_t* bin_hdr;
     uint32_t* bin_region;
     int slow_totals;
-    // the fused map bins its candidates in its own epilogue (1; round 4) or leaves them packed for
-    // k_bin_packed, which runs after it (0: the default)
-    int map_bins;
     uint64_t* stamps;          // development: per-wave phase clocks (k_map1), null = off
     uint32_t ablate;           // development (SKQ_ABLATE, results WRONG when set): k_map1 phases
                                // skipped to price them: 2 entry-list gathers, 4 filter/order/candidate
@@ -263,10 +256,6 @@ int launch_sketch(const SketchParams& p, void* stream);
 int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid = 2048);
 // fused sketch + chain (k_map1: quant mode, one k slot, wide tables, hcap 16 or 32; -4 otherwise)
 int launch_map1(const SketchParams& p, const ChainParams& cp, void* stream);
-// whether k_map1 runs four-wave workgroups, which can bin in their epilogue (map_bins)
-bool map1_bins_ok();
-// (the same for the multi-k passes, skq_map1_pass.hip)
-bool pass_bins_ok();
 // fused sketch + chain for 2..4 k slots (wide or compact tables) by passes: k_map1 in pass mode
 // for each k slot (p.kslot; a raw capacity `cap` of 16 or 32 hashes, at most the hashes' layout
 // stride p.hcap); the last (final_pass) merges the per-k tables, filters, orders and bins

@@ -2831,28 +2831,54 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
     for (uint32_t q = t; q < (s_tot + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
-// the workgroup's bins out: to its slab slot with plain coalesced stores (k_fold_slab sums the
-// chunks: ~0.2M atomics in all instead of ~4M, one per non-empty bin of every workgroup), or
-// with atomics into tx_acc
-__device__ __forceinline__ void bins_out(const unsigned long long* s_bins, uint32_t bs, uint32_t b, uint32_t nb,
-                                         uint32_t ntx, uint64_t* tx_acc, uint64_t* slab) {
-    if (slab) {
-        uint64_t* o = slab + ((uint64_t)blockIdx.x * nb + b) * bs;
-        for (uint32_t i = threadIdx.x; i < bs; i += WG) o[i] = s_bins[i];
-        return;
+// The fused map's packed candidates summed per transcript in ONE pass when the whole transcript set
+// fits a workgroup's LDS (ntx <= TOT_SMALL_TX, u64 bins: 128 KiB): each workgroup walks a contiguous
+// stretch of map waves' packed regions (16-B loads, ChainParams::cand_wtot words each), adds
+// (1 << 40 | score) into its bins with LDS atomics, then adds its non-empty bins into the batch's
+// packed sums tx_acc with coalesced atomics. No binning pass, no headers: for cfg2 (10k transcripts)
+// it replaces k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add
+// their own totals.
+constexpr uint32_t TOT_SMALL_TX = 16384;
+__global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per) {
+    extern __shared__ unsigned long long s_tb[];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (uint32_t i = t; i < p.ntx; i += WG) s_tb[i] = 0;
+    __syncthreads();
+    const uint32_t w0 = blockIdx.x * per, w1 = min(nwaves, w0 + per);
+    for (uint32_t W = w0 + wv; W < w1; W += WG / 64) {  // one map wave's region per wave of this workgroup
+        const uint32_t tot = p.cand_wtot[W];
+        const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)W * 64 * CCAP);
+        for (uint32_t q = lane; q * 4 < tot; q += 64) {
+            const uint4 x = src[q];
+            const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (q * 4 + i < tot)
+                    atomicAdd(&s_tb[xs[i] & 0x3FFFFFu], (1ull << 40) | (unsigned long long)(xs[i] >> 22));
+        }
     }
+    __syncthreads();
+    for (uint32_t i = t; i < p.ntx; i += WG) {
+        const unsigned long long a = s_tb[i];
+        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[i]), a);
+    }
+}
+
+// the workgroup's bins out with atomics into tx_acc: one packed atomic per non-empty bin
+// ((reads << 40) | score: a batch holds < 2^24 reads of score <= 2^10), coalesced over the bins;
+// k_fold_totals unpacks the batch's sums once
+__device__ __forceinline__ void bins_out(const unsigned long long* s_bins, uint32_t bs, uint32_t b, uint32_t ntx,
+                                         uint64_t* tx_acc) {
     for (uint32_t i = threadIdx.x; i < bs; i += WG) {
         const unsigned long long a = s_bins[i];
         const uint32_t tx = b * bs + i;
-        // one packed atomic per bin ((reads << 40) | score: a batch holds < 2^24 reads of score
-        // <= 2^10); k_fold_totals unpacks the batch's sums once
         if (a && tx < ntx) atomicAdd(reinterpret_cast<unsigned long long*>(&tx_acc[tx]), a);
     }
 }
 
 __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nb, uint32_t nW,
                                                uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
-                                               uint32_t rstride, uint64_t* slab) {
+                                               uint32_t rstride) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
     const uint32_t bs = 1u << bits;
@@ -2900,7 +2926,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
         s1 = n1;
     }
     __syncthreads();
-    bins_out(s_bins, bs, b, nb, ntx, tx_acc, slab);
+    bins_out(s_bins, bs, b, ntx, tx_acc);
 }
 
 // k_bin_sum for few, long bucket segments (small transcript sets: a region's segment of a bucket
@@ -2910,7 +2936,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum(uint64_t* tx_acc, uint32_t ntx, 
 template <int GS>
 __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nW,
                                                   uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
-                                                  uint32_t rstride, uint64_t* slab) {
+                                                  uint32_t rstride) {
     extern __shared__ unsigned long long s_bins[];
     const uint32_t t = threadIdx.x, b = blockIdx.y;
     const uint32_t bs = 1u << bits;
@@ -2932,17 +2958,7 @@ __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx
         }
     }
     __syncthreads();
-    bins_out(s_bins, bs, b, gridDim.y, ntx, tx_acc, slab);
-}
-
-// the slab's chunks summed per transcript into the batch's packed sums (coalesced over t)
-__global__ __launch_bounds__(WG) void k_fold_slab(const uint64_t* slab, uint32_t chunks, uint64_t stride, uint64_t* acc,
-                                                 uint32_t ntx) {
-    for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < ntx; t += gridDim.x * WG) {
-        unsigned long long a = 0;
-        for (uint32_t c = 0; c < chunks; ++c) a += slab[c * stride + t];
-        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t]), a);
-    }
+    bins_out(s_bins, bs, b, ntx, tx_acc);
 }
 
 __global__ __launch_bounds__(WG) void k_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t ntx) {
@@ -3155,52 +3171,42 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     uint32_t* hdr = p.bin_hdr;
     const uint32_t* region = p.bin_region;
     if (nb > (uint32_t)WG) return -1;
+    if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: one pass)
+        const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
+        const uint32_t per = std::max<uint32_t>(8, (nwaves + 127) / 128);
+        const size_t lds = (size_t)p.ntx * 8;
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tot_small), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+        hipLaunchKernelGGL(k_tot_small, dim3((nwaves + per - 1) / per), dim3(WG), lds, st, p, nwaves, per);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     if (!binned) {
-        if (p.cpack && nb) {  // (the fused map's packed candidates; SKQ_BINP_CAP: 3 a 1,280-word staging
-            // (development A/B: beside five map workgroups; 1.078 against 1.074 ms per cfg3 step, so
-            // not kept, profiles/r5_totals_kernels_ab.log), 2 a 64-word one, so nearly every
-            // workgroup takes the direct adds (tests))
-            const char* e = std::getenv("SKQ_BINP_CAP");
-            const int cap = e ? std::atoi(e) : 0;
-            if (cap == 3)
-                hipLaunchKernelGGL(k_bin_packed<1280>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
-            else if (cap == 2)
-                hipLaunchKernelGGL(k_bin_packed<64>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
-            else
-                hipLaunchKernelGGL(k_bin_packed<WG * CCAP>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
-        }
+        if (p.cpack && nb)  // (the fused map's packed candidates)
+            hipLaunchKernelGGL(k_bin_packed<WG * CCAP>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
         else
             hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
         if (hipGetLastError() != hipSuccess) return -2;
     }
     if (nb == 0) return 0;
     // chunks * nb ~ 512 workgroups, 1024 for many buckets (their bins are 32 KiB: four workgroups
-    // per CU) (SKQ_BIN_WGS, read at every launch: other counts, development A/B; at most 512 with
-    // the slab, which is sized for that many)
-    uint32_t wgs = nb >= 16 && !p.tx_slab ? 1024 : 512;
-    if (const char* e = std::getenv("SKQ_BIN_WGS")) wgs = (uint32_t)std::max(1, std::min(p.tx_slab ? 512 : 8192, std::atoi(e)));
+    // per CU; profiles/r5_totals_sweep.log)
+    const uint32_t wgs = nb >= 16 ? 1024 : 512;
     const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nW, wgs / nb));
     const uint32_t chunk = (nW + chunks - 1) / chunks;
     const size_t lds = (size_t)8 << bits;
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
     if (nb <= 4) {  // few buckets: long segments per region, a 16-lane group walks each
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum_g<16>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_bin_sum_g<16>, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx,
-                           bits, nW, chunk, hdr, region, (uint32_t)(WG * CCAP), p.tx_slab);
+                           bits, nW, chunk, hdr, region, (uint32_t)(WG * CCAP));
     } else {
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
         hipLaunchKernelGGL(k_bin_sum, dim3((nW + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits,
-                           nb, nW, chunk, hdr, region, (uint32_t)(WG * CCAP), p.tx_slab);
-    }
-    if (hipGetLastError() != hipSuccess) return -2;
-    if (p.tx_slab) {  // (the slab holds (chunks * nb) << bits words: session-sized for 512 of them)
-        const uint32_t nch = (nW + chunk - 1) / chunk;
-        const unsigned grid = (unsigned)std::min<uint32_t>((p.ntx + WG - 1) / WG, 1024);
-        hipLaunchKernelGGL(k_fold_slab, dim3(grid), dim3(WG), 0, st, p.tx_slab, nch, (uint64_t)nb << bits, p.tx_acc,
-                           p.ntx);
+                           nb, nW, chunk, hdr, region, (uint32_t)(WG * CCAP));
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -1,4 +1,4 @@
-// skq_map1.h — k_map1, the fused quant kernel (sketch + index probe + chain + emit + bin), for the
+// skq_map1.h — k_map1, the fused quant kernel (sketch + index probe + chain + emit), for the
 // two map translation units (skq_map1.hip: one k; skq_map1_pass.hip: the multi-k passes). It
 // follows skq_kernels.hip (the device helpers it uses), which each of them includes first.
 #pragma once
@@ -7,17 +7,15 @@ namespace skq {
 
 // k_map1 LDS: static, at LDS address 0, the HCAP + 2 raw rows (Map1Static: row 0 the sink of
 // windows past the capacity, then the retained windows from the last row down, so a row's LDS
-// address is the hashing loop's own counter) and the roll terms; dynamic, the binning's bucket
-// counters, then per wave max(staged codes, one pass of the entry list: MAP_P hashes and their
-// owning lanes)
+// address is the hashing loop's own counter) and the roll terms; dynamic, per wave max(staged
+// codes, one pass of the entry list: MAP_P hashes and their owning lanes)
 // (the per-chunk bad bits sit in the wave's columns of the last raw row, dead until hashing starts)
 // (MAP_P: 8 per read; at 384 — the mean of cfg3's ~6.0 distinct hashes per read x 64 — half of
 // the waves listed their hashes in two passes, the second one a dependent reload and gather
 // round; profiles/r3_map1_writes.log)
 constexpr uint32_t MAP_P = 512;
-// threads per k_map1 workgroup (one k and the multi-k passes): 64 (one wave: a workgroup's LDS is
-// released when ITS wave ends) or WG (four waves, which may bin the candidates in the kernel's
-// epilogue: ChainParams::map_bins)
+// threads per k_map1 workgroup (one k): 64 (one wave: a workgroup's LDS is released when ITS wave
+// ends) or WG (four waves; the default)
 #ifndef SKQ_MAP_WG
 #define SKQ_MAP_WG 256
 #endif
@@ -29,7 +27,6 @@ constexpr int MAP_MW = SKQ_MAP_WG;
 #define SKQ_PASS_WG 64
 #endif
 constexpr int PASS_MW = SKQ_PASS_WG;
-constexpr size_t MAP1_BC_BYTES = (((size_t)WG + 1) * 4 + 15) / 16 * 16;
 // A wave's packed output (lane-ordered runs: this lane's words from its exclusive offset `off`
 // of the wave's `tot`, word j present when has(j), valued val(j)) to 16-B aligned g through the
 // wave's LDS region in chunks of MAP1_OUT_CH words, each written back as 16-B coalesced stores: a
@@ -73,6 +70,31 @@ __device__ __forceinline__ void wave_out_packed(uint32_t* g, uint32_t off, uint3
     }
 }
 
+// The hashing loop's slot counter is the LDS byte address of the lane's next raw-row store (the
+// raw rows sit at LDS address 0, Map1Static). A lane past row 0 moves it below 0: the plain subtract
+// wraps it past the LDS allocation, and the hardware drops a DS store there (tools/micro/lds_oob,
+// profiles/r5_lds_oob.log). That holds ONLY for DS stores (address_space(3), 32-bit addresses):
+// through a generic or global pointer such an address faults, as round 5's k_sketch_server did
+// with a pointer formed below an LDS array. So the counter is only ever used through
+// lds_slot_store, whose pointer is the 32-bit LDS kind (the static_assert), and the debug build
+// (make debuglds: -DSKQ_DEBUG_LDS, tests/test_debug_lds_gpu.py) clamps it at 0 instead — lane 0's
+// sink slot, which nothing reads; a read past its capacity still counts HCAP + 1 windows and goes slow.
+#ifndef SKQ_DEBUG_LDS
+#define SKQ_DEBUG_LDS 0
+#endif
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+#if defined(__HIP_DEVICE_COMPILE__)
+static_assert(sizeof(lds_u32*) == 4, "the slot counter is a 32-bit LDS (DS) address, never a generic pointer");
+#endif
+__device__ __forceinline__ void lds_slot_store(uint32_t addr, uint32_t v) { *(lds_u32*)(size_t)addr = v; }
+__device__ __forceinline__ uint32_t lds_slot_next(uint32_t d, uint32_t adv) {
+#if SKQ_DEBUG_LDS
+    return __builtin_elementwise_sub_sat(d, adv);
+#else
+    return d - adv;  // (may wrap below LDS address 0: see above)
+#endif
+}
+
 template <int HCAP, int MW = WG>
 struct Map1Static {
     uint32_t raw[(HCAP + 2) * MW];  // (first: at LDS address 0, the kernel's only static LDS)
@@ -97,25 +119,21 @@ inline size_t map1_wave_bytes(uint32_t wc, int tab, uint32_t hcap) {
     return ((m > c ? m : c) + 15) & ~(size_t)15;
 }
 
-// sets p.map_wave_bytes / p.map_flag_at; returns the launch's LDS bytes (mw: threads per workgroup;
-// the epilogue's bucket counters only where it may bin, mw = WG)
+// sets p.map_wave_bytes / p.map_flag_at; returns the launch's dynamic LDS bytes (mw: threads per
+// workgroup; the raw rows are static)
 inline size_t map1_layout(SketchParams& p, int tab, uint32_t hcap, uint32_t mw = WG) {
     p.map_wave_bytes = (uint32_t)map1_wave_bytes(p.tile_chunks, tab, hcap);
     p.map_flag_at = (uint32_t)map1_flag_at(tab, hcap);
-    // (the binning epilogue's bucket counters first, their own so they are zeroed up front; the
-    // raw rows are static)
-    (void)hcap;
-    return (mw == (uint32_t)WG ? MAP1_BC_BYTES : 0) + (mw / 64) * (size_t)p.map_wave_bytes;
+    return (mw / 64) * (size_t)p.map_wave_bytes;
 }
 
 // Fused map kernel (quant mode, one k slot, wide tables): k_sketch's staging and hashing, then
 // the retained hashes go straight from registers to the pair-cooperative wide-table count
-// (wide_chunk), the filter and the candidates, then the binning epilogue. The count tables
+// (wide_chunk), the filter and the candidates (k_bin_packed bins them for the totals after it). The count tables
 // overlay LDS the hashing no longer needs: the transcript table the raw slots ([slot][WG], this
 // lane's own), the parked list the wave's staged codes (all of the wave's lanes have left the
 // hashing loop before any counts). Reads k_sketch would hand to the slow path are listed for
-// both slow paths (k_sketch_slow, then k_chain_slow). No early exits: pairs gather together and
-// the epilogue has workgroup barriers.
+// both slow paths (k_sketch_slow, then k_chain_slow). No early exits: pairs gather together.
 // development phase clocks (ChainParams::stamps): 8 u64 per wave, written by lane 0
 #define MAP1_STAMP(i)                                                                           \
     do {                                                                                        \
@@ -146,7 +164,6 @@ __device__ __forceinline__ Map1Static<HCAP, MW>& map1_static() {
 template <int HCAP, int MB, int TAB, bool PASS, int MW>
 __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainParams& cp, const uint32_t ks, const bool FINAL) {
     static_assert(MW == WG || MW == 64 || MW == 128, "a workgroup of 256 threads (4 waves), of two or of one");
-    constexpr size_t BC = MW == WG ? MAP1_BC_BYTES : 0;  // (the binning's bucket counters: WG only)
     // TAB 4: chained entries at the compact tables' slots (one per present key, not per possible
     // key: 0.6 GB at cfg3 instead of 27.5 GB), the misses through the compact entries
     constexpr bool CMP = TAB == 2 || TAB == 4, CHN = TAB == 3 || TAB == 4, CCH = TAB == 4;
@@ -166,16 +183,13 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
     Map1Static<HCAP, MW>& s_st = map1_static<HCAP, MW>();
     uint2* s_tab = s_st.tab;
     const uint2* s_seed = s_tab + 16;
-    uint32_t* s_bc = reinterpret_cast<uint32_t*>(smem);  // the binning's bucket counters (map1_layout)
-    unsigned char* s_wave = smem + BC + wv * wave_bytes;
+    unsigned char* s_wave = smem + wv * wave_bytes;
     uint32_t* s_codes = reinterpret_cast<uint32_t*>(s_wave);
     // raw rows: row 0 the sink, retained window i of the read (position order) in row HCAP + 1 - i;
     // after the hashing, rows 1..TS hold the count tables (s_rows)
     uint32_t* s_raw = s_st.raw;
     uint32_t* s_rows = s_raw + MW;
     uint64_t* s_badw = reinterpret_cast<uint64_t*>(s_raw + (HCAP + 1) * MW + wv * 64);  // (the wave's columns, last row)
-    // (uniform; else k_bin_packed bins the packed candidates after this kernel)
-    const bool bin = MW == WG && (!PASS || FINAL) && cp.accumulate && cp.bin_nb && cp.slow_totals && cp.map_bins;
     for (uint32_t e = tid; e < 16 + 4; e += MW) {  // k slot ks's roll terms, then the seeds
         const uint64_t v = e < 16 ? p.rolltab[ks * 16 + e] : p.rolltab[p.nk * 16 + (e - 16)];
         s_tab[e] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) << 31);
@@ -187,8 +201,6 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         s_st.tb[tid] = make_uint2((uint32_t)v, (uint32_t)(v >> 32) & 1u);
     }
 #endif
-    if (bin)
-        for (uint32_t e = tid; e <= (uint32_t)WG; e += MW) s_bc[e] = 0;
     __syncthreads();
 
     const uint64_t r0 = (uint64_t)blockIdx.x * MW + wv * 64;  // this wave's first read
@@ -350,11 +362,11 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         // (HCAP + 1)-th (the read then goes slow), row 0 the sink of any past it. The lane's slot is
         // kept as its LDS offset d from the raw rows (at LDS address 0: the offset is the store's
         // address), moved by a saturating subtract, so no compare or clamp sits in the loop: a lane
-        // past row 0 lands at offset 0, lane 0's sink slot, which nothing reads. For T < 2^31 the
+        // past row 0 lands at offset 0, lane 0's sink slot, which nothing reads (lds_slot_next). For T < 2^31 the
         // test h <= T is bit 31 of ~((T - h) | h). Every operation in the loop but the rotate is a
         // full-rate VALU form (tools/micro/valu_mix: compares, min/max and the three-operand
         // integer forms issue at half rate).
-        const uint32_t rbase = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)s_raw;
+        const uint32_t rbase = (uint32_t)(size_t)(lds_u32*)s_raw;  // (0: Map1Static is the only static LDS)
         constexpr uint32_t ROW = (uint32_t)MW * 4u;
         constexpr uint32_t ROW_SH = MW == 256 ? 21u : MW == 128 ? 22u : 23u;  // (2^31 >> ROW_SH == ROW)
         static_assert((0x80000000u >> ROW_SH) == ROW, "row stride");
@@ -417,11 +429,11 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
                 lprev = hlo;
                 hlo = h;
                 yprev = e[j].y;
-                *(__attribute__((address_space(3))) uint32_t*)(size_t)(rbase + d) = h;
+                lds_slot_store(rbase + d, h);
                 uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - h, h, 0x80000000u, 0x02) >> ROW_SH
                                                       : (h <= T ? ROW : 0u);
                 if (!decltype(full)::value) adv &= (uint32_t)((int)(j - (int)jn) >> 31);  // (windows past the read)
-                d -= adv;
+                d = lds_slot_next(d, adv);
             }
         };
         uint32_t w0 = 1, bi = 0;
@@ -473,7 +485,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 roll33b(hlo, hhi, e[j]);
-                *(__attribute__((address_space(3))) uint32_t*)(size_t)(rbase + d) = hlo;
+                lds_slot_store(rbase + d, hlo);
                 // (small: ~((T - h) | h) & 2^31 as one bitop3, then the shift down to ROW)
                 uint32_t adv = decltype(small)::value ? (uint32_t)__builtin_amdgcn_bitop3_b32(T - hlo, hlo, 0x80000000u, 0x02) >> ROW_SH
                                                       : (hlo <= T ? ROW : 0u);
@@ -1124,11 +1136,6 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         }
     }
     MAP1_STAMP(4);
-    // (bin_candidates places entries only after its barriers, when every wave's count tables
-    // are dead)
-    if constexpr (MW == WG)
-        if (bin) bin_candidates(cp, tid, blockIdx.x, nc, key, s_bc, s_raw);
-    MAP1_STAMP(5);
 }
 
 // (SKQ_MAP1_WPE: a development A/B of the waves per SIMD the compiler budgets registers for; TAB 4

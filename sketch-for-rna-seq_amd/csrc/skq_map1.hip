@@ -7,25 +7,6 @@
 namespace skq {
 
 constexpr int MW = MAP_MW;
-bool map1_bins_ok() { return MW == WG; }
-
-// SKQ_MAP1_OCC=1: print each k_map1 launch shape's resident workgroups per CU once (stderr)
-static void map1_report_occupancy(const void* kern, size_t lds) {
-    static const bool on = [] {
-        const char* e = std::getenv("SKQ_MAP1_OCC");
-        return e && std::atoi(e) != 0;
-    }();
-    if (!on) return;
-    static std::mutex mu;
-    static std::vector<std::pair<const void*, size_t>> seen;
-    std::lock_guard<std::mutex> g(mu);
-    for (auto& x : seen)
-        if (x.first == kern && x.second == lds) return;
-    seen.emplace_back(kern, lds);
-    int nb = -1;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, MW, lds);
-    std::fprintf(stderr, "[skq] k_map1 %p: %zu B LDS, %d workgroups per CU\n", kern, lds, nb);
-}
 
 int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     if (p0.n == 0) return 0;
@@ -51,12 +32,9 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     case 258: kern = k_map1<32, 4, 2, false, false, MW>; break;
     default: return -4;
     }
-    // (development: SKQ_LDS_PAD bytes of unused LDS per workgroup lower the occupancy, to price it)
-    static const size_t pad = std::getenv("SKQ_LDS_PAD") ? std::strtoull(std::getenv("SKQ_LDS_PAD"), nullptr, 10) : 0;
-    if (lds + pad > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds + pad));
-    map1_report_occupancy(reinterpret_cast<const void*>(kern), lds + pad);
-    hipLaunchKernelGGL(kern, grid, dim3(MW), lds + pad, st, p, cp);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(MW), lds, st, p, cp);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -6,8 +6,6 @@
 
 namespace skq {
 
-bool pass_bins_ok() { return PASS_MW == WG; }
-
 int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap, bool final_pass, void* stream) {
     if (p0.n == 0) return 0;
     if ((cp.wide != 1 && cp.wide != 3) || cap > p0.hcap || p0.kslot >= SKQ_MAX_K) return -4;

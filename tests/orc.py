@@ -56,6 +56,9 @@ def lib():
                                     C.c_double] + [C.c_void_p] * 3 + [C.c_uint32] + [C.c_void_p] * 3 + [C.c_uint32]
         L.orc_map_batch_count.restype = C.c_uint64
         L.orc_map_batch_count.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_double]
+        L.orc_map_digest.restype = C.c_int
+        L.orc_map_digest.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_double, C.c_int,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]
         L.orc_em.restype = C.c_int
         L.orc_em.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.c_double,
                              C.c_void_p]
@@ -246,6 +249,25 @@ def fastq_map(index, fq, nthreads=1, outputs=True, totals=True, hcap=None, ccap=
                    hashes=res["hashes"][:n * nk * hcap].reshape(n, nk, hcap), cand_cnt=res["cand_cnt"][:n],
                    cand_tid=res["cand_tid"][:n * ccap].reshape(n, ccap),
                    cand_score=res["cand_score"][:n * ccap].reshape(n, ccap), kept=res["kept"][:n].astype(bool))
+    if totals:
+        out.update(tx_reads=txr[:index.ntx], tx_score=txs[:index.ntx])
+    return out
+
+
+def map_digest(index, bases, L, nthreads=1, totals=True, thr=None, fraction=CHAIN_FRACTION):
+    """orc_map_digest over fixed-length reads (bases: flat uint8, len n*L): per-read digests
+    (tests/digest.py restates them over an skq export) and the per-transcript totals."""
+    bases = np.ascontiguousarray(bases, np.uint8)
+    n = bases.size // L
+    thr = threshold() if thr is None else thr
+    dg = np.zeros(max(n, 1), np.uint64)
+    txr = np.zeros(max(index.ntx, 1), np.uint64) if totals else None
+    txs = np.zeros(max(index.ntx, 1), np.uint64) if totals else None
+    rc = lib().orc_map_digest(index.h, ptr(bases), L, n, thr, fraction, nthreads, ptr(dg),
+                              ptr(txr) if totals else None, ptr(txs) if totals else None)
+    if rc != 0:
+        raise RuntimeError("orc_map_digest failed (%d)" % rc)
+    out = dict(n=n, digest=dg[:n])
     if totals:
         out.update(tx_reads=txr[:index.ntx], tx_score=txs[:index.ntx])
     return out

@@ -465,27 +465,42 @@ def test_chain_sketches_entry_point(tx300):
         assert list(out["cand_score"][co[r]:co[r + 1]]) == list(sc[:c])
 
 
-@pytest.mark.parametrize("slab", ["0", "1"])
-def test_repeated_batches_accumulate_totals(tx300, slab, monkeypatch):
-    """slab: the totals' bins through k_bin_sum's per-chunk slab and k_fold_slab (SKQ_SLAB=1)."""
-    monkeypatch.setenv("SKQ_SLAB", slab)
+@pytest.mark.parametrize("n", [1000, 600_000])
+def test_repeated_batches_accumulate_totals(tx300, n):
+    """Three different batches through one session, totals accumulated. n = 600k (>= 2^19 reads):
+    a fused map's tail (slow paths, totals binning) runs on the session's side stream and
+    consecutive batches alternate between the session's two frames, the next map writing one while
+    the previous tail still reads and writes the other. The totals are the three batches' sums, and
+    the results read after a batch are that batch's own, read by read (per-read digests: status,
+    retained-hash sets, candidate lists; tests/digest.py)."""
+    import digest
     gi, oi = build([31], tx=tx300)
-    bases, _, _ = synth.reads(tx300, 1000, 150, seed=44)
-    reads = [bases[i * 150:(i + 1) * 150].tobytes() for i in range(1000)]
-    buf, offs = skq.pack_reads(reads)
-    s = skq.Session(gi, 1000, 150)
-    d_buf = skq.DeviceBuffer.from_numpy(buf)
-    for _ in range(3):
-        s.map(d_buf.ptr, None, 1000, 150, fixed_len=150)
-    s.check()
-    ref = oi.map_batch(reads)
-    tr, ts = totals_from(ref, 1000, tx300.ntx)
-    a, b = s.totals()
-    np.testing.assert_array_equal(a, 3 * tr)
-    np.testing.assert_array_equal(b, 3 * ts)
+    s = skq.Session(gi, n, 150)
+    tr = np.zeros(tx300.ntx, np.uint64)
+    ts = np.zeros(tx300.ntx, np.uint64)
+    keep = []
+    for b in range(3):
+        bases, _, _ = synth.reads(tx300, n, 150, seed=44 + b)
+        d = skq.DeviceBuffer.from_numpy(bases)
+        keep.append(d)  # (freed at the end: a batch's tail may still read its reads)
+        s.map(d.ptr, None, n, 150, fixed_len=150)
+        cpu = orc.map_digest(oi, bases, 150, nthreads=16)
+        tr += cpu["tx_reads"]
+        ts += cpu["tx_score"]
+        if b != 1:  # (batch 1's results are left unread: batch 2 resets its frame behind its tail)
+            s.check()
+            dg = digest.export_digest(s.export(), 1)
+            bad = np.nonzero(dg != cpu["digest"])[0]
+            assert len(bad) == 0, "batch %d: %d reads differ (first %s)" % (b, len(bad), bad[:8].tolist())
+    a, c = s.totals()
+    np.testing.assert_array_equal(a, tr)
+    np.testing.assert_array_equal(c, ts)
     s.reset_totals()
     a, _ = s.totals()
     assert a.sum() == 0
+    s.free()
+    for d in keep:
+        d.free()
 
 
 def test_very_long_reads_and_large_postings():
@@ -513,13 +528,11 @@ def test_very_long_reads_and_large_postings():
         compare(out, ref, len(reads), 1)
 
 
-@pytest.mark.parametrize("mapk", ["1", "0"])
 @pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
-def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len, mapk, monkeypatch):
-    """With wide or compact tables, 2-4 k slots map through the k slots' passes — one k_map1
-    launch each (the default) or one k_mapk launch for all (SKQ_MAPK=1) — with no separate
-    count launch; every other probe structure through k_sketch + a count kernel. All bit-exact."""
-    monkeypatch.setenv("SKQ_MAPK", mapk)
+def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len):
+    """With wide or compact tables, 2-4 k slots map through the k slots' passes (one k_map1 launch
+    each) with no separate count launch; every other probe structure through k_sketch + a count
+    kernel. All bit-exact."""
     gi, oi = build(ks, tx=tx300)
     bases, _, _ = synth.reads(tx300, 2000, read_len, seed=77, err=0.002)
     reads = [bases[i * read_len:(i + 1) * read_len].tobytes() for i in range(2000)]
@@ -548,15 +561,11 @@ def test_fused_multi_k_path_is_taken_and_exact(tx300, probe_mode, ks, read_len, 
     np.testing.assert_array_equal(out["totals"][1], ts)
 
 
-@pytest.mark.parametrize("mapk", ["1", "0"])
-@pytest.mark.parametrize("stash", ["1", "0"])
-def test_multi_k_passes_base_image(tx300, probe_mode, monkeypatch, stash, mapk):
+def test_multi_k_passes_base_image(tx300, probe_mode):
     """The k_map1 passes: the first stores each wave's staged bases (2-bit codes + bad bits) and
-    the later passes stage from that image (SKQ_STASH=1, the default) or re-read the bases
-    (SKQ_STASH=0). Variable lengths, an unaligned buffer, bad bytes, short and > 256-bp reads and
-    several batches through one session (the image grows with the batch): bit-exact both ways."""
-    monkeypatch.setenv("SKQ_STASH", stash)
-    monkeypatch.setenv("SKQ_MAPK", mapk)  # (one launch for the k slots, or one per k slot)
+    the later passes stage from that image. Variable lengths, an unaligned buffer, bad bytes, short
+    and > 256-bp reads and several batches through one session (the image grows with the batch):
+    bit-exact."""
     ks = [21, 25, 31]
     gi, oi = build(ks, tx=tx300)
     rng = random.Random(11)

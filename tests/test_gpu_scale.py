@@ -94,14 +94,12 @@ def _case(tx, ks, L, nreads, seed, err=0.001, chained=False):
     return cpu, st, slow
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact", "chain-tight"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact", "chain-tight"])
 def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
-    """chain-slab: the totals through k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: the
-    chained tables at the compact tables' slots (SKQ_CHAIN=2); chain-tight: a device budget the
-    chained tables per possible key do not fit (SKQ_CHAIN_MB=2048), so the index sizes itself to
-    compact entries + chained tables per present key."""
+    """chain-compact: the chained tables at the compact tables' slots (SKQ_CHAIN=2); chain-tight: a
+    device budget the chained tables per possible key do not fit (SKQ_CHAIN_MB=2048), so the index
+    sizes itself to compact entries + chained tables per present key."""
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
-    monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
     if mode == "chain-tight":
         monkeypatch.setenv("SKQ_CHAIN_MB", "2048")
     cpu, st, _ = _case(tx10k, [31], 100, 300_000, seed=201, chained=mode != "map1")
@@ -114,15 +112,11 @@ def test_cfg2_10k_transcripts_100bp(tx10k, mode, monkeypatch):
             assert st["device_bytes"] < 2e9, st
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-slab", "chain-compact", "chain-binp-direct"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact"])
 def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
-    """chain: k_map1 over the chained tables (SKQ_CHAIN=1); chain-slab: and the totals through
-    k_bin_sum's per-chunk slab (SKQ_SLAB=1); chain-compact: over compact tables (SKQ_CHAIN=2);
-    chain-binp-direct: k_bin_packed with a 64-word staging (SKQ_BINP_CAP=2), so its workgroups add
-    their candidates straight into the totals."""
-    monkeypatch.setenv("SKQ_BINP_CAP", "2" if mode == "chain-binp-direct" else "0")
+    """chain: k_map1 over the chained tables (SKQ_CHAIN=1); chain-compact: over compact tables
+    (SKQ_CHAIN=2)."""
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
-    monkeypatch.setenv("SKQ_SLAB", "1" if mode.endswith("slab") else "0")
     cpu, st, slow = _case(tx200k, [31], 150, 400_000, seed=301, chained=mode != "map1")
     assert (st["chained"] > 2) == (mode != "map1"), st
     assert (st["probe"] == "compact") == (mode == "chain-compact"), st
@@ -131,12 +125,10 @@ def test_cfg3_200k_transcripts_150bp(tx200k, mode, monkeypatch):
     assert slow[0] + slow[1] > 0  # the slow paths ran at scale and agreed
 
 
-@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact", "chain-mapk"])
+@pytest.mark.parametrize("mode", ["map1", "chain", "chain-compact"])
 def test_cfg5_multi_k_200k_transcripts(tx200k, mode, monkeypatch):
     """chain: every k slot's pass over its own chained tables (3 x 27.5 GB), one k_map1 launch
-    each; chain-compact: the chained entries at the compact slots (SKQ_CHAIN=2, 3 x ~0.6 GB);
-    chain-mapk: the passes in one k_mapk launch (SKQ_MAPK=1)."""
-    monkeypatch.setenv("SKQ_MAPK", "1" if mode == "chain-mapk" else "0")
+    each; chain-compact: the chained entries at the compact slots (SKQ_CHAIN=2, 3 x ~0.6 GB)."""
     monkeypatch.setenv("SKQ_CHAIN", "0" if mode == "map1" else "2" if mode == "chain-compact" else "1")
     cpu, st, sl = _case(tx200k, [21, 25, 31], 150, 250_000, seed=501, chained=mode != "map1")
     assert (st["chained"] > 2) == (mode != "map1"), st
@@ -150,17 +142,21 @@ def test_full_batch_totals(tx200k, n, seed, ks, monkeypatch):
     """The bench's own batches, one skq_map each: cfg3 (10M x 150 bp, rank 0), cfg4's per-GPU
     shard (12.5M x 150 bp; rank 3's seed, as bench.py --gpus 8 draws it) and cfg5's batch (10M,
     multi-k passes, ~37k slow reads whose runs the slow wave writes while it reads other reads'
-    packed offsets): per-transcript totals equal the oracle's over the same reads as FASTQ text.
-    Each batch runs three times against one oracle pass: over the wide entries, over the chained
-    tables the bench and the CLI default to (an index given the transcripts' sequences), whose
-    marker entries (lists > 8 ids), queries past the table, slow-read hand-off and totals binning
-    are then checked at the full batch too, and over the chained entries at the compact tables'
-    slots (SKQ_CHAIN=2), where a query that is no key lands on another key's slot."""
+    packed offsets): per-transcript totals AND every read's own result equal the oracle's over the
+    same reads. Per read: a 64-bit digest of its status, its retained-hash sets and its candidate
+    list (oracle/oracle.c orc_map_digest; tests/digest.py over the export), so a candidate list
+    moved between reads or equal-score entries swapped, which keep the totals, still fail
+    (src/sparse_chaining.cpp:107-111: the reference's output is per read). Each batch runs three
+    times against one oracle pass: over the wide entries, over the chained tables the bench and the
+    CLI default to (an index given the transcripts' sequences), whose marker entries (lists > 8
+    ids), queries past the table, slow-read hand-off and totals binning are then checked at the
+    full batch too, and over the chained entries at the compact tables' slots (SKQ_CHAIN=2), where a
+    query that is no key lands on another key's slot."""
+    import digest
     L = 150
     tables = skq.build_tables(tx200k.seqs, tx200k.offs, ks, nthreads=NTHREADS)
     bases, _, _ = synth.reads(tx200k, n, L, seed=seed, err=0.001)  # bench.py's batch of rank seed - 1000
-    cpu = orc.fastq_map(_oracle(tables, ks, tx200k.ntx), synth.fastq_bytes(bases, L), nthreads=NTHREADS,
-                        outputs=False, totals=True)
+    cpu = orc.map_digest(_oracle(tables, ks, tx200k.ntx), bases, L, nthreads=NTHREADS)
     assert cpu["n"] == n
     d = skq.DeviceBuffer.from_numpy(bases)
     del bases
@@ -175,10 +171,13 @@ def test_full_batch_totals(tx200k, n, seed, ks, monkeypatch):
         s.check()
         tot = s.totals()
         slow = s.slow_reads()
+        dg = digest.export_digest(s.export(), len(ks))
         s.free()
         index.free()
         np.testing.assert_array_equal(tot[0], cpu["tx_reads"], err_msg="chained=%s" % chained)
         np.testing.assert_array_equal(tot[1], cpu["tx_score"], err_msg="chained=%s" % chained)
+        bad = np.nonzero(dg != cpu["digest"])[0]
+        assert len(bad) == 0, "chained=%s: %d reads differ (first %s)" % (chained, len(bad), bad[:8].tolist())
         assert int(tot[0].sum()) > 3 * n  # ~3.1 candidates per read
         assert slow[0] + slow[1] > 100
     d.free()

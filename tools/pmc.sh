@@ -10,6 +10,9 @@
 #        stall  issue waits, scalar / LDS pipes, instruction cache, L1 translation, texture addresser
 #        lds    LDS instructions, bank and address conflicts
 #        l1     L1 -> L2 read requests and their latency
+#        bound  cycle counters for what binds a kernel (VALU busy cycles, waits, resident waves,
+#               LDS conflicts, the texture addresser), each pass with GRBM_GUI_ACTIVE for the
+#               kernel's cycles; tools/pmc_bound.py derives the fractions
 # e.g. tools/pmc.sh stall gpurun_out/st --probes wide/chain --rounds 2
 set -u
 set_=$1 out=$2
@@ -26,7 +29,10 @@ case "$set_" in
                "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY") ;;
   l1) groups=("TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCC_HIT_sum TCC_MISS_sum"
               "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCP_TOTAL_CACHE_ACCESSES_sum SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES") ;;
-  *) echo "unknown counter set $set_ (mem, inst, stall, lds, l1)"; exit 2 ;;
+  bound) groups=("SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE"
+                 "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_RD SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
+                 "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum SQ_WAVES GRBM_GUI_ACTIVE") ;;
+  *) echo "unknown counter set $set_ (mem, inst, stall, lds, l1, bound)"; exit 2 ;;
 esac
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p "$out"

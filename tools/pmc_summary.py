@@ -10,7 +10,9 @@ d = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
 for f in sorted(glob.glob(d + '/p*/run_counter_collection.csv')):
     for row in csv.DictReader(open(f)):
-        agg[row['Kernel_Name'][:48]][row['Counter_Name']][int(row['Dispatch_Id'])] += float(row['Counter_Value'])
+        # (keyed by pass file and dispatch: a counter in two passes is two sets of dispatches, not one
+        # summed set — round 4's stall summaries doubled SQ_WAVES that way)
+        agg[row['Kernel_Name'][:48]][row['Counter_Name']][(f, int(row['Dispatch_Id']))] += float(row['Counter_Value'])
 for kn, cs in agg.items():
     if 'skq' not in kn:
         continue
