@@ -916,14 +916,39 @@ __device__ __forceinline__ uint32_t quad_or_all(uint32_t v) {
 }
 
 // inclusive prefix sum over the 64 lanes of a wave
+// Inclusive prefix sum over the wave's 64 lanes by DPP: shifts by 1, 2, 4, 8 within each row of 16
+// lanes, then the row broadcasts of lanes 15 (into rows 1 and 3) and 31 (into rows 2 and 3). Twelve
+// VALU and no LDS: the __shfl_up form (SKQ_SCAN_DPP=0) is six dependent ds_bpermute round trips
+// and keeps six 64-bit lane masks in SGPRs, which k_map1 spills to VGPR lanes.
+#ifndef SKQ_SCAN_DPP
+#define SKQ_SCAN_DPP 1
+#endif
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v) {
+    // (bound_ctrl off: a lane whose source is out of its row, or whose row is masked, adds the 0)
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#if SKQ_SCAN_DPP
+    (void)lane;
+    v = dpp_add<0x111, 0xF>(v);  // row_shr:1
+    v = dpp_add<0x112, 0xF>(v);  // row_shr:2
+    v = dpp_add<0x114, 0xF>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xF>(v);  // row_shr:8
+    v = dpp_add<0x142, 0xA>(v);  // row_bcast:15
+    v = dpp_add<0x143, 0xC>(v);  // row_bcast:31
+    return v;
+#else
 #pragma unroll
     for (uint32_t o = 1; o < 64; o <<= 1) {
         const uint32_t x = __shfl_up(v, o, 64);
         if (lane >= o) v += x;
     }
     return v;
+#endif
 }
+// lane 63's value, wave-uniform (v_readlane: no LDS round trip)
+__device__ __forceinline__ uint32_t wave_last(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
 
 // probes per wave held in LDS: 512 per k slot (a 64-read wave of 150 bp reads averages ~384
 // at k = 31; a read that does not fit takes the slow path)

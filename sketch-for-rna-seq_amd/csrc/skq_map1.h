@@ -567,7 +567,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         const uint32_t incl = wave_incl_scan(mw, lane);
         hoff = incl - mw;
         // (the wave's region: the staged codes are dead, the chain step's loads issued)
-        wave_out_packed<HCAP>(p.hashes + (uint64_t)ks * p.hcap * p.n + r0 * p.hcap, hoff, __shfl(incl, 63, 64),
+        wave_out_packed<HCAP>(p.hashes + (uint64_t)ks * p.hcap * p.n + r0 * p.hcap, hoff, wave_last(incl),
                               reinterpret_cast<uint32_t*>(s_wave), lane, [&](int j) { return ((keepm >> j) & 1ull) != 0; },
                               [&](int j) { return v[j]; });
     }
@@ -742,7 +742,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
     const uint32_t m = act ? (uint32_t)__builtin_popcountll(keepm) : 0u;
     const uint32_t incl = wave_incl_scan(m, lane);
     const uint32_t off = incl - m;
-    const uint32_t M = __shfl(incl, 63, 64);
+    const uint32_t M = wave_last(incl);
     {
     // the first pass's list, straight from the sorted registers (v dies here)
     {
@@ -945,7 +945,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
         }
         if (!FINAL && cp.hpack) {  // (uniform) packed: the wave's kept entries in lane order
             const uint32_t incl = wave_incl_scan(km, lane);
-            wave_out_packed<TS>(cp.ktab + (uint64_t)ks * TS * cp.n + r0 * TS, incl - km, __shfl(incl, 63, 64),
+            wave_out_packed<TS>(cp.ktab + (uint64_t)ks * TS * cp.n + r0 * TS, incl - km, wave_last(incl),
                                 reinterpret_cast<uint32_t*>(s_wave), lane, [&](int sl) { return kev[sl] != EMPTY; },
                                 [&](int sl) { return kev[sl]; });
         }
@@ -1080,7 +1080,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
             if (cp.cpack) {  // (uniform) packed: the wave's candidates in lane order, tid | score << 22
                 const uint32_t incl = wave_incl_scan(nc, lane);
                 if (lane == 63 && cp.cand_wtot && nr) cp.cand_wtot[r0 >> 6] = incl;  // (k_bin_packed)
-                wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64),
+                wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, wave_last(incl),
                                     reinterpret_cast<uint32_t*>(s_wave), lane, [&](int d) { return (uint32_t)d < nc; },
                                     [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
             }
@@ -1130,7 +1130,7 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
             const uint32_t incl = wave_incl_scan(nc, lane);
             if (lane == 63 && cp.cand_wtot && nr) cp.cand_wtot[r0 >> 6] = incl;  // (k_bin_packed)
             // (the wave's region: the entry list and the per-read flags are dead)
-            wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, __shfl(incl, 63, 64), reinterpret_cast<uint32_t*>(s_wave),
+            wave_out_packed<TS, true>(cp.cand_tid + r0 * CCAP, incl - nc, wave_last(incl), reinterpret_cast<uint32_t*>(s_wave),
                                 lane, [&](int d) { return (uint32_t)d < nc; },
                                 [&](int d) { return (key[d] & 0x3FFFFFu) | ((1023u - (key[d] >> 22)) << 22); });
         }
