@@ -173,6 +173,7 @@ struct skq_session {
     hipEvent_t ev_fork{}, ev_done[2]{};
     bool done_rec[2] = {false, false};
     bool zeroed[2] = {false, false};
+    bool tail_side[2] = {false, false};  // the frame's batch ran its tail on the side stream
 };
 
 int skq::session_device(const skq_session* s) { return s->idx->device; }
@@ -803,10 +804,11 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
         if (!known) return fail(-1, std::string("SKQ_PROBE: unknown probe kind ") + force);
         if (!std::strcmp(force, "bucket")) return 0;
     } else {
-        // (SKQ_CHAIN=2, or the sizing rule of index_create_impl: a compact index whose placement
-        // fails falls back to the other kinds, as an unforced one does)
-        force = prefer_compact ? "compact" : nullptr;
+        force = nullptr;
     }
+    // (prefer_compact: SKQ_CHAIN=2, or the sizing rule of index_create_impl — compact entries first,
+    // within the same budget checks as an unforced choice; if their placement fails, the wide
+    // entries when they fit, then the other kinds, as an unforced index falls back)
     if (force && !std::strcmp(force, "rank")) return build_rank(ix, ntables, tables, dkeys, dvals);
     uint64_t need = 0, len[SKQ_MAX_K] = {};
     for (uint32_t t = 0; t < ntables; ++t) {
@@ -819,19 +821,21 @@ int build_direct(skq_index* ix, uint32_t ntables, const skq_kmer_table* tables,
     const bool ids_ok = ix->ntx <= (1u << 22) && ix->nlist_words < 0x80000000ull;
     auto forced = [&](const char* kind) { return force && !std::strcmp(force, kind); };
     const bool wide_ok = ids_ok && need * 8 <= budget && need * 8 <= fr / 2;
-    if (wide_ok && (!force || forced("wide"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
+    if (wide_ok && !prefer_compact && (!force || forced("wide"))) return build_wide(ix, ntables, tables, dkeys, dvals, len);
     if (forced("wide")) return 0;  // forced but does not fit: bucket table
     uint64_t cmp_need = 0;  // compact tables: m / 0.95 slots of 32 B + 2-B pilots per 5 keys, per k
     for (uint32_t t = 0; t < ntables; ++t)
         cmp_need += (uint64_t)std::ceil((double)dkeys[t].size() / 0.95) * 32 + 64 + (dkeys[t].size() + 4) / 5 * 2;
     if (ids_ok && (forced("compact") || (!force && cmp_need <= budget && cmp_need <= fr / 2))) {
         const int rc = build_compact(ix, ntables, tables, dkeys, dvals, lists);
-        if (rc == 0 || (forced("compact") && !prefer_compact)) return rc;  // (SKQ_PROBE=compact: its error)
+        if (rc == 0 || forced("compact")) return rc;  // (SKQ_PROBE=compact: its error)
         for (auto& d : ix->d_wdir_t) dev_free(d);  // (placement or allocation failed: another kind)
         for (auto& d : ix->d_wpil_t) dev_free(d);
         for (auto& w : ix->wdir) w = nullptr;
         for (auto& w : ix->wpil) w = nullptr;
+        (void)hipGetLastError();
     }
+    if (wide_ok && prefer_compact && !force) return build_wide(ix, ntables, tables, dkeys, dvals, len);
     if (need > budget || need > fr / 2) return 0;
     hipStream_t st = nullptr;
     uint32_t *dk = nullptr, *dv = nullptr;
@@ -1332,6 +1336,7 @@ static int sketch_impl(skq_session* s, const uint8_t* d_reads, const uint64_t* d
     } else {
         if (int rc = wait_side(s, st)) return rc;  // (the frame's previous tail, the totals' bins)
         s->zeroed[s->fid] = false;
+        s->tail_side[s->fid] = false;
         HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, 8 * 4, st));
         hipEvent_t t0{};
         record(s, 0, &t0, st);
@@ -1410,7 +1415,9 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         skq::ChainParams p2 = p;
         p2.ovf2 = s->f.ovf4;
         p2.ovf_word = skq::C_OVF4;
-        if (skq::launch_general_slow(sp2, p2, sq, 256)) return fail(-3, "general slow-path launch failed");
+        // (32 workgroups: the general reads are rare — none at cfg2, 3, 5 — and each of its workgroups
+        // needs 33 KB of LDS, which beside a running map only frees up as map workgroups retire)
+        if (skq::launch_general_slow(sp2, p2, sq, 32)) return fail(-3, "general slow-path launch failed");
     } else {
         if (sp && skq::launch_sketch_slow(*sp, sq)) return fail(-3, "sketch slow-path launch failed");
         if (skq::launch_chain_slow(p, sq)) return fail(-3, "chain slow-path launch failed");
@@ -1526,6 +1533,7 @@ static int chain_impl(skq_session* s, uint64_t n, const uint8_t* status, const u
     }
     s->cand_packed = false;  // (the chain kernels write the padded rows)
     s->zeroed[s->fid] = false;
+    s->tail_side[s->fid] = false;
     HIP_TRY(hipMemsetAsync(s->f.ctrl + 8, 0, 8 * 4, st));
     hipEvent_t t0{};
     if (!probed) {
@@ -1583,13 +1591,16 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     }
     if (side) {
         // this batch takes the other frame; the previous batch's frame is no longer the results, so
-        // its control words are reset on the side stream behind its tail (anything the caller ran on
-        // those results before this call is ahead of ev_fork on the launch stream)
+        // its control words are reset on the side stream behind its tail (the host reads control
+        // words only synchronously, after sync_side: nothing on the launch stream reads them, so
+        // the reset needs no hand-off from it — one cross-queue wait fewer between two maps)
         std::swap(s->f, s->alt);
         s->fid ^= 1;
         const int o = s->fid ^ 1;
-        HIP_TRY(hipEventRecord(s->ev_fork, st));
-        HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+        if (!s->tail_side[o]) {  // (the previous batch ran on the launch stream: its kernels first)
+            HIP_TRY(hipEventRecord(s->ev_fork, st));
+            HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+        }
         HIP_TRY(hipMemsetAsync(s->alt.ctrl, 0, skq::C_WORDS * 4, s->side));
         HIP_TRY(hipEventRecord(s->ev_done[o], s->side));
         s->done_rec[o] = true;
@@ -1602,6 +1613,7 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
     }
     s->zeroed[s->fid] = false;
+    s->tail_side[s->fid] = side;
     skq::SketchParams sp{};
     skq::ChainParams cp{};
     if (ix->nk > 1 && (!s->f.ktab || !s->f.kcnt)) {  // the per-k tables of the multi-k passes

@@ -2856,36 +2856,42 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
     for (uint32_t q = t; q < (s_tot + 3) / 4; q += WG) reg[q] = sr[q];
 }
 
-// The fused map's packed candidates summed per transcript in ONE pass when the whole transcript set
-// fits a workgroup's LDS (ntx <= TOT_SMALL_TX, u64 bins: 128 KiB): each workgroup walks a contiguous
-// stretch of map waves' packed regions (16-B loads, ChainParams::cand_wtot words each), adds
-// (1 << 40 | score) into its bins with LDS atomics, then adds its non-empty bins into the batch's
-// packed sums tx_acc with coalesced atomics. No binning pass, no headers: for cfg2 (10k transcripts)
-// it replaces k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add
-// their own totals.
-constexpr uint32_t TOT_SMALL_TX = 16384;
-__global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per) {
-    extern __shared__ unsigned long long s_tb[];
+// The fused map's packed candidates summed per transcript with no binning pass, for small
+// transcript sets (ntx <= TOT_SMALL_TX): workgroup (chunk c, range q) walks a contiguous stretch of
+// map waves' packed regions (16-B loads, ChainParams::cand_wtot words each) and adds
+// (1 << 40 | score) into u64 LDS bins for the transcripts of its range (TOT_RANGE_TX of them, so a
+// workgroup needs <= 32 KiB of LDS: beside a running map it starts as soon as one map workgroup
+// retires on a CU, where 80 KiB waited for three), then adds its non-empty bins into the batch's
+// packed sums tx_acc with coalesced atomics. The ranges of one chunk re-read it from the L2 (the
+// q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
+// k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
+constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096;
+__global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr) {
+    __shared__ unsigned long long s_tb[TOT_RANGE_TX];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    for (uint32_t i = t; i < p.ntx; i += WG) s_tb[i] = 0;
+    const uint32_t c = blockIdx.x / nr, q = blockIdx.x % nr;
+    const uint32_t lo = q * TOT_RANGE_TX, hi = min(p.ntx, lo + TOT_RANGE_TX);
+    for (uint32_t i = t; i < TOT_RANGE_TX; i += WG) s_tb[i] = 0;
     __syncthreads();
-    const uint32_t w0 = blockIdx.x * per, w1 = min(nwaves, w0 + per);
+    const uint32_t w0 = c * per, w1 = min(nwaves, w0 + per);
     for (uint32_t W = w0 + wv; W < w1; W += WG / 64) {  // one map wave's region per wave of this workgroup
         const uint32_t tot = p.cand_wtot[W];
         const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)W * 64 * CCAP);
-        for (uint32_t q = lane; q * 4 < tot; q += 64) {
-            const uint4 x = src[q];
+        for (uint32_t e = lane; e * 4 < tot; e += 64) {
+            const uint4 x = src[e];
             const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (q * 4 + i < tot)
-                    atomicAdd(&s_tb[xs[i] & 0x3FFFFFu], (1ull << 40) | (unsigned long long)(xs[i] >> 22));
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t tid = xs[i] & 0x3FFFFFu;
+                if (e * 4 + i < tot && tid - lo < hi - lo)
+                    atomicAdd(&s_tb[tid - lo], (1ull << 40) | (unsigned long long)(xs[i] >> 22));
+            }
         }
     }
     __syncthreads();
-    for (uint32_t i = t; i < p.ntx; i += WG) {
+    for (uint32_t i = t; i < hi - lo; i += WG) {
         const unsigned long long a = s_tb[i];
-        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[i]), a);
+        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[lo + i]), a);
     }
 }
 
@@ -3196,14 +3202,12 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     uint32_t* hdr = p.bin_hdr;
     const uint32_t* region = p.bin_region;
     if (nb > (uint32_t)WG) return -1;
-    if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: one pass)
+    if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: no binning)
         const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
-        const uint32_t per = std::max<uint32_t>(8, (nwaves + 127) / 128);
-        const size_t lds = (size_t)p.ntx * 8;
-        if (lds > 64 * 1024)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tot_small), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-        hipLaunchKernelGGL(k_tot_small, dim3((nwaves + per - 1) / per), dim3(WG), lds, st, p, nwaves, per);
+        const uint32_t nr = (p.ntx + TOT_RANGE_TX - 1) / TOT_RANGE_TX;
+        const uint32_t per = std::max<uint32_t>(16, (nwaves + 63) / 64);  // (<= 64 chunks)
+        const uint32_t nc = (nwaves + per - 1) / per;
+        hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(WG), 0, st, p, nwaves, per, nr);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     if (!binned) {

@@ -81,3 +81,47 @@ def test_cli_index_on_the_gpu(tmp_path):
     ks, names, seqs, tabs = skq.legacy_index_read(out)
     buf, offs = skq.pack_reads(seqs)
     same(tabs, skq.build_tables(buf, offs, [31, 25]))
+
+
+def test_chained_host_build_shared_between_concurrent_indexes():
+    """Indexes built at once from the same tables and sequences (the CLI's one thread per device)
+    share one host build of the chained entries: one reports the build's seconds, the other 0, and
+    both map a batch identically (the share was keyed on a per-call vector's
+    address, so it never happened)."""
+    import threading
+    tx = synth.transcriptome(200_000, seed=1)
+    tables = skq.build_tables(tx.seqs, tx.offs, [31], nthreads=16)
+    out, errs = [None, None], []
+    go = threading.Barrier(2)
+
+    def make(i):
+        try:
+            go.wait()
+            out[i] = skq.Index([31], tx.ntx, tables, seqs=(tx.seqs, tx.offs))
+        except Exception as ex:  # noqa: BLE001
+            errs.append(ex)
+
+    th = [threading.Thread(target=make, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    st = [ix.stats() for ix in out]
+    assert all(s["chained"] > 2 for s in st), st
+    secs = sorted(s["chain_build_s"] for s in st)
+    assert secs[0] == 0 and secs[1] > 0, st
+    bases, _, _ = synth.reads(tx, 20_000, 150, seed=9)
+    d = skq.DeviceBuffer.from_numpy(bases)
+    res = []
+    for ix in out:
+        s = skq.Session(ix, 20_000, 150)
+        s.map(d.ptr, None, 20_000, 150, fixed_len=150)
+        s.check()
+        e = s.export()
+        res.append((e["cand_offs"], e["cand_tid"], e["cand_score"], e["hashes"]))
+        s.free()
+        ix.free()
+    d.free()
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)
