@@ -1380,7 +1380,7 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
                       hipStream_t st, bool side) {
     hipEvent_t t0{};
     const bool totals = accumulate != 0;
-    const bool fork = side || (totals && p.slow_totals && p.n >= (1u << 19));
+    const bool fork = side || (totals && p.slow_totals && !p.cpack && p.n >= (1u << 19));
     hipStream_t tq = st;  // the stream of the totals
     if (fork) {
         if (int rc = ensure_side(s)) return rc;
@@ -1580,7 +1580,10 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     // then, for batches of 512k+ reads, the tail on the side stream in the other frame
     const bool slow_totals = accumulate && ix->ntx <= (1u << 22) && ix->nk <= (uint32_t)skq::NK_FAST && s->bin_nb > 0;
     const bool cpack = !accumulate || slow_totals;
-    bool side = cpack && n_reads >= (1u << 19);
+    // (4M+ reads: beside a 1-ms map the tail's kernels overlap; beside cfg2's 0.09-ms map of 1M reads
+    // they only queue behind its workgroups — 0.15 against 0.11 ms per step — so a small batch runs
+    // its tail on the launch stream, between the maps)
+    bool side = cpack && n_reads >= (1u << 22);
     if (side) {
         if (int rc = ensure_side(s)) return rc;
         if (!s->alt.ctrl && frame_alloc(s, s->alt, s->f.hcap_alloc)) {  // (no room: the tail stays on the launch stream)

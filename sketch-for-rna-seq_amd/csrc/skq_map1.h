@@ -1138,10 +1138,12 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
     MAP1_STAMP(4);
 }
 
-// (SKQ_MAP1_WPE: a development A/B of the waves per SIMD the compiler budgets registers for; TAB 4
-// takes 107-109 VGPRs, 4 waves, where the other kinds fit 5)
+// (SKQ_MAP1_WPE: the waves per SIMD the compiler budgets registers for. 5 (96 VGPRs): the multi-k
+// passes over chained tables otherwise take 99-108 VGPRs, 4 waves; at 5 they spill 4-20 VGPRs to
+// scratch and run 5 % faster at cfg5 (tools/abbench.py, profiles/r6_wpe5_ab.log); the one-k map
+// fits 5 unforced)
 #ifndef SKQ_MAP1_WPE
-#define SKQ_MAP1_WPE 1
+#define SKQ_MAP1_WPE 5
 #endif
 template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false, int MW = WG>
 __global__ __launch_bounds__(MW) __attribute__((amdgpu_waves_per_eu(SKQ_MAP1_WPE))) void k_map1(SketchParams p, ChainParams cp) {

@@ -465,15 +465,17 @@ def test_chain_sketches_entry_point(tx300):
         assert list(out["cand_score"][co[r]:co[r + 1]]) == list(sc[:c])
 
 
-@pytest.mark.parametrize("n", [1000, 600_000])
-def test_repeated_batches_accumulate_totals(tx300, n):
-    """Three different batches through one session, totals accumulated. n = 600k (>= 2^19 reads):
+@pytest.mark.parametrize("n", [1000, 600_000, 4_200_000])
+def test_repeated_batches_accumulate_totals(tx300, n, probe_mode):
+    """Three different batches through one session, totals accumulated. n = 4.2M (>= 2^22 reads):
     a fused map's tail (slow paths, totals binning) runs on the session's side stream and
     consecutive batches alternate between the session's two frames, the next map writing one while
     the previous tail still reads and writes the other. The totals are the three batches' sums, and
     the results read after a batch are that batch's own, read by read (per-read digests: status,
     retained-hash sets, candidate lists; tests/digest.py)."""
     import digest
+    if n > 1_000_000 and probe_mode != "chain":
+        pytest.skip("the side-stream frames once, over the default index kind")
     gi, oi = build([31], tx=tx300)
     s = skq.Session(gi, n, 150)
     tr = np.zeros(tx300.ntx, np.uint64)
@@ -526,6 +528,32 @@ def test_very_long_reads_and_large_postings():
         out = run_gpu(gi, reads, thr=th)
         ref = oi.map_batch(reads, thr=th)
         compare(out, ref, len(reads), 1)
+
+
+def test_multi_k_general_slow_paths(tx300, probe_mode):
+    """Multi-k batches whose slow reads reach the general paths behind k_slow_wave: reads longer
+    than the wave path's 512 windows (re-sketched by k_general_slow, the ovf3 list) and more than
+    255 retained hashes per k (a threshold near UINT32_MAX), mixed with ordinary reads of the same
+    waves, so the re-sketch of one read runs while other workgroups chain reads whose packed offsets
+    depend on it (run marks carry the region shares). Bit-exact per read and in the
+    totals."""
+    ks = [21, 25, 31]
+    gi, oi = build(ks, tx=tx300)
+    rng = random.Random(17)
+    reads = []
+    for i in range(700):
+        s = b"".join(tx300.seq(rng.randrange(tx300.ntx)) for _ in range(3))
+        L = rng.choice([150, 150, 150, 600, 900, 1500]) if i % 5 == 0 else 150
+        L = min(L, len(s))
+        p = rng.randint(0, len(s) - L)
+        reads.append(bytes(s[p:p + L]))
+    for th in (None, orc.threshold(0.6)):
+        out = run_gpu(gi, reads, thr=th)
+        ref = oi.map_batch(reads, thr=th)
+        compare(out, ref, len(reads), len(ks))
+        tr, ts = totals_from(ref, len(reads), tx300.ntx)
+        np.testing.assert_array_equal(out["totals"][0], tr)
+        np.testing.assert_array_equal(out["totals"][1], ts)
 
 
 @pytest.mark.parametrize("ks,read_len", [([21, 25, 31], 150), ([31, 31], 150), ([25, 31], 100), ([21, 31], 220)])
