@@ -1583,7 +1583,11 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     // (4M+ reads: beside a 1-ms map the tail's kernels overlap; beside cfg2's 0.09-ms map of 1M reads
     // they only queue behind its workgroups — 0.15 against 0.11 ms per step — so a small batch runs
     // its tail on the launch stream, between the maps)
-    bool side = cpack && n_reads >= (1u << 22);
+    static const uint64_t side_min = [] {  // (SKQ_SIDE_MIN, development: the batch size from which)
+        const char* e = dev_env("SKQ_SIDE_MIN");
+        return e ? std::strtoull(e, nullptr, 10) : (1ull << 22);
+    }();
+    bool side = cpack && n_reads >= side_min;
     if (side) {
         if (int rc = ensure_side(s)) return rc;
         if (!s->alt.ctrl && frame_alloc(s, s->alt, s->f.hcap_alloc)) {  // (no room: the tail stays on the launch stream)

@@ -1138,15 +1138,18 @@ __device__ __forceinline__ void map1_body(const SketchParams& p, const ChainPara
     MAP1_STAMP(4);
 }
 
-// (SKQ_MAP1_WPE: the waves per SIMD the compiler budgets registers for. 5 (96 VGPRs): the multi-k
-// passes over chained tables otherwise take 99-108 VGPRs, 4 waves; at 5 they spill 4-20 VGPRs to
-// scratch and run 5 % faster at cfg5 (tools/abbench.py, profiles/r6_wpe5_ab.log); the one-k map
-// fits 5 unforced)
+// (SKQ_MAP1_WPE / SKQ_PASS_WPE: the waves per SIMD the compiler budgets registers for, one-k map /
+// multi-k passes. 5 (96 VGPRs): the passes over chained tables otherwise take 99-108 VGPRs, 4 waves;
+// at 5 they spill 4-20 VGPRs to scratch and run 5 % faster at cfg5 (tools/abbench.py,
+// profiles/r6_wpe5_ab.log); the one-k map fits 5 unforced)
 #ifndef SKQ_MAP1_WPE
 #define SKQ_MAP1_WPE 5
 #endif
+#ifndef SKQ_PASS_WPE
+#define SKQ_PASS_WPE 5
+#endif
 template <int HCAP, int MB, int TAB, bool PASS = false, bool FINAL = false, int MW = WG>
-__global__ __launch_bounds__(MW) __attribute__((amdgpu_waves_per_eu(SKQ_MAP1_WPE))) void k_map1(SketchParams p, ChainParams cp) {
+__global__ __launch_bounds__(MW) __attribute__((amdgpu_waves_per_eu(PASS ? SKQ_PASS_WPE : SKQ_MAP1_WPE))) void k_map1(SketchParams p, ChainParams cp) {
     static_assert(PASS || !FINAL, "the final pass is a pass");
     map1_body<HCAP, MB, TAB, PASS, MW>(p, cp, PASS ? p.kslot : 0u, FINAL);
 }
