@@ -1394,8 +1394,8 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
     auto do_totals = [&]() -> int {
         if (!totals) return 0;
         record(s, 3, &t0, tq);
-        if (skq::launch_bin(p, binned(p), tq) ||
-            skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, tq))
+        const int rb = skq::launch_bin(p, binned(p), tq);  // (1: already in the running totals)
+        if (rb < 0 || (rb == 0 && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, tq)))
             return fail(-3, "totals launch failed");
         record_stop(s, 3, t0, tq);
         return 0;

@@ -276,7 +276,8 @@ int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t
 // per-transcript totals of the batch's final candidates into p.tx_acc (k_bin + k_bin_sum), then
 // launch_fold_totals adds them into p.tx_reads / p.tx_score with atomics (commuting with the slow
 // paths' direct adds)
-// (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs)
+// (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs). Returns 0, < 0 on a
+// failure, 1 when the totals went straight into p.tx_reads / p.tx_score (k_tot_small: no fold)
 int launch_bin(const ChainParams& p, int binned, void* stream);
 // whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)
 bool count_bins(const ChainParams& p);

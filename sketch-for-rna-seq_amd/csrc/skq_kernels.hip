@@ -2862,8 +2862,8 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
 // (1 << 40 | score) into u64 LDS bins for the transcripts of its range (TOT_RANGE_TX of them, so a
 // workgroup needs <= 32 KiB of LDS: beside a running map it starts as soon as one map workgroup
 // retires on a CU, where 80 KiB waited for three), then adds its non-empty bins into the batch's
-// packed sums tx_acc with coalesced atomics. The ranges of one chunk re-read it from the L2 (the
-// q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
+// running totals with coalesced atomics (no fold). The ranges of one chunk re-read it from the L2
+// (the q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
 // k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
 constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096;
 __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr) {
@@ -2874,24 +2874,49 @@ __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves
     for (uint32_t i = t; i < TOT_RANGE_TX; i += WG) s_tb[i] = 0;
     __syncthreads();
     const uint32_t w0 = c * per, w1 = min(nwaves, w0 + per);
-    for (uint32_t W = w0 + wv; W < w1; W += WG / 64) {  // one map wave's region per wave of this workgroup
-        const uint32_t tot = p.cand_wtot[W];
-        const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)W * 64 * CCAP);
-        for (uint32_t e = lane; e * 4 < tot; e += 64) {
-            const uint4 x = src[e];
-            const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+    // each wave takes RB map-wave regions at a time: their word counts in one load (lanes 0..RB-1),
+    // then every region's first 256 words (64 x 16 B) loaded together — a region holds 200 words at
+    // cfg2 — so a round is two memory round trips for RB regions, not two per region
+    constexpr uint32_t RB = 16;
+    auto add = [&](uint32_t x) {
+        const uint32_t tid = x & 0x3FFFFFu;
+        if (tid - lo < hi - lo) atomicAdd(&s_tb[tid - lo], (1ull << 40) | (unsigned long long)(x >> 22));
+    };
+    for (uint32_t Wb = w0 + wv * RB; Wb < w1; Wb += (WG / 64) * RB) {
+        const uint32_t mytot = lane < RB && Wb + lane < w1 ? p.cand_wtot[Wb + lane] : 0u;
+        uint4 x[RB];
+        uint32_t tot[RB];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t tid = xs[i] & 0x3FFFFFu;
-                if (e * 4 + i < tot && tid - lo < hi - lo)
-                    atomicAdd(&s_tb[tid - lo], (1ull << 40) | (unsigned long long)(xs[i] >> 22));
+        for (uint32_t u = 0; u < RB; ++u) {
+            tot[u] = (uint32_t)__builtin_amdgcn_readlane((int)mytot, (int)u);
+            const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)(Wb + u) * 64 * CCAP);
+            x[u] = lane * 4 < tot[u] ? src[lane] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < RB; ++u) {
+            const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (lane * 4 + i < tot[u]) add(xs[i]);
+            // (rare: a region past 256 words)
+            const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)(Wb + u) * 64 * CCAP);
+            for (uint32_t e = lane + 64; e * 4 < tot[u]; e += 64) {
+                const uint4 y = src[e];
+                const uint32_t ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (e * 4 + i < tot[u]) add(ys[i]);
             }
         }
     }
     __syncthreads();
+    // (straight into the running totals: no fold launch behind this one)
     for (uint32_t i = t; i < hi - lo; i += WG) {
         const unsigned long long a = s_tb[i];
-        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[lo + i]), a);
+        if (a) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[lo + i]), a >> 40);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[lo + i]), a & ((1ull << 40) - 1));
+        }
     }
 }
 
@@ -3205,10 +3230,10 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: no binning)
         const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
         const uint32_t nr = (p.ntx + TOT_RANGE_TX - 1) / TOT_RANGE_TX;
-        const uint32_t per = std::max<uint32_t>(16, (nwaves + 63) / 64);  // (<= 64 chunks)
+        const uint32_t per = std::max<uint32_t>(64, (nwaves + 63) / 64);  // (<= 64 chunks)
         const uint32_t nc = (nwaves + per - 1) / per;
         hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(WG), 0, st, p, nwaves, per, nr);
-        return hipGetLastError() == hipSuccess ? 0 : -2;
+        return hipGetLastError() == hipSuccess ? 1 : -2;  // (1: the totals are in, no fold)
     }
     if (!binned) {
         if (p.cpack && nb)  // (the fused map's packed candidates)
