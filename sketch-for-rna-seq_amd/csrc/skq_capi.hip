@@ -125,7 +125,12 @@ struct Frame {
     uint32_t* cand_wtot = nullptr;  // per wave of 64 reads: its packed candidate words (k_bin_packed)
     uint32_t* cand_ext = nullptr;
     uint64_t* scratch = nullptr;
+    // control words: two halves of C_WORDS; ctrl is the current batch's. A small fused batch's tail
+    // (on the launch stream) zeroes the other half on its way (k_general_slow) and the next such
+    // batch takes it, so no reset runs between the two maps; every other path resets ctrl itself
     uint32_t* ctrl = nullptr;
+    uint32_t* ctrl_mem = nullptr;
+    bool other_zeroed = false;
     uint32_t* ktab = nullptr;    // multi-k map by passes: per-k count tables (allocated on first use)
     uint8_t* kcnt = nullptr;
     uint32_t* stash = nullptr;   // multi-k map by passes: the first pass's staged bases (SketchParams::stash)
@@ -1180,9 +1185,10 @@ static int frame_alloc(skq_session* s, Frame& fr, uint32_t hcap) {
         (rc = dev_alloc(&fr.ovf4, s->ovf_cap)) || (rc = dev_alloc(&fr.cand_cnt, R)) || (rc = dev_alloc(&fr.pflag, R)) ||
         (rc = dev_alloc(&fr.cand_tid, R * skq::CCAP)) || (rc = dev_alloc(&fr.cand_wtot, (R + 63) / 64)) ||
         (rc = dev_alloc(&fr.cand_score, R * skq::CCAP)) || (rc = dev_alloc(&fr.cand_ext, 2 * s->cand_ext_cap)) ||
-        (rc = dev_alloc(&fr.scratch, s->scratch_cap)) || (rc = dev_alloc(&fr.ctrl, skq::C_WORDS)))
+        (rc = dev_alloc(&fr.scratch, s->scratch_cap)) || (rc = dev_alloc(&fr.ctrl_mem, 2 * skq::C_WORDS)))
         return rc;
-    if (hipMemset(fr.ctrl, 0, skq::C_WORDS * 4) != hipSuccess) return fail(-3, "memset failed");
+    fr.ctrl = fr.ctrl_mem;
+    if (hipMemset(fr.ctrl_mem, 0, 2 * skq::C_WORDS * 4) != hipSuccess) return fail(-3, "memset failed");
     if (dev_alloc(&fr.hashes, R * nk * (uint64_t)hcap) || dev_alloc(&fr.lofs, R * nk * (uint64_t)hcap)) return -3;
     fr.hcap_alloc = hcap;
     return 0;
@@ -1205,7 +1211,7 @@ static void frame_free(Frame& fr) {
     dev_free(fr.cand_wtot);
     dev_free(fr.cand_ext);
     dev_free(fr.scratch);
-    dev_free(fr.ctrl);
+    dev_free(fr.ctrl_mem);
     dev_free(fr.ktab);
     dev_free(fr.kcnt);
     dev_free(fr.stash);
@@ -1393,11 +1399,13 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         if (int rc = wait_side(s, st)) return rc;  // (tx_acc and the bins: an earlier batch's totals may run)
     auto do_totals = [&]() -> int {
         if (!totals) return 0;
-        record(s, 3, &t0, tq);
-        const int rb = skq::launch_bin(p, binned(p), tq);  // (1: already in the running totals)
+        // (timed on the side stream only: on the launch stream a pair of timing events is ~5 us of
+        // the step between two maps)
+        if (fork) record(s, 3, &t0, tq);
+        const int rb = skq::launch_bin(p, binned(p), tq, fork);  // (1: already in the running totals)
         if (rb < 0 || (rb == 0 && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, tq)))
             return fail(-3, "totals launch failed");
-        record_stop(s, 3, t0, tq);
+        if (fork) record_stop(s, 3, t0, tq);
         return 0;
     };
     // (with the count kernel's bins, a two-kernel batch's totals go first: its slow paths add their
@@ -1416,8 +1424,11 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         p2.ovf2 = s->f.ovf4;
         p2.ovf_word = skq::C_OVF4;
         // (32 workgroups: the general reads are rare — none at cfg2, 3, 5 — and each of its workgroups
-        // needs 33 KB of LDS, which beside a running map only frees up as map workgroups retire)
-        if (skq::launch_general_slow(sp2, p2, sq, 32)) return fail(-3, "general slow-path launch failed");
+        // needs 33 KB of LDS, which beside a running map only frees up as map workgroups retire. On
+        // the launch stream it also zeroes the frame's other control words for the next batch.)
+        uint32_t* zn = side ? nullptr : (s->f.ctrl == s->f.ctrl_mem ? s->f.ctrl_mem + skq::C_WORDS : s->f.ctrl_mem);
+        if (skq::launch_general_slow(sp2, p2, sq, 32, zn)) return fail(-3, "general slow-path launch failed");
+        if (zn) s->f.other_zeroed = true;
     } else {
         if (sp && skq::launch_sketch_slow(*sp, sq)) return fail(-3, "sketch slow-path launch failed");
         if (skq::launch_chain_slow(p, sq)) return fail(-3, "chain slow-path launch failed");
@@ -1617,7 +1628,12 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         if (!s->zeroed[s->fid]) HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
     } else {
         if (int rc = wait_side(s, st)) return rc;
-        HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
+        if (s->f.other_zeroed) {  // (the previous small batch's tail zeroed the other half)
+            s->f.ctrl = s->f.ctrl == s->f.ctrl_mem ? s->f.ctrl_mem + skq::C_WORDS : s->f.ctrl_mem;
+            s->f.other_zeroed = false;
+        } else {
+            HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
+        }
     }
     s->zeroed[s->fid] = false;
     s->tail_side[s->fid] = side;

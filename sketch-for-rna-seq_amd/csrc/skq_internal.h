@@ -268,7 +268,9 @@ int launch_count(const ChainParams& p, void* stream);  // k_count<nk>
 int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid = 2048);
 // k_sketch_slow then k_chain_slow per read in one launch, over the chain list p.ovf2 (the fused
 // map's tail behind k_slow_wave: the reads still flagged ST_SLOW1 are re-sketched first)
-int launch_general_slow(const SketchParams& sp, const ChainParams& p, void* stream, unsigned grid = 256);
+// (zero_next: control words zeroed on the way, for the next batch; null: none)
+int launch_general_slow(const SketchParams& sp, const ChainParams& p, void* stream, unsigned grid = 256,
+                        uint32_t* zero_next = nullptr);
 // the wave slow path behind k_map1 and its passes (wide or compact tables, <= 4 k slots; -4 otherwise):
 // the listed reads it cannot take go on to ovf3 (C_OVF3) and ovf4 (C_OVF4)
 int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf3, uint32_t* ovf4, void* stream);
@@ -278,7 +280,9 @@ int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t
 // paths' direct adds)
 // (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs). Returns 0, < 0 on a
 // failure, 1 when the totals went straight into p.tx_reads / p.tx_score (k_tot_small: no fold)
-int launch_bin(const ChainParams& p, int binned, void* stream);
+// (beside_map: on the side stream, beside the next batch's map: kernels sized to start in the LDS a
+// retiring map workgroup frees)
+int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map);
 // whether launch_count's kernel bins the totals itself (k_count3 with p.bin_nb > 0)
 bool count_bins(const ChainParams& p);
 int launch_dir_scatter(uint32_t* dir, const uint32_t* keys, const uint32_t* vals, uint64_t n, void* stream);

@@ -2240,7 +2240,10 @@ __global__ __launch_bounds__(WG) void k_chain_slow(ChainParams p) {
 // k_chain_slow's work in their order; a read's chain reads only its own sets, and the packed
 // offsets of its wave's other reads come from shares that a concurrent re-sketch keeps
 // (hash_list<true>). Saves the second launch of the batch's tail.
-__global__ __launch_bounds__(WG) void k_general_slow(SketchParams sp, ChainParams p) {
+// zero_next (or null): the control words of the frame's other half, zeroed for the next batch here,
+// so the launch stream needs no reset between two maps (skq_capi.hip Frame::ctrl_mem)
+__global__ __launch_bounds__(WG) void k_general_slow(SketchParams sp, ChainParams p, uint32_t* zero_next) {
+    if (zero_next && blockIdx.x == 0 && threadIdx.x < C_WORDS) zero_next[threadIdx.x] = 0;
     // one LDS region for both steps (each ends / starts at a barrier): a workgroup needs no more
     // than k_chain_slow's, so the launch's workgroups still fit beside the side stream's (with
     // both regions apart, 50 KB each, it waited for k_bin_packed's workgroups: 71 µs at cfg3)
@@ -2859,19 +2862,20 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
 // The fused map's packed candidates summed per transcript with no binning pass, for small
 // transcript sets (ntx <= TOT_SMALL_TX): workgroup (chunk c, range q) walks a contiguous stretch of
 // map waves' packed regions (16-B loads, ChainParams::cand_wtot words each) and adds
-// (1 << 40 | score) into u64 LDS bins for the transcripts of its range (TOT_RANGE_TX of them, so a
-// workgroup needs <= 32 KiB of LDS: beside a running map it starts as soon as one map workgroup
-// retires on a CU, where 80 KiB waited for three), then adds its non-empty bins into the batch's
+// (1 << 40 | score) into u64 LDS bins for the transcripts of its range: all of them when it runs
+// alone on the chip (the launch stream, between two maps), TOT_RANGE_TX beside a running map (32 KiB
+// of LDS: it then starts as soon as one map workgroup retires on a CU, where 80 KiB waited for
+// three), then adds its non-empty bins into the
 // running totals with coalesced atomics (no fold). The ranges of one chunk re-read it from the L2
 // (the q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
 // k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
 constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096;
-__global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr) {
-    __shared__ unsigned long long s_tb[TOT_RANGE_TX];
+__global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr, uint32_t range) {
+    extern __shared__ unsigned long long s_tb[];  // (range bins)
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t c = blockIdx.x / nr, q = blockIdx.x % nr;
-    const uint32_t lo = q * TOT_RANGE_TX, hi = min(p.ntx, lo + TOT_RANGE_TX);
-    for (uint32_t i = t; i < TOT_RANGE_TX; i += WG) s_tb[i] = 0;
+    const uint32_t lo = q * range, hi = min(p.ntx, lo + range);
+    for (uint32_t i = t; i < range; i += WG) s_tb[i] = 0;
     __syncthreads();
     const uint32_t w0 = c * per, w1 = min(nwaves, w0 + per);
     // each wave takes RB map-wave regions at a time: their word counts in one load (lanes 0..RB-1),
@@ -3132,7 +3136,8 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // a 64-lane workgroup per listed read, grid-stride (the list length is on the device); 16
     // per CU fit (LDS ~9 KB, < 100 VGPRs)
-    const dim3 grid(SW_GRID), blk(64);
+    // (a small batch's few slow reads need fewer workgroups: an empty list still dispatches all)
+    const dim3 grid((unsigned)std::min<uint64_t>(SW_GRID, std::max<uint64_t>(256, cp.n / 2048))), blk(64);
     const bool cmp = cp.wide == 3;
     switch (cp.nk) {
     case 1:
@@ -3162,9 +3167,9 @@ int launch_chain_slow(const ChainParams& p, void* stream, unsigned grid) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_general_slow(const SketchParams& sp, const ChainParams& p, void* stream, unsigned grid) {
+int launch_general_slow(const SketchParams& sp, const ChainParams& p, void* stream, unsigned grid, uint32_t* zero_next) {
     if (p.n == 0) return 0;
-    hipLaunchKernelGGL(k_general_slow, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), sp, p);
+    hipLaunchKernelGGL(k_general_slow, dim3(grid), dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), sp, p, zero_next);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -3219,7 +3224,7 @@ int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_bin(const ChainParams& p, int binned, void* stream) {
+int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) {
     if (p.n == 0) return 0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const uint32_t nW = (uint32_t)((p.n + WG - 1) / WG);
@@ -3229,10 +3234,15 @@ int launch_bin(const ChainParams& p, int binned, void* stream) {
     if (nb > (uint32_t)WG) return -1;
     if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: no binning)
         const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
-        const uint32_t nr = (p.ntx + TOT_RANGE_TX - 1) / TOT_RANGE_TX;
-        const uint32_t per = std::max<uint32_t>(64, (nwaves + 63) / 64);  // (<= 64 chunks)
+        const uint32_t range = beside_map ? TOT_RANGE_TX : p.ntx;
+        const uint32_t nr = (p.ntx + range - 1) / range;
+        const uint32_t per = std::max<uint32_t>(64, (nwaves + 127) / 128);  // (<= 128 chunks)
         const uint32_t nc = (nwaves + per - 1) / per;
-        hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(WG), 0, st, p, nwaves, per, nr);
+        const size_t lds = (size_t)range * 8;
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tot_small), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+        hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(WG), lds, st, p, nwaves, per, nr, range);
         return hipGetLastError() == hipSuccess ? 1 : -2;  // (1: the totals are in, no fold)
     }
     if (!binned) {
