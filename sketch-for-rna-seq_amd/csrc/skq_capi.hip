@@ -162,7 +162,11 @@ struct skq_session {
     uint32_t bin_bits = 13, bin_nb = 0;
     uint32_t* bin_hdr = nullptr;
     uint32_t* bin_region = nullptr;
-    uint64_t* tx_acc = nullptr;  // a batch's packed sums (k_bin_sum), folded into tx_reads / tx_score
+    // the batches' packed sums (reads << 40 | score per transcript: k_bin_sum, k_tot_small), folded
+    // into tx_reads / tx_score (k_fold_totals) when they are read, or before the reads they hold
+    // could pass 2^24 (acc_reads: the reads of the batches added since the last fold)
+    uint64_t* tx_acc = nullptr;
+    uint64_t acc_reads = 0;
     uint64_t* tx_reads = nullptr;
     uint64_t* tx_score = nullptr;
     // explicit-sketch chaining (skq_chain_sketches) keeps its inputs' layout for export
@@ -892,6 +896,16 @@ static int sync_side(skq_session* s) {
     return 0;
 }
 
+// the packed sums into the running totals, on st, behind every batch's totals (the readers of
+// tx_reads / tx_score call this first)
+static int fold_totals(skq_session* s, hipStream_t st) {
+    if (!s->acc_reads) return 0;
+    if (int rc = wait_side(s, st)) return rc;
+    if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, st)) return fail(-3, "fold failed");
+    s->acc_reads = 0;
+    return 0;
+}
+
 static int ensure_side(skq_session* s) {
     if (s->side) return 0;
     HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
@@ -1402,9 +1416,16 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
         // (timed on the side stream only: on the launch stream a pair of timing events is ~5 us of
         // the step between two maps)
         if (fork) record(s, 3, &t0, tq);
-        const int rb = skq::launch_bin(p, binned(p), tq, fork);  // (1: already in the running totals)
-        if (rb < 0 || (rb == 0 && skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, tq)))
-            return fail(-3, "totals launch failed");
+        // the packed sums fold when this batch could carry a transcript's reads past 2^24 (every
+        // earlier writer of tx_acc is ahead of tq: the side stream runs tails in order, and a
+        // launch-stream tail waited for it above)
+        if (s->acc_reads + p.n > skq::MAX_BATCH) {
+            if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, tq)) return fail(-3, "fold failed");
+            s->acc_reads = 0;
+        }
+        const int rb = skq::launch_bin(p, binned(p), tq, fork);
+        if (rb < 0) return fail(-3, "totals launch failed");
+        s->acc_reads += p.n;
         if (fork) record_stop(s, 3, t0, tq);
         return 0;
     };
@@ -1750,8 +1771,13 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
 
 int skq_session_results(skq_session* s, skq_results* o) {
     if (!s || !o) return fail(-1, "null argument");
-    {  // the batch's tail and the totals may still run on the side stream
+    {  // the batch's tail and the totals may still run on the side stream; the packed sums fold
         DeviceGuard g(s->idx->device);
+        if (s->acc_reads) {
+            hipStream_t fs = s->side ? s->side : nullptr;
+            if (int rc = fold_totals(s, fs)) return rc;
+            HIP_TRY(hipStreamSynchronize(fs));
+        }
         if (int rc = sync_side(s)) return rc;
     }
     o->n_reads = s->n_reads;
@@ -1800,6 +1826,7 @@ int skq_session_reset_totals(skq_session* s, void* stream) {
     if (int rc = wait_side(s, st)) return rc;
     HIP_TRY(hipMemsetAsync(s->tx_reads, 0, s->idx->ntx * 8ull, st));
     HIP_TRY(hipMemsetAsync(s->tx_acc, 0, s->idx->ntx * 8ull, st));
+    s->acc_reads = 0;
     HIP_TRY(hipMemsetAsync(s->tx_score, 0, s->idx->ntx * 8ull, st));
     return 0;
 }
@@ -1955,6 +1982,7 @@ int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, i
     const size_t bytes = s->idx->ntx * 8ull;
     const hipMemcpyKind kind = to_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     if (int rc = wait_side(s, st)) return rc;
+    if (int rc = fold_totals(s, st)) return rc;
     if (tx_reads) HIP_TRY(hipMemcpyAsync(tx_reads, s->tx_reads, bytes, kind, st));
     if (tx_score) HIP_TRY(hipMemcpyAsync(tx_score, s->tx_score, bytes, kind, st));
     if (!to_device) HIP_TRY(hipStreamSynchronize(st));

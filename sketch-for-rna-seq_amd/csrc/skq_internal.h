@@ -279,7 +279,7 @@ int launch_fold_totals(uint64_t* acc, uint64_t* reads, uint64_t* score, uint32_t
 // launch_fold_totals adds them into p.tx_reads / p.tx_score with atomics (commuting with the slow
 // paths' direct adds)
 // (binned = 1: the count kernel already wrote the bins; only k_bin_sum runs). Returns 0, < 0 on a
-// failure, 1 when the totals went straight into p.tx_reads / p.tx_score (k_tot_small: no fold)
+// failure. The sums land in p.tx_acc, packed (reads << 40 | score): k_fold_totals unpacks them
 // (beside_map: on the side stream, beside the next batch's map: kernels sized to start in the LDS a
 // retiring map workgroup frees)
 int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map);

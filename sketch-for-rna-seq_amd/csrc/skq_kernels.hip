@@ -2866,8 +2866,8 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
 // alone on the chip (the launch stream, between two maps), TOT_RANGE_TX beside a running map (32 KiB
 // of LDS: it then starts as soon as one map workgroup retires on a CU, where 80 KiB waited for
 // three), then adds its non-empty bins into the
-// running totals with coalesced atomics (no fold). The ranges of one chunk re-read it from the L2
-// (the q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
+// packed sums tx_acc with coalesced atomics. The ranges of one chunk re-read it from the L2 (the
+// q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
 // k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
 constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096;
 __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr, uint32_t range) {
@@ -2914,13 +2914,9 @@ __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves
         }
     }
     __syncthreads();
-    // (straight into the running totals: no fold launch behind this one)
     for (uint32_t i = t; i < hi - lo; i += WG) {
         const unsigned long long a = s_tb[i];
-        if (a) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[lo + i]), a >> 40);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[lo + i]), a & ((1ull << 40) - 1));
-        }
+        if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[lo + i]), a);
     }
 }
 
@@ -3236,14 +3232,14 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
         const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
         const uint32_t range = beside_map ? TOT_RANGE_TX : p.ntx;
         const uint32_t nr = (p.ntx + range - 1) / range;
-        const uint32_t per = std::max<uint32_t>(64, (nwaves + 127) / 128);  // (<= 128 chunks)
+        const uint32_t per = std::max<uint32_t>(64, (nwaves + 63) / 64);  // (<= 64 chunks)
         const uint32_t nc = (nwaves + per - 1) / per;
         const size_t lds = (size_t)range * 8;
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tot_small), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
         hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(WG), lds, st, p, nwaves, per, nr, range);
-        return hipGetLastError() == hipSuccess ? 1 : -2;  // (1: the totals are in, no fold)
+        return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     if (!binned) {
         if (p.cpack && nb)  // (the fused map's packed candidates)
