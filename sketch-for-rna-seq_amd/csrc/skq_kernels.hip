@@ -2862,10 +2862,9 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
 // The fused map's packed candidates summed per transcript with no binning pass, for small
 // transcript sets (ntx <= TOT_SMALL_TX): workgroup (chunk c, range q) walks a contiguous stretch of
 // map waves' packed regions (16-B loads, ChainParams::cand_wtot words each) and adds
-// (1 << 40 | score) into u64 LDS bins for the transcripts of its range: all of them when it runs
-// alone on the chip (the launch stream, between two maps), TOT_RANGE_TX beside a running map (32 KiB
-// of LDS: it then starts as soon as one map workgroup retires on a CU, where 80 KiB waited for
-// three), then adds its non-empty bins into the
+// (1 << 40 | score) into u64 LDS bins for the transcripts of its range (2560 between two maps;
+// TOT_RANGE_TX beside a running map: 32 KiB of LDS, so it starts as soon as one map workgroup
+// retires on a CU, where 80 KiB waited for three), then adds its non-empty bins into the
 // packed sums tx_acc with coalesced atomics. The ranges of one chunk re-read it from the L2 (the
 // q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
 // k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
@@ -3230,7 +3229,10 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
     if (nb > (uint32_t)WG) return -1;
     if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: no binning)
         const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
-        const uint32_t range = beside_map ? TOT_RANGE_TX : p.ntx;
+        // (ranges of <= 2560 ids between maps: a workgroup's flush is one 8-B atomic per bin, and a
+        // CU issues such wave-instructions only every ~50 ns (MI355X_MICROARCH.md, global atomics),
+        // so 64 workgroups flushing 10k bins each took 21 us where 256 flushing 2.5k take ~4)
+        const uint32_t range = beside_map ? TOT_RANGE_TX : std::min<uint32_t>(p.ntx, 2560);
         const uint32_t nr = (p.ntx + range - 1) / range;
         const uint32_t per = std::max<uint32_t>(64, (nwaves + 63) / 64);  // (<= 64 chunks)
         const uint32_t nc = (nwaves + per - 1) / per;
