@@ -2870,47 +2870,65 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
 // k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
 constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096;
 __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr, uint32_t range) {
-    extern __shared__ unsigned long long s_tb[];  // (range bins)
+    extern __shared__ unsigned long long s_tb[];  // (range bins, then the chunk's region word counts)
+    uint32_t* s_tot = reinterpret_cast<uint32_t*>(s_tb + range);
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t c = blockIdx.x / nr, q = blockIdx.x % nr;
     const uint32_t lo = q * range, hi = min(p.ntx, lo + range);
-    for (uint32_t i = t; i < range; i += WG) s_tb[i] = 0;
-    __syncthreads();
     const uint32_t w0 = c * per, w1 = min(nwaves, w0 + per);
-    // each wave takes RB map-wave regions at a time: their word counts in one load (lanes 0..RB-1),
-    // then every region's first 256 words (64 x 16 B) loaded together — a region holds 200 words at
-    // cfg2 — so a round is two memory round trips for RB regions, not two per region
-    constexpr uint32_t RB = 16;
+    for (uint32_t i = t; i < range; i += WG) s_tb[i] = 0;
+    for (uint32_t i = t; i < w1 - w0; i += WG) s_tot[i] = p.cand_wtot[w0 + i];  // (every count in one round trip)
+    __syncthreads();
+    // each wave takes RB map-wave regions a round, their first 256 words (64 x 16 B; a region holds
+    // ~200 words at cfg2) loaded together, the next round's loads issued before this round's adds:
+    // one exposed memory round trip per workgroup rather than two per region
+    constexpr uint32_t RB = 8;
     auto add = [&](uint32_t x) {
         const uint32_t tid = x & 0x3FFFFFu;
         if (tid - lo < hi - lo) atomicAdd(&s_tb[tid - lo], (1ull << 40) | (unsigned long long)(x >> 22));
     };
-    for (uint32_t Wb = w0 + wv * RB; Wb < w1; Wb += (WG / 64) * RB) {
-        const uint32_t mytot = lane < RB && Wb + lane < w1 ? p.cand_wtot[Wb + lane] : 0u;
-        uint4 x[RB];
-        uint32_t tot[RB];
+    auto issue = [&](uint32_t Wb, uint4 (&x)[RB]) {
 #pragma unroll
         for (uint32_t u = 0; u < RB; ++u) {
-            tot[u] = (uint32_t)__builtin_amdgcn_readlane((int)mytot, (int)u);
-            const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)(Wb + u) * 64 * CCAP);
-            x[u] = lane * 4 < tot[u] ? src[lane] : make_uint4(0, 0, 0, 0);
+            const uint32_t W = Wb + u;
+            const uint32_t tot = W < w1 ? s_tot[W - w0] : 0u;
+            const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)W * 64 * CCAP);
+            x[u] = lane * 4 < tot ? src[lane] : make_uint4(0, 0, 0, 0);
         }
+    };
+    auto consume = [&](uint32_t Wb, const uint4 (&x)[RB]) {
 #pragma unroll
         for (uint32_t u = 0; u < RB; ++u) {
+            const uint32_t W = Wb + u;
+            const uint32_t tot = W < w1 ? s_tot[W - w0] : 0u;
             const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                if (lane * 4 + i < tot[u]) add(xs[i]);
-            // (rare: a region past 256 words)
-            const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)(Wb + u) * 64 * CCAP);
-            for (uint32_t e = lane + 64; e * 4 < tot[u]; e += 64) {
+                if (lane * 4 + i < tot) add(xs[i]);
+            const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)W * 64 * CCAP);
+            for (uint32_t e = lane + 64; e * 4 < tot; e += 64) {  // (rare: a region past 256 words)
                 const uint4 y = src[e];
                 const uint32_t ys[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    if (e * 4 + i < tot[u]) add(ys[i]);
+                    if (e * 4 + i < tot) add(ys[i]);
             }
         }
+    };
+    constexpr uint32_t STEP = (WG / 64) * RB;
+    uint32_t Wb = w0 + wv * RB;
+    uint4 xa[RB], xb[RB];
+    if (Wb < w1) issue(Wb, xa);
+    while (Wb < w1) {
+        const uint32_t Wn = Wb + STEP;
+        if (Wn < w1) issue(Wn, xb);
+        consume(Wb, xa);
+        Wb = Wn;
+        if (Wb >= w1) break;
+        const uint32_t Wm = Wb + STEP;
+        if (Wm < w1) issue(Wm, xa);
+        consume(Wb, xb);
+        Wb = Wm;
     }
     __syncthreads();
     for (uint32_t i = t; i < hi - lo; i += WG) {
@@ -3234,9 +3252,9 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
         // so 64 workgroups flushing 10k bins each took 21 us where 256 flushing 2.5k take ~4)
         const uint32_t range = beside_map ? TOT_RANGE_TX : std::min<uint32_t>(p.ntx, 2560);
         const uint32_t nr = (p.ntx + range - 1) / range;
-        const uint32_t per = std::max<uint32_t>(64, (nwaves + 63) / 64);  // (<= 64 chunks)
+        const uint32_t per = std::min<uint32_t>(1024, std::max<uint32_t>(64, (nwaves + 63) / 64));  // (<= 64 chunks)
         const uint32_t nc = (nwaves + per - 1) / per;
-        const size_t lds = (size_t)range * 8;
+        const size_t lds = (size_t)range * 8 + (size_t)per * 4;
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tot_small), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
