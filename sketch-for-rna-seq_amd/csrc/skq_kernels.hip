@@ -3250,9 +3250,16 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
         // (ranges of <= 2560 ids between maps: a workgroup's flush is one 8-B atomic per bin, and a
         // CU issues such wave-instructions only every ~50 ns (MI355X_MICROARCH.md, global atomics),
         // so 64 workgroups flushing 10k bins each took 21 us where 256 flushing 2.5k take ~4)
-        const uint32_t range = beside_map ? TOT_RANGE_TX : std::min<uint32_t>(p.ntx, 2560);
+        uint32_t range = beside_map ? TOT_RANGE_TX : std::min<uint32_t>(p.ntx, 2560);
+        uint32_t chunks = 64;
+        if (const char* e = std::getenv("SKQ_DEV")) {  // (development sweep: SKQ_TOT_RANGE, SKQ_TOT_CHUNKS)
+            if (std::atoi(e) == 1) {
+                if (const char* r = std::getenv("SKQ_TOT_RANGE")) range = std::max(256, std::atoi(r));
+                if (const char* r = std::getenv("SKQ_TOT_CHUNKS")) chunks = std::max(1, std::atoi(r));
+            }
+        }
         const uint32_t nr = (p.ntx + range - 1) / range;
-        const uint32_t per = std::min<uint32_t>(1024, std::max<uint32_t>(64, (nwaves + 63) / 64));  // (<= 64 chunks)
+        const uint32_t per = std::min<uint32_t>(1024, std::max<uint32_t>(16, (nwaves + chunks - 1) / chunks));
         const uint32_t nc = (nwaves + per - 1) / per;
         const size_t lds = (size_t)range * 8 + (size_t)per * 4;
         if (lds > 64 * 1024)
