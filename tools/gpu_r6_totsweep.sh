@@ -6,8 +6,9 @@ o=gpurun_out/$1
 mkdir -p $o
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export SKQ_DEV=1
-for v in "64 10000" "16 10000" "32 10000" "64 2560" "256 2560" "128 5000" "256 10000"; do
-  set -- $v
+VARIANTS=${VARIANTS:-"64_10000 16_10000 32_10000 64_2560 128_5000"}
+for v in $VARIANTS; do
+  set -- ${v/_/ }
   export SKQ_TOT_CHUNKS=$1 SKQ_TOT_RANGE=$2
   timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d $o/tr_$1_$2 -o run -- python3 bench.py --config cfg2 --no-cpu-baseline --no-end-to-end --steps 10 --warmup 2 --cpu-reads 20000 > $o/b_$1_$2.json 2> $o/b_$1_$2.err || { echo "run $v failed"; tail -20 $o/b_$1_$2.err; exit 1; }
   python3 - $o/tr_$1_$2/run_kernel_trace.csv "$v" <<'PY'
