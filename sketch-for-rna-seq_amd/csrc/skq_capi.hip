@@ -19,6 +19,10 @@
 
 #include "skq_internal.h"
 
+namespace skq {
+thread_local LaunchEvents g_launch_ev;
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -258,17 +262,36 @@ double pass_sigmas() {
     return v;
 }
 
+// a timing scope: kinds 0-2 (the launch stream's map, sketch, probe, count) bind their events to
+// the scope's dispatches (skq::launch_timed); kind 3 (the side stream's tail) records marker events
 void record(skq_session* s, int kind, hipEvent_t* start, hipStream_t st) {
     if (!s->timing) return;
     (void)hipEventCreate(start);
-    (void)hipEventRecord(*start, st);
+    if (kind == 3) {
+        (void)hipEventRecord(*start, st);
+        return;
+    }
+    hipEvent_t stop;
+    (void)hipEventCreate(&stop);
+    skq::g_launch_ev = {*start, stop};
 }
 
 void record_stop(skq_session* s, int kind, hipEvent_t start, hipStream_t st) {
     if (!s->timing) return;
     hipEvent_t stop;
-    (void)hipEventCreate(&stop);
-    (void)hipEventRecord(stop, st);
+    if (kind == 3) {
+        (void)hipEventCreate(&stop);
+        (void)hipEventRecord(stop, st);
+    } else {
+        stop = static_cast<hipEvent_t>(skq::g_launch_ev.stop);
+        const bool launched = skq::g_launch_ev.start == nullptr;  // (consumed by a first launch)
+        skq::g_launch_ev = {};
+        if (!launched) {
+            (void)hipEventDestroy(start);
+            (void)hipEventDestroy(stop);
+            return;
+        }
+    }
     s->timed.push_back({kind, start, stop});
 }
 

@@ -10,6 +10,17 @@ struct skq_tables;
 
 namespace skq {
 
+// kernel timing without marker packets: while a scope's events are set (skq_capi.hip record()),
+// the timed launchers (launch_timed, skq_kernels.hip) bind them to the dispatches themselves —
+// hipExtLaunchKernel: the start event to the first launch's start, the stop event to the last
+// launch's end — so nothing is queued between a batch's kernels (a hipEventRecord pair around the
+// map was ~6 us of each step, profiles/r6_tail_traces.log)
+struct LaunchEvents {
+    void* start = nullptr;
+    void* stop = nullptr;
+};
+extern thread_local LaunchEvents g_launch_ev;
+
 constexpr int WG = 256;            // threads per workgroup for both kernels (4 waves)
 constexpr int LFAST = 256;         // reads longer than this take the slow path
 constexpr int DCAP = 16;           // distinct transcripts per read on the fast chain path

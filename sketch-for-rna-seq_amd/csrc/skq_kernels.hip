@@ -19,6 +19,7 @@
 //                  transcripts, > 4 k slots). One workgroup per listed read, sorting in LDS; they walk device-side
 //                  work lists with a fixed grid, so no host round trip is needed.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -57,6 +58,15 @@
 #endif
 
 namespace skq {
+
+// a launch of the timed kernels (the map, the sketch, probe and count): the scope's events bound
+// to the dispatch (skq_internal.h LaunchEvents), the start one only to the scope's first launch
+template <typename K, typename... A>
+inline void launch_timed(K kern, dim3 grid, dim3 blk, size_t lds, hipStream_t st, A... args) {
+    const hipEvent_t a = static_cast<hipEvent_t>(g_launch_ev.start), b = static_cast<hipEvent_t>(g_launch_ev.stop);
+    g_launch_ev.start = nullptr;
+    hipExtLaunchKernelGGL(kern, grid, blk, (uint32_t)lds, st, a, b, 0u, args...);
+}
 
 // ---------------------------------------------------------------------------------------------
 // small helpers
@@ -2868,16 +2878,16 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
 // packed sums tx_acc with coalesced atomics. The ranges of one chunk re-read it from the L2 (the
 // q-th range of chunk c is workgroup c * R + q). For cfg2 (10k transcripts) this replaces
 // k_bin_packed + k_bin_sum_g. Slow reads have no share of their wave's region and add their own.
-constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096;
-__global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr, uint32_t range) {
+constexpr uint32_t TOT_SMALL_TX = 16384, TOT_RANGE_TX = 4096, TOT_WG = 1024;
+__global__ __launch_bounds__(TOT_WG) void k_tot_small(ChainParams p, uint32_t nwaves, uint32_t per, uint32_t nr, uint32_t range) {
     extern __shared__ unsigned long long s_tb[];  // (range bins, then the chunk's region word counts)
     uint32_t* s_tot = reinterpret_cast<uint32_t*>(s_tb + range);
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, nt = blockDim.x;  // (256 or TOT_WG threads)
     const uint32_t c = blockIdx.x / nr, q = blockIdx.x % nr;
     const uint32_t lo = q * range, hi = min(p.ntx, lo + range);
     const uint32_t w0 = c * per, w1 = min(nwaves, w0 + per);
-    for (uint32_t i = t; i < range; i += WG) s_tb[i] = 0;
-    for (uint32_t i = t; i < w1 - w0; i += WG) s_tot[i] = p.cand_wtot[w0 + i];  // (every count in one round trip)
+    for (uint32_t i = t; i < range; i += nt) s_tb[i] = 0;
+    for (uint32_t i = t; i < w1 - w0; i += nt) s_tot[i] = p.cand_wtot[w0 + i];  // (every count in one round trip)
     __syncthreads();
     // each wave takes RB map-wave regions a round, their first 256 words (64 x 16 B; a region holds
     // ~200 words at cfg2) loaded together, the next round's loads issued before this round's adds:
@@ -2887,13 +2897,15 @@ __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves
         const uint32_t tid = x & 0x3FFFFFu;
         if (tid - lo < hi - lo) atomicAdd(&s_tb[tid - lo], (1ull << 40) | (unsigned long long)(x >> 22));
     };
+    // (the loads are unconditional — a region slot always holds 1024 words; words past its count are
+    // ignored below — so no branch splits them and the compiler keeps the next round in flight
+    // while this round is summed: vmcnt(RB), not vmcnt(0))
     auto issue = [&](uint32_t Wb, uint4 (&x)[RB]) {
 #pragma unroll
         for (uint32_t u = 0; u < RB; ++u) {
-            const uint32_t W = Wb + u;
-            const uint32_t tot = W < w1 ? s_tot[W - w0] : 0u;
+            const uint32_t W = min(Wb + u, w1 - 1);
             const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + (uint64_t)W * 64 * CCAP);
-            x[u] = lane * 4 < tot ? src[lane] : make_uint4(0, 0, 0, 0);
+            x[u] = src[lane];
         }
     };
     auto consume = [&](uint32_t Wb, const uint4 (&x)[RB]) {
@@ -2915,23 +2927,23 @@ __global__ __launch_bounds__(WG) void k_tot_small(ChainParams p, uint32_t nwaves
             }
         }
     };
-    constexpr uint32_t STEP = (WG / 64) * RB;
+    const uint32_t STEP = (nt / 64) * RB;
     uint32_t Wb = w0 + wv * RB;
     uint4 xa[RB], xb[RB];
     if (Wb < w1) issue(Wb, xa);
-    while (Wb < w1) {
+    while (Wb < w1) {  // (a round past the chunk's end loads its last region again, unused)
         const uint32_t Wn = Wb + STEP;
-        if (Wn < w1) issue(Wn, xb);
+        issue(Wn, xb);
         consume(Wb, xa);
         Wb = Wn;
         if (Wb >= w1) break;
         const uint32_t Wm = Wb + STEP;
-        if (Wm < w1) issue(Wm, xa);
+        issue(Wm, xa);
         consume(Wb, xb);
         Wb = Wm;
     }
     __syncthreads();
-    for (uint32_t i = t; i < hi - lo; i += WG) {
+    for (uint32_t i = t; i < hi - lo; i += nt) {
         const unsigned long long a = s_tb[i];
         if (a) atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_acc[lo + i]), a);
     }
@@ -3065,7 +3077,7 @@ int launch_sketch(const SketchParams& p, void* stream) {
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, grid, dim3(WG), lds, s, p);
+        launch_timed(kern, grid, dim3(WG), lds, s, p);
     };
     switch (p.hcap * 2 + (p.nthash ? 1 : 0)) {
     case 32: go(k_sketch<16, false>); break;
@@ -3088,7 +3100,7 @@ int launch_sketch_slow(const SketchParams& p, void* stream, unsigned grid) {
 int launch_probe(const ChainParams& p, void* stream) {
     if (p.n == 0) return 0;
     const dim3 grid((unsigned)((p.n + WG - 1) / WG));
-    hipLaunchKernelGGL(k_probe, grid, dim3(WG), chain_lds_bytes(p.nk), reinterpret_cast<hipStream_t>(stream), p);
+    launch_timed(k_probe, grid, dim3(WG), chain_lds_bytes(p.nk), reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -3101,11 +3113,11 @@ int launch_count(const ChainParams& p, void* stream) {
         auto go = [&](auto mode) {
             constexpr int M = decltype(mode)::value;
             switch (p.nk) {
-            case 1: hipLaunchKernelGGL((k_count3<1, M>), grid, dim3(WG), 0, st, p); break;
-            case 2: hipLaunchKernelGGL((k_count3<2, M>), grid, dim3(WG), 0, st, p); break;
-            case 3: hipLaunchKernelGGL((k_count3<3, M>), grid, dim3(WG), 0, st, p); break;
-            case 4: hipLaunchKernelGGL((k_count3<4, M>), grid, dim3(WG), 0, st, p); break;
-            default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, st, p); break;
+            case 1: launch_timed(k_count3<1, M>, grid, dim3(WG), 0, st, p); break;
+            case 2: launch_timed(k_count3<2, M>, grid, dim3(WG), 0, st, p); break;
+            case 3: launch_timed(k_count3<3, M>, grid, dim3(WG), 0, st, p); break;
+            case 4: launch_timed(k_count3<4, M>, grid, dim3(WG), 0, st, p); break;
+            default: launch_timed(k_route_slow, grid, dim3(WG), 0, st, p); break;
             }
         };
         // wide tables, 2..4 k slots: the entry-parallel count
@@ -3114,16 +3126,16 @@ int launch_count(const ChainParams& p, void* stream) {
             const bool cmp = p.wide == 3;
             switch (p.nk) {
             case 2:
-                if (cmp) hipLaunchKernelGGL((k_countw<2, true>), grid, dim3(WG), 0, st, p);
-                else hipLaunchKernelGGL((k_countw<2, false>), grid, dim3(WG), 0, st, p);
+                if (cmp) launch_timed(k_countw<2, true>, grid, dim3(WG), 0, st, p);
+                else launch_timed(k_countw<2, false>, grid, dim3(WG), 0, st, p);
                 break;
             case 3:
-                if (cmp) hipLaunchKernelGGL((k_countw<3, true>), grid, dim3(WG), 0, st, p);
-                else hipLaunchKernelGGL((k_countw<3, false>), grid, dim3(WG), 0, st, p);
+                if (cmp) launch_timed(k_countw<3, true>, grid, dim3(WG), 0, st, p);
+                else launch_timed(k_countw<3, false>, grid, dim3(WG), 0, st, p);
                 break;
             default:
-                if (cmp) hipLaunchKernelGGL((k_countw<4, true>), grid, dim3(WG), 0, st, p);
-                else hipLaunchKernelGGL((k_countw<4, false>), grid, dim3(WG), 0, st, p);
+                if (cmp) launch_timed(k_countw<4, true>, grid, dim3(WG), 0, st, p);
+                else launch_timed(k_countw<4, false>, grid, dim3(WG), 0, st, p);
                 break;
             }
             return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -3134,11 +3146,11 @@ int launch_count(const ChainParams& p, void* stream) {
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     switch (p.nk) {
-    case 1: hipLaunchKernelGGL(k_count<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-    case 2: hipLaunchKernelGGL(k_count<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-    case 3: hipLaunchKernelGGL(k_count<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-    case 4: hipLaunchKernelGGL(k_count<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
-    default: hipLaunchKernelGGL(k_route_slow, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 1: launch_timed(k_count<1>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 2: launch_timed(k_count<2>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 3: launch_timed(k_count<3>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    case 4: launch_timed(k_count<4>, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
+    default: launch_timed(k_route_slow, grid, dim3(WG), 0, reinterpret_cast<hipStream_t>(stream), p); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -3265,7 +3277,7 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tot_small), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
-        hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(WG), lds, st, p, nwaves, per, nr, range);
+        hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(beside_map ? WG : TOT_WG), lds, st, p, nwaves, per, nr, range);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     if (!binned) {

@@ -34,7 +34,7 @@ int launch_map1(const SketchParams& p0, const ChainParams& cp, void* stream) {
     }
     if (lds > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(MW), lds, st, p, cp);
+    launch_timed(kern, grid, dim3(MW), lds, st, p, cp);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -17,22 +17,22 @@ int launch_map1_pass(const SketchParams& p0, const ChainParams& cp, uint32_t cap
     const size_t lds = map1_layout(p, tab, cap, MW);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (cap * 16 + tab * 2 + (final_pass ? 1 : 0)) {
-    case 256: hipLaunchKernelGGL((k_map1<16, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 257: hipLaunchKernelGGL((k_map1<16, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 260: hipLaunchKernelGGL((k_map1<16, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 261: hipLaunchKernelGGL((k_map1<16, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 262: hipLaunchKernelGGL((k_map1<16, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 263: hipLaunchKernelGGL((k_map1<16, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 264: hipLaunchKernelGGL((k_map1<16, 4, 4, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 265: hipLaunchKernelGGL((k_map1<16, 4, 4, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 512: hipLaunchKernelGGL((k_map1<32, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 513: hipLaunchKernelGGL((k_map1<32, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 516: hipLaunchKernelGGL((k_map1<32, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 517: hipLaunchKernelGGL((k_map1<32, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 518: hipLaunchKernelGGL((k_map1<32, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 519: hipLaunchKernelGGL((k_map1<32, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 520: hipLaunchKernelGGL((k_map1<32, 4, 4, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 521: hipLaunchKernelGGL((k_map1<32, 4, 4, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 256: launch_timed((k_map1<16, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 257: launch_timed((k_map1<16, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 260: launch_timed((k_map1<16, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 261: launch_timed((k_map1<16, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 262: launch_timed((k_map1<16, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 263: launch_timed((k_map1<16, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 264: launch_timed((k_map1<16, 4, 4, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 265: launch_timed((k_map1<16, 4, 4, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 512: launch_timed((k_map1<32, 4, 0, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 513: launch_timed((k_map1<32, 4, 0, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 516: launch_timed((k_map1<32, 4, 2, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 517: launch_timed((k_map1<32, 4, 2, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 518: launch_timed((k_map1<32, 4, 3, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 519: launch_timed((k_map1<32, 4, 3, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 520: launch_timed((k_map1<32, 4, 4, true, false, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 521: launch_timed((k_map1<32, 4, 4, true, true, MW>), grid, dim3(MW), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -52,14 +52,14 @@ int launch_mapk(const SketchParams& p0, const ChainParams& cp, uint32_t cap, voi
     const size_t lds = map1_layout(p, tab, cap, MW);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (cap * 8 + tab) {
-    case 128: hipLaunchKernelGGL((k_mapk<16, 4, 0, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 130: hipLaunchKernelGGL((k_mapk<16, 4, 2, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 131: hipLaunchKernelGGL((k_mapk<16, 4, 3, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 132: hipLaunchKernelGGL((k_mapk<16, 4, 4, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 256: hipLaunchKernelGGL((k_mapk<32, 4, 0, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 258: hipLaunchKernelGGL((k_mapk<32, 4, 2, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 259: hipLaunchKernelGGL((k_mapk<32, 4, 3, MW>), grid, dim3(MW), lds, st, p, cp); break;
-    case 260: hipLaunchKernelGGL((k_mapk<32, 4, 4, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 128: launch_timed((k_mapk<16, 4, 0, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 130: launch_timed((k_mapk<16, 4, 2, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 131: launch_timed((k_mapk<16, 4, 3, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 132: launch_timed((k_mapk<16, 4, 4, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 256: launch_timed((k_mapk<32, 4, 0, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 258: launch_timed((k_mapk<32, 4, 2, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 259: launch_timed((k_mapk<32, 4, 3, MW>), grid, dim3(MW), lds, st, p, cp); break;
+    case 260: launch_timed((k_mapk<32, 4, 4, MW>), grid, dim3(MW), lds, st, p, cp); break;
     default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
