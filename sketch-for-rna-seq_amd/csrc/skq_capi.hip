@@ -183,7 +183,7 @@ struct skq_session {
     // side-stream work on frame x (its tail, then the reset of its control words once the next
     // batch has taken the other frame: zeroed[x])
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork{}, ev_done[2]{};
+    hipEvent_t ev_fork{}, ev_map{}, ev_done[2]{};  // (ev_map: bound to a side batch's map dispatch)
     bool done_rec[2] = {false, false};
     bool zeroed[2] = {false, false};
     bool tail_side[2] = {false, false};  // the frame's batch ran its tail on the side stream
@@ -933,6 +933,7 @@ static int ensure_side(skq_session* s) {
     if (s->side) return 0;
     HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_map, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_done[0], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_done[1], hipEventDisableTiming));
     return 0;
@@ -1314,6 +1315,7 @@ int skq_session_free(skq_session* s) {
         (void)hipStreamSynchronize(s->side);
         (void)hipStreamDestroy(s->side);
         (void)hipEventDestroy(s->ev_fork);
+        (void)hipEventDestroy(s->ev_map);
         (void)hipEventDestroy(s->ev_done[0]);
         (void)hipEventDestroy(s->ev_done[1]);
     }
@@ -1420,15 +1422,18 @@ int skq_sketch_seqs(skq_session* s, const uint8_t* d_seqs, const uint64_t* d_off
 static int binned(const skq::ChainParams& p) { return p.slow_totals && !p.cpack ? 1 : 0; }
 
 static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::ChainParams& p, int accumulate,
-                      hipStream_t st, bool side) {
+                      hipStream_t st, bool side, hipEvent_t map_end = nullptr) {
     hipEvent_t t0{};
     const bool totals = accumulate != 0;
     const bool fork = side || (totals && p.slow_totals && !p.cpack && p.n >= (1u << 19));
     hipStream_t tq = st;  // the stream of the totals
     if (fork) {
         if (int rc = ensure_side(s)) return rc;
-        HIP_TRY(hipEventRecord(s->ev_fork, st));
-        HIP_TRY(hipStreamWaitEvent(s->side, s->ev_fork, 0));
+        if (!map_end) {  // (else the event bound to the map's dispatch: no marker on the launch stream)
+            HIP_TRY(hipEventRecord(s->ev_fork, st));
+            map_end = s->ev_fork;
+        }
+        HIP_TRY(hipStreamWaitEvent(s->side, map_end, 0));
         tq = s->side;
     }
     hipStream_t sq = side ? s->side : st;  // the stream of the slow paths
@@ -1726,6 +1731,10 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
     cp.cand_wtot = s->f.cand_wtot;
     hipEvent_t t0{};
     record(s, 0, &t0, st);
+    // (a side batch's tail waits for the map through an event bound to its last dispatch — the
+    // timing scope's stop event when one is open)
+    if (side && !skq::g_launch_ev.stop) skq::g_launch_ev.stop = s->ev_map;
+    hipEvent_t map_end = side ? static_cast<hipEvent_t>(skq::g_launch_ev.stop) : nullptr;
     int rc = 0;
     if (ix->nk == 1) {
         rc = skq::launch_map1(sp, cp, stream);
@@ -1752,9 +1761,13 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
             }
         }
     }
-    if (rc) return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
+    if (rc) {
+        skq::g_launch_ev = {};
+        return fail(-3, rc == -4 ? "map kernel: unsupported capacity" : "map launch failed");
+    }
     record_stop(s, 0, t0, st);
-    if (int rc = chain_tail(s, &sp, cp, accumulate, st, side)) return rc;
+    skq::g_launch_ev = {};
+    if (int rc = chain_tail(s, &sp, cp, accumulate, st, side, map_end)) return rc;
     s->have_chain = true;
     // the fused kernels filled no probe offsets (lofs): a later skq_chain on these sketches
     // probes them itself (k_probe, then the count kernel over the packed sets)

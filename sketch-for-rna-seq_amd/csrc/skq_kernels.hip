@@ -3259,17 +3259,13 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
     if (nb > (uint32_t)WG) return -1;
     if (!binned && p.cpack && p.ntx <= TOT_SMALL_TX && p.cand_wtot) {  // (small transcript sets: no binning)
         const uint32_t nwaves = (uint32_t)((p.n + 63) / 64);
-        // (ranges of <= 2560 ids between maps: a workgroup's flush is one 8-B atomic per bin, and a
-        // CU issues such wave-instructions only every ~50 ns (MI355X_MICROARCH.md, global atomics),
-        // so 64 workgroups flushing 10k bins each took 21 us where 256 flushing 2.5k take ~4)
-        uint32_t range = beside_map ? TOT_RANGE_TX : std::min<uint32_t>(p.ntx, 2560);
-        uint32_t chunks = 64;
-        if (const char* e = std::getenv("SKQ_DEV")) {  // (development sweep: SKQ_TOT_RANGE, SKQ_TOT_CHUNKS)
-            if (std::atoi(e) == 1) {
-                if (const char* r = std::getenv("SKQ_TOT_RANGE")) range = std::max(256, std::atoi(r));
-                if (const char* r = std::getenv("SKQ_TOT_CHUNKS")) chunks = std::max(1, std::atoi(r));
-            }
-        }
+        // between maps: 1024-thread workgroups, 64 chunks of the batch's map waves, ranges of <= 5120
+        // ids (40 KiB of bins: two ranges at cfg2's 10k). Swept at cfg2 (profiles/r6_tot_small_sweep.log):
+        // 64 chunks x 5000 ids 13.9 us, x 2560 16.2, x 10000 19+; 128 chunks (twice the flush atomics)
+        // 17-20 us; 256-thread workgroups 19-26 us (one wave per SIMD: each wave waits on its own loads)
+        const uint32_t nr0 = (p.ntx + 5119) / 5120;
+        const uint32_t range = beside_map ? TOT_RANGE_TX : (p.ntx + nr0 - 1) / nr0;
+        const uint32_t chunks = 64;
         const uint32_t nr = (p.ntx + range - 1) / range;
         const uint32_t per = std::min<uint32_t>(1024, std::max<uint32_t>(16, (nwaves + chunks - 1) / chunks));
         const uint32_t nc = (nwaves + per - 1) / per;
