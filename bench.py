@@ -532,7 +532,7 @@ def measure(cname, cfg, args, rank, world, dev, gpu, sample, totals_dev=True):
         fr["requests"] = requests["frac"]
     top = max(fr, key=fr.get)
     bound = top if fr[top] >= 0.7 else "latency"
-    bj, bf = load_profile_json("r6_pmc_bound_%s.json" % tname)
+    bj, bf = load_profile_json("pmc_bound_%s.json" % tname)
     bound_ev = None
     if bj is not None and bj.get("kernel") == kname:
         bound_ev = dict(bj.get("derived", {}), source=bf, measured=bj.get("measured"))

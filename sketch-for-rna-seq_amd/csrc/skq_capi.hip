@@ -1673,7 +1673,9 @@ static int map_fused(skq_session* s, const uint8_t* d_reads, const uint64_t* d_o
         s->done_rec[o] = true;
         s->zeroed[o] = true;
         // this frame's last tail (two batches back) and its reset
-        if (s->done_rec[s->fid]) HIP_TRY(hipStreamWaitEvent(st, s->ev_done[s->fid], 0));
+        // (a tail already done needs no barrier packet on the launch stream)
+        if (s->done_rec[s->fid] && hipEventQuery(s->ev_done[s->fid]) != hipSuccess)
+            HIP_TRY(hipStreamWaitEvent(st, s->ev_done[s->fid], 0));
         if (!s->zeroed[s->fid]) HIP_TRY(hipMemsetAsync(s->f.ctrl, 0, skq::C_WORDS * 4, st));
     } else {
         if (int rc = wait_side(s, st)) return rc;

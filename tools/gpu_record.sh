@@ -1,5 +1,5 @@
 #!/bin/bash
-# Record call (round 5): calibrated traffic (FETCH_SIZE / WRITE_SIZE) and instruction-count passes
+# Record call (rounds 5-6): calibrated traffic (FETCH_SIZE / WRITE_SIZE) and instruction-count passes
 # per single-GPU config, the kernel-trace stats of the default bench, then the default bench
 # line itself (cfg3, with the cfg2 / cfg5 legs). The JSON the passes produce go to profiles/ on the
 # box (so the bench lines read them) and to gpurun_out/ (to be committed).
@@ -27,15 +27,23 @@ for spec in "cfg3|k_map1=150|10000000" "cfg2|k_map1=100|1000000" "cfg5|k_map1 x3
   cp $o/valu_$c.json profiles/valu_$c.json
   echo "$c: traffic and instruction counts done"
 done
+# what binds k_map1 (cycle counters over tools/kbench.py: cfg3, 10M reads, the default chained
+# tables), then the stall and LDS sets for the record
+tools/pmc.sh bound $o/bound --probes auto/chain --rounds 2 > $o/bound.log 2>&1 || { echo "bound failed"; tail -20 $o/bound.log; exit 1; }
+python3 tools/pmc_bound.py $o/bound k_map1 10000000 "tools/pmc.sh bound over tools/kbench.py (cfg3, 10M reads, chained), tools/pmc_bound.py; $t" > $o/pmc_bound_cfg3.json || { echo "pmc_bound failed"; exit 1; }
+cp $o/pmc_bound_cfg3.json profiles/pmc_bound_cfg3.json
+for set_ in stall lds; do
+  tools/pmc.sh $set_ $o/$set_ --probes auto/chain --rounds 2 > $o/$set_.log 2>&1 || { echo "$set_ failed"; tail -20 $o/$set_.log; exit 1; }
+done
+echo "pmc sets done"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/stats -o run -- python3 bench.py --no-cpu-baseline --no-end-to-end --no-extra-configs > $o/stats_bench.json 2> $o/stats_bench.err || { echo "stats bench failed"; tail -20 $o/stats_bench.err; exit 1; }
 timeout -k 10 500 python3 bench.py > $o/bench.json 2> $o/bench.err || { echo "bench failed"; tail -30 $o/bench.err; exit 1; }
 python3 - "$o/bench.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["roofline"]
-print("cfg3 %.3f G reads/s, %.4f ms/step, k_map1 %.4f ms, frac %.4f, bound %s, valu frac %s, traffic %s" % (
-    d["value"] / 1e9, d["ms_per_step"], r["avg_launch_ms"], r["frac"], r["bound"],
-    (r.get("valu") or {}).get("frac"), r.get("traffic")))
+print("cfg3 %.3f G reads/s, %.4f ms/step, k_map1 %.4f ms, frac %.4f, bound %s, fractions %s, traffic %s" % (
+    d["value"] / 1e9, d["ms_per_step"], r["avg_launch_ms"], r["frac"], r["bound"], r.get("fractions"), r.get("traffic")))
 for c, x in (d.get("configs") or {}).items():
     rx = x["roofline"]
     print("%s %.3f G reads/s, %.4f ms/step, frac %.4f, bound %s, parity %s" % (c, x["value"] / 1e9, x["ms_per_step"], rx["frac"], rx["bound"], x["parity_sample"][:40]))

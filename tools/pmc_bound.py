@@ -14,7 +14,7 @@ quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs, so kernel cycles = GRBM_
   ta_busy        TA_TA_BUSY_sum / (CUs * kernel cycles)              the texture addresser (one per CU)
   salu_busy      SQ_ACTIVE_INST_SCA * 4 / (CUs * kernel cycles)      the scalar unit (one per CU)
 
-usage: tools/pmc_bound.py PMC_DIR KERNEL_SUBSTRING MIN_GRID > out.json
+usage: tools/pmc_bound.py PMC_DIR KERNEL_SUBSTRING MIN_GRID [MEASURED_NOTE] > out.json
 """
 import collections
 import csv
@@ -50,6 +50,8 @@ for pdir in sorted(glob.glob(os.path.join(d, "p*")), key=lambda x: int(os.path.b
                 if g >= min_grid:
                     durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
 out = {"kernel": kname, "counters": vals}
+if len(sys.argv) > 4:
+    out["measured"] = sys.argv[4]
 if durs:
     out["dispatch_ms_median"] = statistics.median(durs)
 g = vals.get("GRBM_GUI_ACTIVE")
