@@ -3,16 +3,23 @@
 kernel, each pass's counters summed over their rows (XCDs / instances), then the median over the
 dispatches of one pass; a counter collected in several passes is read from the first.
 
-Derived figures (MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count
-quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs, so kernel cycles = GRBM_GUI_ACTIVE / 8):
-  valu_busy      SQ_ACTIVE_INST_VALU * 4 / (SIMDs * kernel cycles)   cycles a SIMD's VALU works
-  valu_issue     SQ_INSTS_VALU * 2 / (SIMDs * kernel cycles)         the instruction-count form
-                 (a wave64 instruction at full rate = 2 cycles of a SIMD-32)
-  wait_frac      SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES                   wave time waiting on a dependency
-  waves_per_simd SQ_WAVE_CYCLES * 4 / (SIMDs * kernel cycles)        achieved resident waves
-  lds_conflict   SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS           conflict cycles per LDS-active cycle
-  ta_busy        TA_TA_BUSY_sum / (CUs * kernel cycles)              the texture addresser (one per CU)
-  salu_busy      SQ_ACTIVE_INST_SCA * 4 / (CUs * kernel cycles)      the scalar unit (one per CU)
+Derived figures (MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_WAIT_* count quad-cycles; GRBM_GUI_ACTIVE
+is summed over the 8 XCDs, so kernel cycles = GRBM_GUI_ACTIVE / 8). On this stack SQ_ACTIVE_INST_VALU
+and SQ_ACTIVE_INST_SCA return instruction counts (equal to SQ_INSTS_VALU / within 2 % of
+SQ_INSTS_SALU), not busy cycles, so no busy-cycle fraction is derived from them; the issue-count
+forms are:
+  valu_issue     SQ_INSTS_VALU * 2 / (SIMDs * kernel cycles)   a wave64 instruction at full rate = 2
+                 cycles of a SIMD-32 (three-operand forms take ~2x: profiles/r4_valu_rate.log)
+  salu_issue     SQ_INSTS_SALU / (CUs * kernel cycles)          one scalar instruction per CU per cycle
+  lds_issue      SQ_INSTS_LDS / (CUs * kernel cycles)           one LDS instruction per CU per cycle
+  wait_frac      SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES              wave time waiting on a dependency
+  active_frac    SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES            wave time issuing
+  waves_per_simd SQ_WAVE_CYCLES * 4 / (SIMDs * kernel cycles)   achieved resident waves
+  lds_conflict   SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS      conflict cycles per LDS-active cycle
+  ta_busy        TA_TA_BUSY_sum / (CUs * kernel cycles)         the texture addresser (one per CU)
+  ta_stalled_by_tc  TA_ADDR_STALLED_BY_TC_CYCLES_sum / (CUs * kernel cycles)
+  tcp_pending_stall TCP_PENDING_STALL_CYCLES_sum / (CUs * kernel cycles)   the vector L1 waiting on
+                 data pending from the L2
 
 usage: tools/pmc_bound.py PMC_DIR KERNEL_SUBSTRING MIN_GRID [MEASURED_NOTE] > out.json
 """
@@ -61,10 +68,12 @@ if g:
     if durs:
         out["effective_clock_GHz"] = kc / (statistics.median(durs) * 1e-3) / 1e9
     der = {}
-    if "SQ_ACTIVE_INST_VALU" in vals:
-        der["valu_busy"] = vals["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * kc)
     if "SQ_INSTS_VALU" in vals:
         der["valu_issue"] = vals["SQ_INSTS_VALU"] * 2 / (SIMDS * kc)
+    if "SQ_INSTS_SALU" in vals:
+        der["salu_issue"] = vals["SQ_INSTS_SALU"] / (CUS * kc)
+    if "SQ_INSTS_LDS" in vals:
+        der["lds_issue"] = vals["SQ_INSTS_LDS"] / (CUS * kc)
     if "SQ_WAVE_CYCLES" in vals:
         der["waves_per_simd"] = vals["SQ_WAVE_CYCLES"] * 4 / (SIMDS * kc)
         if "SQ_WAIT_INST_ANY" in vals:
@@ -73,13 +82,15 @@ if g:
             der["active_frac"] = vals["SQ_ACTIVE_INST_ANY"] / vals["SQ_WAVE_CYCLES"]
     if "SQ_LDS_BANK_CONFLICT" in vals and vals.get("SQ_ACTIVE_INST_LDS"):
         der["lds_conflict"] = vals["SQ_LDS_BANK_CONFLICT"] / vals["SQ_ACTIVE_INST_LDS"]
-    if "SQ_ACTIVE_INST_LDS" in vals:
-        der["lds_busy"] = vals["SQ_ACTIVE_INST_LDS"] * 4 / (CUS * kc)
     if "TA_TA_BUSY_sum" in vals:
         der["ta_busy"] = vals["TA_TA_BUSY_sum"] / (CUS * kc)
     if "TA_ADDR_STALLED_BY_TC_CYCLES_sum" in vals:
         der["ta_stalled_by_tc"] = vals["TA_ADDR_STALLED_BY_TC_CYCLES_sum"] / (CUS * kc)
-    if "SQ_ACTIVE_INST_SCA" in vals:
-        der["salu_busy"] = vals["SQ_ACTIVE_INST_SCA"] * 4 / (CUS * kc)
+    if "TCP_PENDING_STALL_CYCLES_sum" in vals:
+        der["tcp_pending_stall"] = vals["TCP_PENDING_STALL_CYCLES_sum"] / (CUS * kc)
+    if "SQ_ACTIVE_INST_VALU" in vals and "SQ_INSTS_VALU" in vals:
+        out["note"] = ("SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU = %.3f: the busy counter returns the instruction "
+                       "count on this stack, so only issue-count fractions are derived" %
+                       (vals["SQ_ACTIVE_INST_VALU"] / vals["SQ_INSTS_VALU"]))
     out["derived"] = der
 print(json.dumps(out, indent=1))
