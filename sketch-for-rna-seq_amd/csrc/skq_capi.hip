@@ -183,7 +183,8 @@ struct skq_session {
     // side-stream work on frame x (its tail, then the reset of its control words once the next
     // batch has taken the other frame: zeroed[x])
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork{}, ev_map{}, ev_done[2]{};  // (ev_map: bound to a side batch's map dispatch)
+    hipEvent_t ev_fork{}, ev_map{}, ev_done[2]{};
+    hipStream_t last_st{};  // (the stream of the last batch's tail: where a results call folds the sums)  // (ev_map: bound to a side batch's map dispatch)
     bool done_rec[2] = {false, false};
     bool zeroed[2] = {false, false};
     bool tail_side[2] = {false, false};  // the frame's batch ran its tail on the side stream
@@ -1425,6 +1426,7 @@ static int chain_tail(skq_session* s, const skq::SketchParams* sp, const skq::Ch
                       hipStream_t st, bool side, hipEvent_t map_end = nullptr) {
     hipEvent_t t0{};
     const bool totals = accumulate != 0;
+    s->last_st = st;
     const bool fork = side || (totals && p.slow_totals && !p.cpack && p.n >= (1u << 19));
     hipStream_t tq = st;  // the stream of the totals
     if (fork) {
@@ -1807,15 +1809,21 @@ int skq_chain_sketches(skq_session* s, uint64_t n_reads, const uint32_t* d_hashe
                       accumulate, false, stream);
 }
 
-int skq_session_results(skq_session* s, skq_results* o) {
+int skq_session_results(skq_session* s, skq_results* o) { return skq::session_results(s, o, true); }
+
+}  // extern "C"
+
+namespace skq {
+// (fold = false: the per-read arrays only — the EM's append and the ingest's status copy — so no
+// fold kernel is queued per batch)
+int session_results(skq_session* s, skq_results* o, bool fold) {
     if (!s || !o) return fail(-1, "null argument");
-    {  // the batch's tail and the totals may still run on the side stream; the packed sums fold
+    {  // the batch's tail and the totals may still run on the side stream (the host waits for it);
+       // the packed sums fold on the stream of the last batch's tail, behind it, so tx_reads /
+       // tx_score are current once the caller's stream is synchronized (skq.h)
         DeviceGuard g(s->idx->device);
-        if (s->acc_reads) {
-            hipStream_t fs = s->side ? s->side : nullptr;
-            if (int rc = fold_totals(s, fs)) return rc;
-            HIP_TRY(hipStreamSynchronize(fs));
-        }
+        if (fold && s->acc_reads)
+            if (int rc = fold_totals(s, s->last_st)) return rc;
         if (int rc = sync_side(s)) return rc;
     }
     o->n_reads = s->n_reads;
@@ -1837,6 +1845,9 @@ int skq_session_results(skq_session* s, skq_results* o) {
     o->tx_score = s->tx_score;
     return 0;
 }
+}  // namespace skq
+
+extern "C" {
 
 int skq_session_check(skq_session* s, void* stream) {
     if (!s) return fail(-1, "null session");

@@ -510,7 +510,7 @@ int skq_em_add(skq_em_set* em, uint64_t nreads, const uint64_t* cand_offs, const
 int skq_em_add_session(skq_em_set* em, skq_session* s, void* stream) {
     if (!em || !s) return efail(-1, "null argument");
     skq_results res{};
-    if (int rc = skq_session_results(s, &res)) return rc;
+    if (int rc = skq::session_results(s, &res, false)) return rc;
     if (skq::session_device(s) != em->device) return efail(-1, "session and EM set on different devices");
     if (res.ntx != em->ntx) return efail(-1, "session index and EM set disagree on the transcript count");
     const uint64_t n = res.n_reads;

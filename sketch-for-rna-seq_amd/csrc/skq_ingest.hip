@@ -814,7 +814,7 @@ int skq_ingest_map(skq_ingest* g, uint32_t threshold, double fraction, int accum
                  stream);
     if (!rc) {
         skq_results res{};
-        rc = skq_session_results(g->s, &res);
+        rc = skq::session_results(g->s, &res, false);
         if (!rc) {
             k_copy_status<<<blocks(m, 256), 256, 0, st>>>(res.status, g->status.p + g->records, (uint32_t)m);
             if (hipGetLastError() != hipSuccess) rc = ifail(-3, "status copy failed");

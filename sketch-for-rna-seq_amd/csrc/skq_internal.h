@@ -21,6 +21,9 @@ struct LaunchEvents {
 };
 extern thread_local LaunchEvents g_launch_ev;
 
+// skq_session_results with or without folding the packed per-transcript sums (skq_capi.hip)
+int session_results(skq_session* s, skq_results* o, bool fold);
+
 constexpr int WG = 256;            // threads per workgroup for both kernels (4 waves)
 constexpr int LFAST = 256;         // reads longer than this take the slow path
 constexpr int DCAP = 16;           // distinct transcripts per read on the fast chain path
