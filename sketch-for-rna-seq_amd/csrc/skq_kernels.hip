@@ -2782,40 +2782,41 @@ __global__ __launch_bounds__(WG) void k_bin(ChainParams p, uint32_t bits, uint32
 // or less — a workgroup with more candidates than that adds them all directly (64-bit atomics into
 // the running totals) and leaves its region empty. (1,280 words, ~6 KB of LDS, would fit beside
 // five k_map1 workgroups on a CU: measured no faster, launch_bin.)
-template <uint32_t CAPW>
-__global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nW,
+template <uint32_t CAPW, int G>
+__global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits, uint32_t nb, uint32_t nWg,
                                                    uint32_t* hdr, uint32_t* region) {
     __shared__ uint32_t s_bc[WG + 1];
     __shared__ uint32_t s_tot;
     __shared__ __attribute__((aligned(16))) uint32_t s_reg[CAPW];
-    const uint32_t t = threadIdx.x, w = blockIdx.x, lane = t & 63;
+    const uint32_t t = threadIdx.x, w = blockIdx.x, lane = t & 63, v = t >> 6;
     s_bc[t] = 0;
     if (t == 0) s_bc[WG] = 0;
-    // each wave takes one map wave's region: its packed words [0, tot) (ChainParams::cand_wtot, the
-    // map's own count of them) read coalesced, 16 B per lane per round of 256 words. A full wave's
-    // first round is loaded beside its count, not after it (the region is allocated whatever its
-    // fill; the words past tot are masked), so the kernel waits on one memory round trip, where the
-    // per-read counts, their scan and then each lane's own run took two and touched a line per lane
-    const uint64_t W = (uint64_t)w * (WG / 64) + (t >> 6), r0 = W * 64;  // (the map wave)
-    const uint32_t tot = r0 < p.n ? p.cand_wtot[W] : 0u;  // (wave-uniform)
-    const uint4* src = reinterpret_cast<const uint4*>(p.cand_tid + r0 * CCAP) + lane;
-    const uint32_t lim = r0 + 64 <= p.n ? 256u : tot;  // (a partial last wave: only what it holds)
-    constexpr int R = 64 * CCAP / 256;  // rounds of a full region
-    uint4 x[R];
+    // wave v takes map wave v of each of the G map workgroups w * G .. w * G + G - 1: their packed
+    // words [0, tot) (ChainParams::cand_wtot, the map's own count of them), the first 256 of each
+    // in one 16-B load per lane, all G loads issued beside the counts, so the kernel waits on one
+    // memory round trip (the words past 256 — a region of more than 4 candidates per read — are
+    // read again per lane in both passes below). G > 1: one binned region per G map workgroups,
+    // whose bucket segments are G times longer for k_bin_sum4
+    uint32_t tot[G];
+    uint4 x[G];
+    const uint32_t* src[G];
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const uint32_t e = q * 256 + lane * 4;
-        const bool ld = q == 0 ? e < lim : e < tot;
-        x[q] = ld ? src[q * 64] : make_uint4(0, 0, 0, 0);
+    for (int g = 0; g < G; ++g) {
+        const uint64_t W = ((uint64_t)w * G + g) * (WG / 64) + v, r0 = W * 64;
+        tot[g] = r0 < p.n ? p.cand_wtot[W] : 0u;  // (wave-uniform)
+        src[g] = p.cand_tid + (r0 < p.n ? r0 : 0) * CCAP;
+        const uint32_t lim = r0 + 64 <= p.n ? 256u : tot[g];  // (a partial last wave: only what it holds)
+        x[g] = lane * 4 < lim ? reinterpret_cast<const uint4*>(src[g])[lane] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     const uint32_t mask = (1u << bits) - 1u;
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const uint32_t xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+    for (int g = 0; g < G; ++g) {
+        const uint32_t xs[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            if (q * 256 + lane * 4 + i < tot) atomicAdd(&s_bc[(xs[i] & 0x3FFFFFu) >> bits], 1u);
+            if (lane * 4 + i < tot[g]) atomicAdd(&s_bc[(xs[i] & 0x3FFFFFu) >> bits], 1u);
+        for (uint32_t e = 256 + lane; e < tot[g]; e += 64) atomicAdd(&s_bc[(src[g][e] & 0x3FFFFFu) >> bits], 1u);
     }
     __syncthreads();
     if (t < 64) {  // one wave scans the (<= 256) bucket counts, 4 per lane
@@ -2827,44 +2828,46 @@ __global__ __launch_bounds__(WG) void k_bin_packed(ChainParams p, uint32_t bits,
             sum += c4[u];
         }
         const uint32_t bi = wave_incl_scan(sum, t);
-        const uint32_t all = __shfl(bi, 63, 64);
+        const uint32_t all = wave_last(bi);
         const bool fits = all <= CAPW;
         uint32_t run = bi - sum;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t b = 4 * t + u;
             if (b < nb) {
-                hdr[(uint64_t)b * nW + w] = fits ? run : 0u;
+                hdr[(uint64_t)b * nWg + w] = fits ? run : 0u;
                 s_bc[b] = run;
             }
             run += c4[u];
         }
         if (t == 63) {
-            hdr[(uint64_t)nb * nW + w] = fits ? bi : 0u;
+            hdr[(uint64_t)nb * nWg + w] = fits ? bi : 0u;
             s_tot = bi;
         }
     }
     __syncthreads();
     const bool fits = s_tot <= CAPW;  // (uniform)
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const uint32_t xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (q * 256 + lane * 4 + i >= tot) continue;
-            const uint32_t tid = xs[i] & 0x3FFFFFu, score = xs[i] >> 22;
-            if (fits) {
-                const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
-                s_reg[pos] = (tid & mask) | (score << bits);
-            } else {  // (more candidates than the staging holds: straight into the totals)
-                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid]), 1ull);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
-            }
+    auto place = [&](uint32_t xw) {
+        const uint32_t tid = xw & 0x3FFFFFu, score = xw >> 22;
+        if (fits) {
+            const uint32_t pos = atomicAdd(&s_bc[tid >> bits], 1u);
+            s_reg[pos] = (tid & mask) | (score << bits);
+        } else {  // (more candidates than the staging holds: straight into the totals)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_reads[tid]), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.tx_score[tid]), (unsigned long long)score);
         }
+    };
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint32_t xs[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (lane * 4 + i < tot[g]) place(xs[i]);
+        for (uint32_t e = 256 + lane; e < tot[g]; e += 64) place(src[g][e]);
     }
     if (!fits) return;  // (uniform)
     __syncthreads();
-    uint4* reg = reinterpret_cast<uint4*>(region + (uint64_t)w * (WG * CCAP));
+    uint4* reg = reinterpret_cast<uint4*>(region + (uint64_t)w * CAPW);
     const uint4* sr = reinterpret_cast<const uint4*>(s_reg);
     for (uint32_t q = t; q < (s_tot + 3) / 4; q += WG) reg[q] = sr[q];
 }
@@ -3040,6 +3043,44 @@ __global__ __launch_bounds__(WG) void k_bin_sum_g(uint64_t* tx_acc, uint32_t ntx
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (q + u * GS < s1) atomicAdd(&s_bins[x[u] & (bs - 1u)], (1ull << 40) | (unsigned long long)(x[u] >> bits));
+        }
+    }
+    __syncthreads();
+    bins_out(s_bins, bs, b, ntx, tx_acc);
+}
+
+// k_bin_sum over k_bin_packed's grouped regions (G map workgroups each: a bucket's segment holds
+// ~65 entries at cfg3): a group of GS lanes per region reads its segment as 16-B words, U per lane
+// in flight (GS * U * 4 entries a round)
+template <int GS>
+__global__ __launch_bounds__(WG) void k_bin_sum4(uint64_t* tx_acc, uint32_t ntx, uint32_t bits, uint32_t nW,
+                                                 uint32_t chunk, const uint32_t* hdr, const uint32_t* region,
+                                                 uint32_t rstride) {
+    extern __shared__ unsigned long long s_bins[];
+    const uint32_t t = threadIdx.x, b = blockIdx.y;
+    const uint32_t bs = 1u << bits;
+    for (uint32_t i = t; i < bs; i += WG) s_bins[i] = 0;
+    __syncthreads();
+    const uint32_t w0 = blockIdx.x * chunk, w1 = min(nW, w0 + chunk);
+    const uint32_t g = t / GS, gl = t % GS;
+    constexpr int U = 4;
+    for (uint32_t w = w0 + g; w < w1; w += WG / GS) {
+        const uint32_t s0 = hdr[(uint64_t)b * nW + w], s1 = hdr[(uint64_t)(b + 1) * nW + w];
+        const uint4* reg4 = reinterpret_cast<const uint4*>(region + (uint64_t)w * rstride);  // (16-B aligned)
+        for (uint32_t q = (s0 & ~3u) + 4 * gl; q < s1; q += 4 * GS * U) {
+            uint4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = reg4[min((q + 4 * GS * u) / 4, (s1 - 1) / 4)];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t j = q + 4 * GS * u + i;
+                    if (j >= s0 && j < s1)
+                        atomicAdd(&s_bins[xs[i] & (bs - 1u)], (1ull << 40) | (unsigned long long)(xs[i] >> bits));
+                }
+            }
         }
     }
     __syncthreads();
@@ -3276,9 +3317,32 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
         hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(beside_map ? WG : TOT_WG), lds, st, p, nwaves, per, nr, range);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
+    // the fused map's packed candidates: one binned region per bin_g map workgroups (development
+    // A/B: SKQ_BIN_G 1, 4 or 8; SKQ_BIN_GS 4 or 8 lanes per region in k_bin_sum4)
+    static const int bin_g = [] {
+        const char* d = std::getenv("SKQ_DEV");
+        const char* e = d && std::atoi(d) == 1 ? std::getenv("SKQ_BIN_G") : nullptr;
+        const int v = e ? std::atoi(e) : 4;
+        return v == 1 || v == 8 ? v : 4;
+    }();
+    static const int bin_gs = [] {
+        const char* d = std::getenv("SKQ_DEV");
+        const char* e = d && std::atoi(d) == 1 ? std::getenv("SKQ_BIN_GS") : nullptr;
+        return e && std::atoi(e) == 8 ? 8 : 4;
+    }();
+    const bool grouped = !binned && p.cpack && nb > 4 && bin_g > 1;
+    const uint32_t nWb = grouped ? (nW + bin_g - 1) / bin_g : nW;  // (binned regions)
+    const uint32_t rstride = grouped && bin_g == 8 ? 2 * WG * CCAP : WG * CCAP;  // (words per binned region)
     if (!binned) {
-        if (p.cpack && nb)  // (the fused map's packed candidates)
-            hipLaunchKernelGGL(k_bin_packed<WG * CCAP>, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
+        if (p.cpack && nb && grouped && bin_g == 8)
+            hipLaunchKernelGGL((k_bin_packed<2 * WG * CCAP, 8>), dim3(nWb), dim3(WG), 0, st, p, bits, nb, nWb, p.bin_hdr,
+                               p.bin_region);
+        else if (p.cpack && nb && grouped)
+            hipLaunchKernelGGL((k_bin_packed<WG * CCAP, 4>), dim3(nWb), dim3(WG), 0, st, p, bits, nb, nWb, p.bin_hdr,
+                               p.bin_region);
+        else if (p.cpack && nb)
+            hipLaunchKernelGGL((k_bin_packed<WG * CCAP, 1>), dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr,
+                               p.bin_region);
         else
             hipLaunchKernelGGL(k_bin, dim3(nW), dim3(WG), 0, st, p, bits, nb, nW, p.bin_hdr, p.bin_region);
         if (hipGetLastError() != hipSuccess) return -2;
@@ -3287,10 +3351,16 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
     // chunks * nb ~ 512 workgroups, 1024 for many buckets (their bins are 32 KiB: four workgroups
     // per CU; profiles/r5_totals_sweep.log)
     const uint32_t wgs = nb >= 16 ? 1024 : 512;
-    const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nW, wgs / nb));
-    const uint32_t chunk = (nW + chunks - 1) / chunks;
+    const uint32_t chunks = std::max<uint32_t>(1, std::min<uint32_t>(nWb, wgs / nb));
+    const uint32_t chunk = (nWb + chunks - 1) / chunks;
     const size_t lds = (size_t)8 << bits;
-    if (nb <= 4) {  // few buckets: long segments per region, a 16-lane group walks each
+    if (grouped) {
+        auto kern = bin_gs == 8 ? k_bin_sum4<8> : k_bin_sum4<4>;
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3((nWb + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits, nWb,
+                           chunk, hdr, region, rstride);
+    } else if (nb <= 4) {  // few buckets: long segments per region, a 16-lane group walks each
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum_g<16>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
