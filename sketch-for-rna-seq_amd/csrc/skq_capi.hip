@@ -932,18 +932,7 @@ static int fold_totals(skq_session* s, hipStream_t st) {
 
 static int ensure_side(skq_session* s) {
     if (s->side) return 0;
-    if (const char* e = dev_env("SKQ_SIDE_CUS")) {  // (development A/B: the side stream on every
-        // (256 / N)-th CU only)
-        const int n = std::max(1, std::min(256, std::atoi(e)));
-        uint32_t mask[8] = {};
-        for (int i = 0; i < n; ++i) {
-            const int cu = i * 256 / n;
-            mask[cu >> 5] |= 1u << (cu & 31);
-        }
-        HIP_TRY(hipExtStreamCreateWithCUMask(&s->side, 8, mask));
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-    }
+    HIP_TRY(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_map, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_done[0], hipEventDisableTiming));

@@ -3317,27 +3317,15 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
         hipLaunchKernelGGL(k_tot_small, dim3(nc * nr), dim3(beside_map ? WG : TOT_WG), lds, st, p, nwaves, per, nr, range);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
-    // the fused map's packed candidates: one binned region per bin_g map workgroups (development
-    // A/B: SKQ_BIN_G 1, 4 or 8; SKQ_BIN_GS 4 or 8 lanes per region in k_bin_sum4)
-    static const int bin_g = [] {
-        const char* d = std::getenv("SKQ_DEV");
-        const char* e = d && std::atoi(d) == 1 ? std::getenv("SKQ_BIN_G") : nullptr;
-        const int v = e ? std::atoi(e) : 4;
-        return v == 1 || v == 8 ? v : 4;
-    }();
-    static const int bin_gs = [] {
-        const char* d = std::getenv("SKQ_DEV");
-        const char* e = d && std::atoi(d) == 1 ? std::getenv("SKQ_BIN_GS") : nullptr;
-        return e && std::atoi(e) == 8 ? 8 : 4;
-    }();
-    const bool grouped = !binned && p.cpack && nb > 4 && bin_g > 1;
-    const uint32_t nWb = grouped ? (nW + bin_g - 1) / bin_g : nW;  // (binned regions)
-    const uint32_t rstride = grouped && bin_g == 8 ? 2 * WG * CCAP : WG * CCAP;  // (words per binned region)
+    // the fused map's packed candidates: one binned region per four map workgroups (k_bin_packed<4096,
+    // 4>), summed by k_bin_sum4 — against one per map workgroup, cfg3 9.50 -> 9.95 G reads/s on one
+    // box; three or eight per region, unstaged stores and 2^10-2^11-id buckets measured slower
+    // (profiles/r6_bin_group_ab.log)
+    const bool grouped = !binned && p.cpack && nb > 4;
+    const uint32_t nWb = grouped ? (nW + 3) / 4 : nW;  // (binned regions)
+    const uint32_t rstride = WG * CCAP;                 // (words per binned region)
     if (!binned) {
-        if (p.cpack && nb && grouped && bin_g == 8)
-            hipLaunchKernelGGL((k_bin_packed<2 * WG * CCAP, 8>), dim3(nWb), dim3(WG), 0, st, p, bits, nb, nWb, p.bin_hdr,
-                               p.bin_region);
-        else if (p.cpack && nb && grouped)
+        if (grouped)
             hipLaunchKernelGGL((k_bin_packed<WG * CCAP, 4>), dim3(nWb), dim3(WG), 0, st, p, bits, nb, nWb, p.bin_hdr,
                                p.bin_region);
         else if (p.cpack && nb)
@@ -3355,11 +3343,11 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
     const uint32_t chunk = (nWb + chunks - 1) / chunks;
     const size_t lds = (size_t)8 << bits;
     if (grouped) {
-        auto kern = bin_gs == 8 ? k_bin_sum4<8> : k_bin_sum4<4>;
         if (lds > 64 * 1024)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, dim3((nWb + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx, bits, nWb,
-                           chunk, hdr, region, rstride);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum4<4>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_bin_sum4<4>, dim3((nWb + chunk - 1) / chunk, nb), dim3(WG), lds, st, p.tx_acc, p.ntx,
+                           bits, nWb, chunk, hdr, region, rstride);
     } else if (nb <= 4) {  // few buckets: long segments per region, a 16-lane group walks each
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_sum_g<16>),
