@@ -1,5 +1,5 @@
 #!/bin/bash
-# quick check: a subset of GPU tests (TESTS), then cfg2 / cfg3 bench traces. usage: tools/gpu_r6_quick.sh TAG "pytest args"
+# quick check: a subset of GPU tests, untraced bench lines (PLAIN) and bench kernel traces (TRACED, default cfg2 cfg3). usage: PLAIN="cfg..." TRACED="cfg..." tools/gpu_quick.sh TAG "pytest args"
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 o=gpurun_out/$1

@@ -1,7 +1,8 @@
 #!/bin/bash
-# A/B of the totals binning variants at cfg3 (development switches, SKQ_DEV=1): untraced bench
-# lines, then kernel-trace medians of the tail kernels.
-# usage: tools/gpu_bin_g.sh TAG "name:VAR=V,VAR=V name2:..."   (TRACE="name ..." to trace some)
+# Named variants of development switches (SKQ_DEV=1) in one process tree at cfg3: an untraced bench
+# line each, then kernel-trace medians of the map and the tail kernels for those named in TRACE
+# (round 6: the totals binning's grouping and the CU-masked side stream, profiles/r6_bin_group_ab.log).
+# usage: tools/gpu_variants.sh TAG "name:VAR=V,VAR=V name2:..."   (TRACE="name ..." to trace some)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 o=gpurun_out/$1; mkdir -p $o
