@@ -187,10 +187,12 @@ typedef struct {
     const uint64_t* tx_score; /* per transcript: sum of those reads' scores (accumulated)      */
     uint32_t hash_layout;     /* 0: padded rows, 1: per-wave packed (above)                     */
     uint32_t cand_layout;     /* 0: padded rows, 1: per-wave packed (above)                     */
-    /* (batches of 512k+ reads finish their totals on the session's own side stream, which the
-     * launch stream does not wait for: skq_session_results blocks the host until that work is
-     * done, so tx_reads / tx_score are current once the caller's stream is synchronized too;
-     * skq_session_totals waits for it on the caller's stream instead) */
+    /* (fused maps of 4M+ reads run their whole tail — slow paths and totals — on the session's
+     * own side stream, which the launch stream does not wait for: skq_session_results blocks the
+     * host until that work is done, and folds the batch's packed per-transcript sums into
+     * tx_reads / tx_score on the stream the last batch's tail ran on, so they are current once
+     * the caller's stream is synchronized; skq_session_totals waits for it all on the caller's
+     * stream instead) */
 } skq_results;
 int skq_session_results(skq_session* s, skq_results* out);
 

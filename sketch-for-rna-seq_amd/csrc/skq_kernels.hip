@@ -3319,8 +3319,9 @@ int launch_bin(const ChainParams& p, int binned, void* stream, bool beside_map) 
     }
     // the fused map's packed candidates: one binned region per four map workgroups (k_bin_packed<4096,
     // 4>), summed by k_bin_sum4 — against one per map workgroup, cfg3 9.50 -> 9.95 G reads/s on one
-    // box; three or eight per region, unstaged stores and 2^10-2^11-id buckets measured slower
-    // (profiles/r6_bin_group_ab.log)
+    // box; two, three or eight per region, unstaged stores and 2^10-2^11-id buckets measured slower,
+    // the forms small enough in LDS to run beside five map workgroups per CU too: their overlap
+    // slows the map more than it saves (profiles/r6_bin_group_ab.log)
     const bool grouped = !binned && p.cpack && nb > 4;
     const uint32_t nWb = grouped ? (nW + 3) / 4 : nW;  // (binned regions)
     const uint32_t rstride = WG * CCAP;                 // (words per binned region)
