@@ -370,11 +370,18 @@ def measure(cname, cfg, args, rank, world, dev, gpu, sample, totals_dev=True):
     log("%s setup %.1fs: %d transcripts, %d reads x %d bp, index %s" % (
         cname, time.time() - t0, tx.ntx, n, L, index.stats()))
 
+    # the collective's own stream: the step's totals are snapshotted on the session's tail stream
+    # and all-reduced there, so the next map on the launch stream does not wait for the tail or
+    # the all-reduce (the last step's all-reduce is inside the timed region: its synchronize)
+    comm = torch.cuda.Stream(dev) if world > 1 else None
+    cp_ = C.c_void_p(comm.cuda_stream) if comm is not None else None
+
     def step():
         sess.map(d_reads.data_ptr(), None, n, L, fixed_len=L, stream=sp)
         if world > 1:  # the one collective: per-transcript totals, summed over ranks (RCCL)
-            sess.totals_to_device(totals[0].data_ptr(), totals[1].data_ptr(), stream=sp)
-            sdist.allreduce_totals(totals)
+            with torch.cuda.stream(comm):
+                sess.totals_async(totals[0].data_ptr(), totals[1].data_ptr(), stream=cp_)
+                sdist.allreduce_totals(totals)
 
     if args.preheat == "matmul":  # ~100 ms of unrelated GPU work (clocks)
         x = torch.randn(8192, 8192, device=dev)

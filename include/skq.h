@@ -212,6 +212,12 @@ int skq_session_export(skq_session* s, uint8_t* status, uint64_t* hash_offs, uin
 /* Copy the per-transcript totals (ntx each) to host or device memory. */
 int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, int to_device,
                        void* stream);
+/* The same snapshot into device memory without holding `stream` behind the batch's tail: after
+ * `stream`'s work so far (the previous snapshot's consumer, e.g. an all-reduce), the totals are
+ * folded and copied on the stream the last batch's tail runs on, in order with the tails, and
+ * `stream` waits for the copy. The launch stream's next map does not wait for any of it (bench.py
+ * --gpus N: the per-step all-reduce of the totals overlaps the next map). */
+int skq_session_totals_async(skq_session* s, uint64_t* d_reads, uint64_t* d_score, void* stream);
 
 /* ---- FASTQ ingest on the GPU (process_fastq_single_pass's reader, src/main.cpp:113-148) ------
  * The FASTQ text itself goes to the device: a reader thread pulls the file into pinned staging

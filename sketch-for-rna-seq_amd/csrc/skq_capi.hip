@@ -184,7 +184,8 @@ struct skq_session {
     // batch has taken the other frame: zeroed[x])
     hipStream_t side = nullptr;
     hipEvent_t ev_fork{}, ev_map{}, ev_done[2]{};
-    hipStream_t last_st{};  // (the stream of the last batch's tail: where a results call folds the sums)  // (ev_map: bound to a side batch's map dispatch)
+    hipStream_t last_st{};
+    hipEvent_t ev_snap[2]{};  // (skq_session_totals_async: the consumer's work, the copy)  // (the stream of the last batch's tail: where a results call folds the sums)  // (ev_map: bound to a side batch's map dispatch)
     bool done_rec[2] = {false, false};
     bool zeroed[2] = {false, false};
     bool tail_side[2] = {false, false};  // the frame's batch ran its tail on the side stream
@@ -1312,6 +1313,8 @@ int skq_session_free(skq_session* s) {
         (void)hipEventDestroy(t.start);
         (void)hipEventDestroy(t.stop);
     }
+    if (s->ev_snap[0]) (void)hipEventDestroy(s->ev_snap[0]);
+    if (s->ev_snap[1]) (void)hipEventDestroy(s->ev_snap[1]);
     if (s->side) {
         (void)hipStreamSynchronize(s->side);
         (void)hipStreamDestroy(s->side);
@@ -2035,6 +2038,40 @@ int skq_session_totals(skq_session* s, uint64_t* tx_reads, uint64_t* tx_score, i
     if (tx_reads) HIP_TRY(hipMemcpyAsync(tx_reads, s->tx_reads, bytes, kind, st));
     if (tx_score) HIP_TRY(hipMemcpyAsync(tx_score, s->tx_score, bytes, kind, st));
     if (!to_device) HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int skq_session_totals_async(skq_session* s, uint64_t* d_reads, uint64_t* d_score, void* stream) {
+    if (!s || !d_reads || !d_score) return fail(-1, "null argument");
+    DeviceGuard g(s->idx->device);
+    hipStream_t cs = reinterpret_cast<hipStream_t>(stream);
+    // the stream of the last batch's tail: every earlier tail is ordered before it (a side batch's
+    // tail waits for the launch stream's earlier ones, a launch-stream batch for the side stream's)
+    hipStream_t ts = s->tail_side[s->fid] && s->side ? s->side : s->last_st;
+    if (!s->ev_snap[0]) {
+        HIP_TRY(hipEventCreateWithFlags(&s->ev_snap[0], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s->ev_snap[1], hipEventDisableTiming));
+    }
+    if (ts != cs) {
+        HIP_TRY(hipEventRecord(s->ev_snap[0], cs));
+        HIP_TRY(hipStreamWaitEvent(ts, s->ev_snap[0], 0));
+    }
+    if (s->acc_reads) {
+        if (skq::launch_fold_totals(s->tx_acc, s->tx_reads, s->tx_score, s->idx->ntx, ts)) return fail(-3, "fold failed");
+        s->acc_reads = 0;
+    }
+    const size_t bytes = s->idx->ntx * 8ull;
+    HIP_TRY(hipMemcpyAsync(d_reads, s->tx_reads, bytes, hipMemcpyDeviceToDevice, ts));
+    HIP_TRY(hipMemcpyAsync(d_score, s->tx_score, bytes, hipMemcpyDeviceToDevice, ts));
+    if (ts != cs) {
+        HIP_TRY(hipEventRecord(s->ev_snap[1], ts));
+        HIP_TRY(hipStreamWaitEvent(cs, s->ev_snap[1], 0));
+    }
+    if (s->side && ts == s->side) {  // (the frame's done event now follows the copy too: a later reset or
+        // results call waits for it)
+        HIP_TRY(hipEventRecord(s->ev_done[s->fid], s->side));
+        s->done_rec[s->fid] = true;
+    }
     return 0;
 }
 

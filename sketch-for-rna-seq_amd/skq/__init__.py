@@ -73,6 +73,7 @@ def lib():
             "skq_session_reset_totals": (i32, [vp, vp]),
             "skq_session_export": (i32, [vp] + [vp] * 6 + [C.POINTER(u64), C.POINTER(u64)]),
             "skq_session_totals": (i32, [vp, vp, vp, i32, vp]),
+            "skq_session_totals_async": (i32, [vp, vp, vp, vp]),
             "skq_malloc": (i32, [i32, C.c_size_t, C.POINTER(vp)]),
             "skq_free": (i32, [vp]),
             "skq_memcpy_h2d": (i32, [vp, vp, C.c_size_t, vp]),
@@ -307,6 +308,12 @@ class Session:
 
     def totals_to_device(self, d_reads_ptr, d_score_ptr, stream=None):
         _check(lib().skq_session_totals(self.h, d_reads_ptr, d_score_ptr, 1, stream))
+
+    def totals_async(self, d_reads_ptr, d_score_ptr, stream=None):
+        """The totals into device memory on the session's tail stream, after `stream`'s work so far,
+        with `stream` waiting for the copy (include/skq.h skq_session_totals_async): the next map
+        does not wait for it."""
+        _check(lib().skq_session_totals_async(self.h, d_reads_ptr, d_score_ptr, stream))
 
     def reset_totals(self, stream=None):
         _check(lib().skq_session_reset_totals(self.h, stream))
