@@ -1,5 +1,5 @@
 #!/bin/bash
-# Named variants of development switches (SKQ_DEV=1) in one process tree at cfg3: an untraced bench
+# Named variants of development switches (SKQ_DEV=1) at cfg3 (or CFG): an untraced bench
 # line each, then kernel-trace medians of the map and the tail kernels for those named in TRACE
 # (round 6: the totals binning's grouping and the CU-masked side stream, profiles/r6_bin_group_ab.log).
 # usage: tools/gpu_variants.sh TAG "name:VAR=V,VAR=V name2:..."   (TRACE="name ..." to trace some)
@@ -13,14 +13,14 @@ run() {  # name spec out [extra bench args]
 }
 for v in $2; do
   name=${v%%:*}; spec=${v#*:}
-  run $name "$spec" x timeout -k 10 200 python3 bench.py --config cfg3 --no-cpu-baseline --no-end-to-end > $o/$name.json 2> $o/$name.err || { echo "$name failed"; tail -5 $o/$name.err; exit 1; }
+  run $name "$spec" x timeout -k 10 200 python3 bench.py --config ${CFG:-cfg3} --no-cpu-baseline --no-end-to-end > $o/$name.json 2> $o/$name.err || { echo "$name failed"; tail -5 $o/$name.err; exit 1; }
   echo -n "$name: "; python3 tools/bench_summary.py $o/$name.json | head -1 | cut -c1-110
 done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for v in $2; do
   name=${v%%:*}; spec=${v#*:}
   case " ${TRACE:-} " in *" $name "*) ;; *) continue ;; esac
-  run $name "$spec" x timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d $o/tr_$name -o run -- python3 bench.py --config cfg3 --no-cpu-baseline --no-end-to-end --steps 10 > $o/t_$name.json 2> $o/t_$name.err || { echo "trace $name failed"; exit 1; }
+  run $name "$spec" x timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d $o/tr_$name -o run -- python3 bench.py --config ${CFG:-cfg3} --no-cpu-baseline --no-end-to-end --steps 10 > $o/t_$name.json 2> $o/t_$name.err || { echo "trace $name failed"; exit 1; }
   python3 - $o/tr_$name/run_kernel_trace.csv $name <<'PY'
 import csv, sys, statistics, collections
 d = collections.defaultdict(list)
