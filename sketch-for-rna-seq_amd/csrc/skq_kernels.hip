@@ -3202,7 +3202,8 @@ int launch_slow_wave(const SketchParams& p, const ChainParams& cp, uint32_t* ovf
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // a 64-lane workgroup per listed read, grid-stride (the list length is on the device); 16
     // per CU fit (LDS ~9 KB, < 100 VGPRs)
-    // (a small batch's few slow reads need fewer workgroups: an empty list still dispatches all)
+    // (a small batch's few slow reads need fewer workgroups: an empty list still dispatches all;
+    // at cfg3 a quarter or an eighth of the grid measured 0.5-1 % slower, profiles/r6_slow_wave_grid_ab.log)
     const dim3 grid((unsigned)std::min<uint64_t>(SW_GRID, std::max<uint64_t>(256, cp.n / 2048))), blk(64);
     const bool cmp = cp.wide == 3;
     switch (cp.nk) {
