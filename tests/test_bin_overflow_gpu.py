@@ -1,9 +1,11 @@
-"""The totals binning's rare paths (k_bin_packed<4096, 4>, launch_bin): a transcript set of groups
-of twelve near-copies, so every read lists ~12 candidates — a map wave's packed region then holds
-more than the 256 words loaded with the counts (the words past 256 are re-read per lane), and four
-map workgroups more than the 4096 words the staging holds (their candidates go straight into the
-totals with 64-bit atomics). > 32768 transcripts, so the totals take the grouped binning (5
-buckets of 2^13 ids). Per read (digest) and per transcript against the oracle."""
+"""The totals' rare paths: a transcript set of groups of twelve near-copies, so every read lists
+~12 candidates and a map wave's packed region holds more than the 256 words the totals kernels
+load in their first round (the words past 256 are read again per lane). 3,400 groups (40,800
+transcripts): the grouped binning (k_bin_packed<4096, 4>, 5 buckets of 2^13 ids), where four map
+workgroups also overflow the 4096-word staging (their candidates go straight into the totals with
+64-bit atomics). 1,000 groups (12,000 transcripts): k_tot_small, between the maps (300k reads) and
+beside the next map on the side stream (4.2M reads, 256-thread workgroups, 4096-id ranges). Per
+read (digest) and per transcript against the oracle."""
 import numpy as np
 import pytest
 import torch  # noqa: F401  (one HIP runtime per process)
@@ -15,10 +17,10 @@ from skq import synth
 
 pytestmark = pytest.mark.gpu
 
-L, N, COPIES, BASE = 150, 300_000, 12, 3_400
+L, COPIES = 150, 12
 
 
-def _copies_transcriptome(seed=71):
+def _copies_transcriptome(BASE, seed=71):
     rng = np.random.default_rng(seed)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     pieces, names = [], []
@@ -35,9 +37,12 @@ def _copies_transcriptome(seed=71):
     return synth.Transcriptome(np.concatenate(pieces), offs, names)
 
 
-def test_binning_overflow_paths_match_the_oracle():
-    tx = _copies_transcriptome()
-    assert tx.ntx > 32768
+@pytest.mark.parametrize("base,N,modes", [(3_400, 300_000, (False, True)), (1_000, 300_000, (False, True)),
+                                          (1_000, 4_200_000, (False,))],
+                         ids=["grouped-bins", "tot-small", "tot-small-side"])
+def test_binning_overflow_paths_match_the_oracle(base, N, modes):
+    tx = _copies_transcriptome(base)
+    assert (tx.ntx > 32768) == (base == 3_400) and (tx.ntx <= 16384) == (base == 1_000)
     ks = [31]
     tables = skq.build_tables(tx.seqs, tx.offs, ks, nthreads=16)
     keys, offs, tids = tables[31]
@@ -45,7 +50,7 @@ def test_binning_overflow_paths_match_the_oracle():
     bases, _, _ = synth.reads(tx, N, L, seed=72, err=0.001)
     cpu = orc.map_digest(oi, bases, L, nthreads=16)
     d = skq.DeviceBuffer.from_numpy(bases)
-    for chained in (False, True):
+    for chained in modes:
         index = skq.Index(ks, tx.ntx, tables, seqs=(tx.seqs, tx.offs) if chained else None)
         s = skq.Session(index, N, L)
         s.map(d.ptr, None, N, L, fixed_len=L)
