@@ -505,6 +505,45 @@ def test_repeated_batches_accumulate_totals(tx300, n, probe_mode):
         d.free()
 
 
+def test_mixed_batch_sizes_switch_streams(tx300, probe_mode):
+    """Batches of alternating size through one session, totals accumulated: 4.2M reads (tail on the
+    side stream, the other frame), 1000 (tail on the launch stream, after waiting for the side
+    stream), 4.2M (the fork behind a launch-stream tail), 600k, 4.2M, 4.2M. Each batch's results per
+    read right after it, and the running totals after each, against the oracle — the hand-offs
+    between the two streams and the two frames' control words in every order they occur."""
+    import digest
+    if probe_mode != "chain":
+        pytest.skip("the streams and frames once, over the default index kind")
+    gi, oi = build([31], tx=tx300)
+    sizes = [4_200_000, 1000, 4_200_000, 600_000, 4_200_000, 4_200_000]
+    s = skq.Session(gi, max(sizes), 150)
+    tr = np.zeros(tx300.ntx, np.uint64)
+    ts = np.zeros(tx300.ntx, np.uint64)
+    keep = []
+    for b, n in enumerate(sizes):
+        bases, _, _ = synth.reads(tx300, n, 150, seed=90 + b)
+        d = skq.DeviceBuffer.from_numpy(bases)
+        keep.append(d)
+        s.map(d.ptr, None, n, 150, fixed_len=150)
+        cpu = orc.map_digest(oi, bases, 150, nthreads=16)
+        tr += cpu["tx_reads"]
+        ts += cpu["tx_score"]
+        if b != 4:  # (batch 4's results are left unread: the next batch resets its frame behind its tail)
+            s.check()
+            dg = digest.export_digest(s.export(), 1)
+            bad = np.nonzero(dg != cpu["digest"])[0]
+            assert len(bad) == 0, "batch %d (%d reads): %d reads differ (first %s)" % (b, n, len(bad), bad[:8].tolist())
+            a, c = s.totals()
+            np.testing.assert_array_equal(a, tr, err_msg="after batch %d" % b)
+            np.testing.assert_array_equal(c, ts, err_msg="after batch %d" % b)
+    a, c = s.totals()
+    np.testing.assert_array_equal(a, tr)
+    np.testing.assert_array_equal(c, ts)
+    s.free()
+    for d in keep:
+        d.free()
+
+
 def test_very_long_reads_and_large_postings():
     # whole transcripts as reads (up to ~4 kb) plus 8-12 kb concatenations: the slow sketch path
     # beyond its LDS capacity and the slow chain path beyond LDS (global scratch)
