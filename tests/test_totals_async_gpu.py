@@ -48,3 +48,31 @@ def test_async_snapshots_scale_with_the_batches(setup, n):
     for k in range(3):
         np.testing.assert_array_equal(got[k], (k + 1) * got[0])
     np.testing.assert_array_equal(got[2], final)
+
+
+@pytest.mark.parametrize("n", [100_000, 4_200_000])
+def test_results_totals_are_current_after_the_stream(setup, n):
+    """skq_session_results folds the batch's packed sums on the stream of the last batch's tail
+    (include/skq.h): once that stream is synchronized, the device totals it points at equal
+    skq_session_totals' copy."""
+    tx, index = setup
+    bases, _, _ = synth.reads(tx, n, L, seed=63)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(bases).to(dev)
+    s = skq.Session(index, n, L)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(2):
+        s.map(d.data_ptr(), None, n, L, fixed_len=L, stream=sp, accumulate=True)
+    r = s.results()
+    torch.cuda.synchronize(dev)
+    got = []
+    for ptr in (r.tx_reads, r.tx_score):
+        h = np.zeros(tx.ntx, np.uint64)
+        assert skq.lib().skq_memcpy_d2h(h.ctypes.data, ptr, h.nbytes, None) == 0
+        got.append(h)
+    torch.cuda.synchronize(dev)
+    want = s.totals()
+    s.free()
+    assert got[0].sum() >= 2 * n
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1], want[1])
